@@ -1,0 +1,340 @@
+"""ctypes bindings for the parity oracle (TEST INFRASTRUCTURE ONLY).
+
+Two CPU libraries sit behind this module:
+
+* ``oracle/liboracle_sph.so`` -- the plain-C restatement (``sph_oracle.c``); always
+  buildable (``make -C oracle``); travels to the GPU box.
+* ``oracle/_ref/libsph_ref.so`` -- the reference's own USER-SPH compute code compiled from
+  /root/reference/src (``oracle/build_ref.sh``); exists only where it was built.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg import this.
+Nothing in the product package (``lammps-sph-multiphase_amd/``) may import it.
+
+Arrays follow LAMMPS conventions (see sph_oracle.h): x/v/vest/f are (n, 3) float64,
+per-type tables are length ntypes+1 and per-pair tables (ntypes+1, ntypes+1), 1-based.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle_sph.so")
+REF_SO = os.path.join(HERE, "_ref", "libsph_ref.so")
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_lp = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_i, _l, _d = C.c_int, C.c_long, C.c_double
+
+
+class OrcDomain(C.Structure):
+    _fields_ = [("dim", C.c_int), ("boxlo", C.c_double * 3), ("boxhi", C.c_double * 3),
+                ("periodic", C.c_int * 3)]
+
+
+def build_oracle() -> str:
+    src = os.path.join(HERE, "sph_oracle.c")
+    if (not os.path.exists(ORACLE_SO)) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE, "liboracle_sph.so"], check=True)
+    return ORACLE_SO
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = C.CDLL(build_oracle())
+        P = C.POINTER(OrcDomain)
+        L.orc_pbc.argtypes = [P, _i, _dp]
+        L.orc_borders.argtypes = [P, _d, _i, _dp, _ip, _i, _ip, _ip]
+        L.orc_borders.restype = _i
+        L.orc_forward_comm.argtypes = [P, _i, _i, _ip, _ip, _dp, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]
+        L.orc_reverse_comm.argtypes = [_i, _i, _ip, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_cutneighsq.argtypes = [_i, _dp, _d, _dp, C.POINTER(C.c_double)]
+        L.orc_neigh_full.argtypes = [_i, _i, _i, _dp, _ip, _i, _dp, _lp, C.c_void_p, _l]
+        L.orc_neigh_full.restype = _l
+        L.orc_neigh_half_from_full.argtypes = [_i, _dp, _lp, _ip, _lp, C.c_void_p]
+        L.orc_neigh_half_from_full.restype = _l
+        L.orc_rhosum.argtypes = [_i, _i, _dp, _ip, _i, _dp, _dp, _dp, _lp, _ip, _dp]
+        L.orc_taitwater.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp, _dp,
+                                    _dp, _dp, _dp, _lp, _ip, _dp, _dp, _dp, C.c_void_p]
+        L.orc_taitwater_morris.argtypes = L.orc_taitwater.argtypes
+        L.orc_heatconduction.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp,
+                                         _dp, _lp, _ip, _dp]
+        for n in ("orc_kernel_quintic2d", "orc_kernel_quintic3d", "orc_dw_quintic2d",
+                  "orc_dw_quintic3d"):
+            getattr(L, n).argtypes = [_d]
+            getattr(L, n).restype = _d
+        L.orc_rhosum_multiphase.argtypes = [_i, _i, _dp, _ip, _i, _dp, _dp, _dp, _lp, _ip,
+                                            _dp]
+        L.orc_taitwater_multiphase.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp,
+                                               _dp, _dp, _dp, _dp, _dp, _dp, _dp, _lp, _ip,
+                                               _dp]
+        L.orc_heatconduction_phasechange.argtypes = [_i, _i, _i, _dp, _dp, _dp, _dp, _dp,
+                                                     _ip, _i, _dp, C.c_void_p, C.c_void_p,
+                                                     _dp, _dp, _lp, _ip, _dp]
+        L.orc_colorgradient.argtypes = [_i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp, _lp,
+                                        _ip, _dp]
+        L.orc_meso_setup.argtypes = [_i, _dp, _dp]
+        L.orc_meso_initial.argtypes = [_i, _d, _d, _ip, _dp, C.c_void_p, _dp, _dp, _dp, _dp,
+                                       _dp, _dp, _dp, _dp]
+        L.orc_meso_final.argtypes = [_i, _d, _ip, _dp, C.c_void_p, _dp, _dp, _dp, _dp, _dp,
+                                     _dp]
+        _lib = L
+    return _lib
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def ref():
+    """The reference's own compute code (oracle/_ref), or None if it was not built."""
+    global _ref
+    if _ref is None and ref_available():
+        R = C.CDLL(REF_SO)
+        R.ref_neigh_full.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _dp, _dp, _d, _dp,
+                                     _lp, C.c_void_p, _l]
+        R.ref_neigh_full.restype = _l
+        R.ref_neigh_half_from_full.argtypes = [_i, _i, _dp, _lp, _ip, _lp, C.c_void_p]
+        R.ref_neigh_half_from_full.restype = _l
+        R.ref_rhosum.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
+        R.ref_taitwater.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _dp,
+                                    _dp, _dp, _lp, _ip, _dp, _dp, _dp]
+        R.ref_taitwater_morris.argtypes = R.ref_taitwater.argtypes
+        R.ref_heatconduction.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
+                                         _dp, _lp, _ip, _dp]
+        R.ref_rhosum_multiphase.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
+        R.ref_taitwater_multiphase.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp,
+                                               _dp, _dp, _dp, _dp, _dp, _dp, _lp, _ip, _dp]
+        R.ref_heatconduction_phasechange.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _dp,
+                                                     _dp, _ip, _dp, C.c_void_p, C.c_void_p,
+                                                     _dp, _lp, _ip, _dp]
+        R.ref_colorgradient.argtypes = [_i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _lp,
+                                        _ip, _dp]
+        for n in ("ref_kernel_quintic2d", "ref_kernel_quintic3d", "ref_dw_quintic2d",
+                  "ref_dw_quintic3d"):
+            getattr(R, n).argtypes = [_d]
+            getattr(R, n).restype = _d
+        _ref = R
+    return _ref
+
+
+# ---------------------------------------------------------------------------------------
+# System description
+# ---------------------------------------------------------------------------------------
+@dataclass
+class System:
+    """Owned particles of one periodic (or not) orthogonal box, LAMMPS atom_style meso."""
+
+    dim: int
+    boxlo: np.ndarray
+    boxhi: np.ndarray
+    periodic: tuple
+    x: np.ndarray            # (n,3)
+    v: np.ndarray            # (n,3)
+    type: np.ndarray         # (n,) int32, 1-based
+    rho: np.ndarray
+    e: np.ndarray
+    cv: np.ndarray
+    ntypes: int
+    mass: np.ndarray         # (ntypes+1,)
+    rmass: np.ndarray | None = None
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        return int(self.x.shape[0])
+
+    def domain(self) -> OrcDomain:
+        d = OrcDomain()
+        d.dim = self.dim
+        for k in range(3):
+            d.boxlo[k] = float(self.boxlo[k])
+            d.boxhi[k] = float(self.boxhi[k])
+            d.periodic[k] = int(self.periodic[k])
+        return d
+
+    def copy(self) -> "System":
+        s = System(self.dim, self.boxlo.copy(), self.boxhi.copy(), tuple(self.periodic),
+                   self.x.copy(), self.v.copy(), self.type.copy(), self.rho.copy(),
+                   self.e.copy(), self.cv.copy(), self.ntypes, self.mass.copy(),
+                   None if self.rmass is None else self.rmass.copy(), dict(self.extra))
+        return s
+
+
+def cubic_lattice(n: int, dx: float = 1.0, jitter: float = 0.1, seed: int = 12345,
+                  vel_sigma: float = 0.01, vseed: int = 4928459, ntypes: int = 1,
+                  type2_frac: float = 0.0, tseed: int = 87287, dim: int = 3,
+                  mass=(1.0,), rho=(1.0,), e=(0.0,), cv=(1.0,)) -> System:
+    """SURVEY.md section 8(d) synthetic boxes: sc lattice n^dim, spacing dx, periodic, every
+    coordinate jittered by U(-jitter, jitter)*dx, gaussian velocities; optional type 2 by
+    Bernoulli(type2_frac).  (numpy RNG -- not LAMMPS' RanPark -- the same arrays are fed
+    to every implementation under test.)"""
+    nz = n if dim == 3 else 1
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(nz), indexing="ij"),
+                 -1).reshape(-1, 3)
+    # LAMMPS create_atoms loops z outermost then y then x; order atoms the same way
+    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]
+    x = g.astype(np.float64) * dx
+    rng = np.random.default_rng(seed)
+    x += rng.uniform(-jitter, jitter, size=x.shape) * dx
+    if dim == 2:
+        x[:, 2] = 0.0
+    N = x.shape[0]
+    vr = np.random.default_rng(vseed)
+    v = vr.normal(0.0, vel_sigma, size=(N, 3))
+    if dim == 2:
+        v[:, 2] = 0.0
+    t = np.ones(N, dtype=np.int32)
+    if ntypes >= 2 and type2_frac > 0:
+        tr = np.random.default_rng(tseed)
+        t[tr.random(N) < type2_frac] = 2
+    mass_t = np.zeros(ntypes + 1)
+    rho_t = np.zeros(ntypes + 1)
+    e_t = np.zeros(ntypes + 1)
+    cv_t = np.zeros(ntypes + 1)
+    for k in range(1, ntypes + 1):
+        mass_t[k] = mass[min(k - 1, len(mass) - 1)]
+        rho_t[k] = rho[min(k - 1, len(rho) - 1)]
+        e_t[k] = e[min(k - 1, len(e) - 1)]
+        cv_t[k] = cv[min(k - 1, len(cv) - 1)]
+    boxlo = np.zeros(3)
+    boxhi = np.array([n * dx, n * dx, (n * dx) if dim == 3 else 0.5 * dx])
+    if dim == 2:
+        boxlo[2] = -0.5 * dx
+    return System(dim, boxlo, boxhi, (1, 1, 1 if dim == 3 else 0), x, v, t, rho_t[t].copy(),
+                  e_t[t].copy(), cv_t[t].copy(), ntypes, mass_t)
+
+
+# ---------------------------------------------------------------------------------------
+# Wrappers around the C restatement
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Ghosted:
+    """Owned + ghost atoms after CommBrick::borders (one process)."""
+
+    nlocal: int
+    nghost: int
+    x: np.ndarray            # (nall,3)
+    type: np.ndarray
+    owner: np.ndarray        # (nghost,)
+    image: np.ndarray        # (nghost,3)
+
+    @property
+    def nall(self) -> int:
+        return self.nlocal + self.nghost
+
+    def gather(self, a: np.ndarray) -> np.ndarray:
+        """Extend a per-owned array to owned+ghost by copying from owners."""
+        return np.concatenate([a, a[self.owner]], axis=0)
+
+
+def borders(sysm: System, cutghost: float, x: np.ndarray | None = None) -> Ghosted:
+    L = lib()
+    xo = sysm.x if x is None else x
+    n = xo.shape[0]
+    nmax = int(n * 3 + 1000)
+    while True:
+        xa = np.zeros((nmax, 3))
+        xa[:n] = xo
+        ta = np.zeros(nmax, dtype=np.int32)
+        ta[:n] = sysm.type
+        own = np.zeros(nmax, dtype=np.int32)
+        img = np.zeros(3 * nmax, dtype=np.int32)
+        d = sysm.domain()
+        ng = L.orc_borders(C.byref(d), cutghost, n, xa, ta, nmax, own, img)
+        if ng >= 0:
+            break
+        nmax *= 2
+    return Ghosted(n, ng, xa[:n + ng].copy(), ta[:n + ng].copy(), own[:ng].copy(),
+                   img[:3 * ng].reshape(-1, 3).copy())
+
+
+def cutneighsq(ntypes: int, cutmax: np.ndarray, skin: float):
+    out = np.zeros((ntypes + 1, ntypes + 1))
+    cm = C.c_double()
+    lib().orc_cutneighsq(ntypes, np.ascontiguousarray(cutmax, dtype=np.float64), skin, out,
+                         C.byref(cm))
+    return out, cm.value
+
+
+def neigh_full(dim: int, g: Ghosted, ntypes: int, cns: np.ndarray):
+    L = lib()
+    off = np.zeros(g.nlocal + 1, dtype=np.int64)
+    tot = L.orc_neigh_full(dim, g.nlocal, g.nall, g.x, g.type, ntypes, cns, off, None, 0)
+    neigh = np.zeros(max(tot, 1), dtype=np.int32)
+    tot2 = L.orc_neigh_full(dim, g.nlocal, g.nall, g.x, g.type, ntypes, cns, off,
+                            neigh.ctypes.data, tot)
+    assert tot2 == tot
+    return off, neigh[:tot]
+
+
+def half_from_full(g: Ghosted, foff: np.ndarray, fneigh: np.ndarray):
+    L = lib()
+    hoff = np.zeros(g.nlocal + 1, dtype=np.int64)
+    fn = np.ascontiguousarray(fneigh if fneigh.size else np.zeros(1, np.int32))
+    tot = L.orc_neigh_half_from_full(g.nlocal, g.x, foff, fn, hoff, None)
+    h = np.zeros(max(tot, 1), dtype=np.int32)
+    L.orc_neigh_half_from_full(g.nlocal, g.x, foff, fn, hoff, h.ctypes.data)
+    return hoff, h[:tot]
+
+
+def _nz(a):
+    return a if a.size else np.zeros(1, dtype=a.dtype)
+
+
+def rhosum(dim, g: Ghosted, ntypes, mass, cut, off, neigh):
+    cut = np.ascontiguousarray(cut, dtype=np.float64)
+    cutsq = cut * cut
+    rho = np.zeros(g.nall)
+    lib().orc_rhosum(dim, g.nlocal, g.x, g.type, ntypes, mass, cut, cutsq, off, _nz(neigh),
+                     rho)
+    return rho[:g.nlocal]
+
+
+def taitwater(dim, g: Ghosted, ntypes, newton, vest_all, rho_all, mass, rho0, c0, visc,
+              cut, off, neigh, morris=False, B=None, virial=False):
+    cut = np.ascontiguousarray(cut, dtype=np.float64)
+    cutsq = cut * cut
+    if B is None:
+        B = c0 * c0 * rho0 / 7.0
+    f = np.zeros((g.nall, 3))
+    drho = np.zeros(g.nall)
+    de = np.zeros(g.nall)
+    vir = np.zeros(6)
+    fn = lib().orc_taitwater_morris if morris else lib().orc_taitwater
+    fn(dim, g.nlocal, newton, g.x, np.ascontiguousarray(vest_all), np.ascontiguousarray(rho_all),
+       g.type, ntypes, mass, rho0, c0, np.ascontiguousarray(B, dtype=np.float64),
+       np.ascontiguousarray(visc, dtype=np.float64), cut, cutsq, off, _nz(neigh), f, drho, de,
+       vir.ctypes.data if virial else None)
+    if virial:
+        return f, drho, de, vir
+    return f, drho, de
+
+
+def heatconduction(dim, g: Ghosted, ntypes, newton, e_all, rho_all, mass, alpha, cut, off,
+                   neigh):
+    cut = np.ascontiguousarray(cut, dtype=np.float64)
+    de = np.zeros(g.nall)
+    lib().orc_heatconduction(dim, g.nlocal, newton, g.x, np.ascontiguousarray(e_all),
+                             np.ascontiguousarray(rho_all), g.type, ntypes, mass,
+                             np.ascontiguousarray(alpha, dtype=np.float64), cut, cut * cut,
+                             off, _nz(neigh), de)
+    return de
+
+
+def reverse_comm(g: Ghosted, f=None, drho=None, de=None):
+    lib().orc_reverse_comm(g.nlocal, g.nghost, g.owner if g.nghost else np.zeros(1, np.int32),
+                           None if f is None else f.ctypes.data,
+                           None if drho is None else drho.ctypes.data,
+                           None if de is None else de.ctypes.data)

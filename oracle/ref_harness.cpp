@@ -1,0 +1,582 @@
+// ref_harness.cpp -- drives the REFERENCE's own USER-SPH compute code (compiled from
+// /root/reference/src by oracle/build_ref.sh into oracle/_ref/libsph_ref.so).
+// TEST INFRASTRUCTURE ONLY: used to pin the C restatement (sph_oracle.c) and to
+// generate tests/golden fixtures.  Never part of the product.
+//
+// What runs is reference code, unmodified:
+//   Neighbor::setup_bins/stencil_full_bin_{2d,3d}/bin_atoms/full_bin  (neighbor.cpp,
+//     neigh_stencil.cpp, neigh_full.cpp)  and  Neighbor::half_from_full_newton
+//     (neigh_derive.cpp:83-150)
+//   PairSPH{RhoSum,Taitwater,TaitwaterMorris,HeatConduction,RhoSumMultiphase,
+//     TaitwaterMultiphase,HeatConductionPhaseChange,ColorGradient}::compute, ::init_one
+//     and Pair::init (pair.cpp:174-229)
+//   AtomVecMeso{,Multiphase}::grow for the per-atom arrays.
+// The LAMMPS top-level object, Atom, Domain, Force and Update are not constructed
+// (their translation units need generated style_*.h headers, which we do not create);
+// this harness zero-allocates those objects and fills only the fields the code above
+// reads.  Coefficients are written straight into the pair's tables because
+// Pair*::coeff() parses strings through Force (force.cpp), which is not built; the
+// formulas applied are the coeff() ones (cited below).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <new>
+
+#include "mpi.h"
+#include "lammps.h"
+#include "memory.h"
+#include "error.h"
+#include "atom.h"
+#include "atom_vec_meso.h"
+#include "atom_vec_meso_multiphase.h"
+#include "domain.h"
+#include "force.h"
+#include "update.h"
+#include "comm_brick.h"
+#include "neighbor.h"
+#include "neigh_list.h"
+#include "neigh_request.h"
+#include "pair_sph_rhosum.h"
+#include "pair_sph_taitwater.h"
+#include "pair_sph_taitwater_morris.h"
+#include "pair_sph_heatconduction.h"
+#include "pair_sph_rhosum_multiphase.h"
+#include "pair_sph_taitwater_multiphase.h"
+#include "pair_sph_heatconduction_phasechange.h"
+#include "pair_sph_colorgradient.h"
+
+using namespace LAMMPS_NS;
+
+namespace {
+
+template <class T> T *zalloc() { return static_cast<T *>(calloc(1, sizeof(T))); }
+
+struct HNeighbor : public Neighbor {
+  HNeighbor(LAMMPS *l) : Neighbor(l) {}
+  using Neighbor::bboxlo;
+  using Neighbor::bboxhi;
+  using Neighbor::triclinic;
+  using Neighbor::bin_atoms;
+  using Neighbor::full_bin;
+  using Neighbor::half_from_full_newton;
+  using Neighbor::stencil_full_bin_2d;
+  using Neighbor::stencil_full_bin_3d;
+  using Neighbor::sx;
+  using Neighbor::sy;
+  using Neighbor::sz;
+  using Neighbor::smax;
+  using Neighbor::dimension;
+  using Neighbor::exclude;
+  using Neighbor::mbins;
+  using Neighbor::maxbin;
+  using Neighbor::cutneighsq;
+  using Neighbor::bins;
+  using Neighbor::cutneighmaxsq;
+};
+
+struct HComm : public CommBrick {
+  HComm(LAMMPS *l) : CommBrick(l) { nswap = 0; }
+};
+
+struct HRhoSum : public PairSPHRhoSum {
+  HRhoSum(LAMMPS *l) : PairSPHRhoSum(l) {}
+  using PairSPHRhoSum::allocate;
+  using PairSPHRhoSum::cut;
+  using PairSPHRhoSum::nstep;
+};
+struct HTait : public PairSPHTaitwater {
+  HTait(LAMMPS *l) : PairSPHTaitwater(l) {}
+  using PairSPHTaitwater::allocate;
+  using PairSPHTaitwater::cut;
+  using PairSPHTaitwater::rho0;
+  using PairSPHTaitwater::soundspeed;
+  using PairSPHTaitwater::B;
+  using PairSPHTaitwater::viscosity;
+};
+struct HMorris : public PairSPHTaitwaterMorris {
+  HMorris(LAMMPS *l) : PairSPHTaitwaterMorris(l) {}
+  using PairSPHTaitwaterMorris::allocate;
+  using PairSPHTaitwaterMorris::cut;
+  using PairSPHTaitwaterMorris::rho0;
+  using PairSPHTaitwaterMorris::soundspeed;
+  using PairSPHTaitwaterMorris::B;
+  using PairSPHTaitwaterMorris::viscosity;
+};
+struct HHeat : public PairSPHHeatConduction {
+  HHeat(LAMMPS *l) : PairSPHHeatConduction(l) {}
+  using PairSPHHeatConduction::allocate;
+  using PairSPHHeatConduction::cut;
+  using PairSPHHeatConduction::alpha;
+};
+struct HRhoMP : public PairSPHRhoSumMultiphase {
+  HRhoMP(LAMMPS *l) : PairSPHRhoSumMultiphase(l) {}
+  using PairSPHRhoSumMultiphase::allocate;
+  using PairSPHRhoSumMultiphase::cut;
+  using PairSPHRhoSumMultiphase::nstep;
+};
+struct HTaitMP : public PairSPHTaitwaterMultiphase {
+  HTaitMP(LAMMPS *l) : PairSPHTaitwaterMultiphase(l) {}
+  using PairSPHTaitwaterMultiphase::allocate;
+  using PairSPHTaitwaterMultiphase::cut;
+  using PairSPHTaitwaterMultiphase::rho0;
+  using PairSPHTaitwaterMultiphase::soundspeed;
+  using PairSPHTaitwaterMultiphase::B;
+  using PairSPHTaitwaterMultiphase::gamma;
+  using PairSPHTaitwaterMultiphase::rbackground;
+  using PairSPHTaitwaterMultiphase::viscosity;
+};
+struct HHeatPC : public PairSPHHeatConductionPhaseChange {
+  HHeatPC(LAMMPS *l) : PairSPHHeatConductionPhaseChange(l) {}
+  using PairSPHHeatConductionPhaseChange::allocate;
+  using PairSPHHeatConductionPhaseChange::cut;
+  using PairSPHHeatConductionPhaseChange::alpha;
+  using PairSPHHeatConductionPhaseChange::fixflag;
+  using PairSPHHeatConductionPhaseChange::tc;
+};
+struct HCG : public PairSPHColorGradient {
+  HCG(LAMMPS *l) : PairSPHColorGradient(l) {}
+  using PairSPHColorGradient::allocate;
+  using PairSPHColorGradient::cut;
+  using PairSPHColorGradient::alpha;
+  using PairSPHColorGradient::nstep;
+};
+
+// One self-contained "LAMMPS" universe per call: owned atoms + ghosts supplied by the
+// caller (positions already imaged), newton_pair as given.
+struct World {
+  LAMMPS *lmp;
+  HComm *comm;
+  HNeighbor *neigh;
+  AtomVec *avec;
+  int nall;
+
+  World(int dim, int ntypes, int nlocal, int nghost, int newton, int multiphase) {
+    lmp = zalloc<LAMMPS>();
+    lmp->world = MPI_COMM_WORLD;
+    lmp->screen = NULL;
+    lmp->logfile = NULL;
+    lmp->memory = new Memory(lmp);
+    lmp->error = new Error(lmp);
+    lmp->atom = zalloc<Atom>();
+    lmp->domain = zalloc<Domain>();
+    lmp->force = zalloc<Force>();
+    lmp->update = zalloc<Update>();
+    lmp->domain->dimension = dim;
+    lmp->domain->triclinic = 0;
+    lmp->force->newton_pair = newton;
+    lmp->force->newton = newton;
+    lmp->update->ntimestep = 0;
+    comm = new HComm(lmp);
+    lmp->comm = comm;
+    neigh = new HNeighbor(lmp);
+    lmp->neighbor = neigh;
+    Atom *atom = lmp->atom;
+    atom->ntypes = ntypes;
+    atom->nlocal = nlocal;
+    atom->nghost = nghost;
+    nall = nlocal + nghost;
+    if (multiphase)
+      avec = new AtomVecMesoMultiPhase(lmp);
+    else
+      avec = new AtomVecMeso(lmp);
+    atom->avec = avec;
+    avec->grow(nall > 0 ? nall : 1);
+    atom->mass = (double *)calloc(ntypes + 1, sizeof(double));
+    atom->rmass_flag = multiphase;
+  }
+};
+
+void fill_atoms(World &w, const double *x, const double *vest, const double *rho,
+                const double *e, const double *cv, const int *type, const double *rmass) {
+  Atom *a = w.lmp->atom;
+  for (int i = 0; i < w.nall; i++) {
+    for (int k = 0; k < 3; k++) {
+      a->x[i][k] = x[3 * i + k];
+      a->f[i][k] = 0.0;
+      if (a->vest) a->vest[i][k] = vest ? vest[3 * i + k] : 0.0;
+      if (a->v) a->v[i][k] = vest ? vest[3 * i + k] : 0.0;
+    }
+    a->type[i] = type[i];
+    a->mask[i] = 1;
+    if (a->rho) a->rho[i] = rho ? rho[i] : 0.0;
+    if (a->drho) a->drho[i] = 0.0;
+    if (a->e) a->e[i] = e ? e[i] : 0.0;
+    if (a->de) a->de[i] = 0.0;
+    if (a->cv) a->cv[i] = cv ? cv[i] : 0.0;
+    if (a->rmass && rmass) a->rmass[i] = rmass[i];
+  }
+}
+
+// Build a NeighList from caller CSR (owned atoms, ilist = identity).
+NeighList *make_list(World &w, int nlocal, const long *off, const int *neigh) {
+  NeighList *l = new NeighList(w.lmp);
+  l->inum = nlocal;
+  l->gnum = 0;
+  l->ilist = (int *)malloc(sizeof(int) * (nlocal > 0 ? nlocal : 1));
+  l->numneigh = (int *)malloc(sizeof(int) * (nlocal > 0 ? nlocal : 1));
+  l->firstneigh = (int **)malloc(sizeof(int *) * (nlocal > 0 ? nlocal : 1));
+  for (int i = 0; i < nlocal; i++) {
+    l->ilist[i] = i;
+    l->numneigh[i] = (int)(off[i + 1] - off[i]);
+    l->firstneigh[i] = const_cast<int *>(neigh) + off[i];
+  }
+  return l;
+}
+
+void free_list(NeighList *l) {
+  free(l->ilist);
+  free(l->numneigh);
+  free(l->firstneigh);
+  l->ilist = NULL;
+  l->numneigh = NULL;
+  l->firstneigh = NULL;
+}
+
+// Pair::init (pair.cpp:174-229) minus init_style (no neighbor request machinery here):
+// cutsq[i][j] = cutsq[j][i] = cut*cut with cut = init_one(i,j).
+void pair_init_cutsq(Pair *p, int ntypes) {
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      double cut = p->init_one(i, j);
+      p->cutsq[i][j] = p->cutsq[j][i] = cut * cut;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Full list by the reference's own binned builder.  x holds nlocal owned + nghost ghost
+// atoms.  cutneighsq is (nt+1)^2.  On return off[0..nlocal], neigh[] (cap entries).
+long ref_neigh_full(int dim, int ntypes, int nlocal, int nghost, const double *x,
+                    const int *type, const double *boxlo, const double *boxhi,
+                    const double *sublo, const double *subhi, double cutghost,
+                    const double *cutneighsq, long *off, int *neigh, long cap) {
+  World w(dim, ntypes, nlocal, nghost, 1, 0);
+  fill_atoms(w, x, NULL, NULL, NULL, NULL, type, NULL);
+  Domain *d = w.lmp->domain;
+  for (int k = 0; k < 3; k++) {
+    d->boxlo[k] = boxlo[k];
+    d->boxhi[k] = boxhi[k];
+    d->sublo[k] = sublo[k];
+    d->subhi[k] = subhi[k];
+    d->prd[k] = boxhi[k] - boxlo[k];
+    w.comm->cutghost[k] = cutghost;
+  }
+  HNeighbor *n = w.neigh;
+  n->dimension = dim;
+  n->triclinic = 0;
+  n->exclude = 0;
+  n->bboxlo = d->boxlo;
+  n->bboxhi = d->boxhi;
+  w.lmp->memory->create(n->cutneighsq, ntypes + 1, ntypes + 1, "neigh:cutneighsq");
+  double cmax = 0.0;
+  for (int i = 0; i <= ntypes; i++)
+    for (int j = 0; j <= ntypes; j++) {
+      n->cutneighsq[i][j] = cutneighsq[i * (ntypes + 1) + j];
+      if (i && j) cmax = fmax(cmax, sqrt(cutneighsq[i * (ntypes + 1) + j]));
+    }
+  n->cutneighmax = cmax;
+  n->cutneighmaxsq = cmax * cmax;  // Neighbor::init, neighbor.cpp:280
+  n->setup_bins();
+  // Neighbor::build, neighbor.cpp:1477-1481: bins sized to atom->nmax
+  n->maxbin = w.lmp->atom->nmax;
+  w.lmp->memory->create(n->bins, n->maxbin, "bins");
+  NeighList *l = new NeighList(w.lmp);
+  l->setup_pages(100000, 2000, 0);
+  l->grow(nlocal + nghost + 1);
+  l->stencil_allocate(n->smax, 1 /*BIN: enum{NSQ,BIN,MULTI}, neigh_list.cpp:28*/);
+  if (dim == 3)
+    n->stencil_full_bin_3d(l, n->sx, n->sy, n->sz);
+  else
+    n->stencil_full_bin_2d(l, n->sx, n->sy, n->sz);
+  n->full_bin(l);  // bins atoms itself (binatomflag = 1)
+  long tot = 0;
+  for (int ii = 0; ii < l->inum; ii++) {
+    int i = l->ilist[ii];
+    off[i] = tot;
+    tot += l->numneigh[i];
+  }
+  off[nlocal] = tot;
+  if (neigh) {
+    if (tot > cap) return -1;
+    for (int ii = 0; ii < l->inum; ii++) {
+      int i = l->ilist[ii];
+      memcpy(neigh + off[i], l->firstneigh[i], sizeof(int) * l->numneigh[i]);
+    }
+  }
+  return tot;
+}
+
+// Neighbor::half_from_full_newton on a caller full list.
+long ref_neigh_half_from_full(int nlocal, int nghost, const double *x, const long *foff,
+                              const int *fneigh, long *hoff, int *hneigh) {
+  World w(3, 1, nlocal, nghost, 1, 0);
+  int *type = (int *)calloc(nlocal + nghost + 1, sizeof(int));
+  for (int i = 0; i < nlocal + nghost; i++) type[i] = 1;
+  fill_atoms(w, x, NULL, NULL, NULL, NULL, type, NULL);
+  free(type);
+  NeighList *full = make_list(w, nlocal, foff, fneigh);
+  NeighList *half = new NeighList(w.lmp);
+  half->setup_pages(100000, 2000, 0);
+  half->grow(nlocal + nghost + 1);
+  half->listfull = full;
+  w.neigh->half_from_full_newton(half);
+  long tot = 0;
+  for (int ii = 0; ii < half->inum; ii++) {
+    int i = half->ilist[ii];
+    hoff[i] = tot;
+    if (hneigh) memcpy(hneigh + tot, half->firstneigh[i], sizeof(int) * half->numneigh[i]);
+    tot += half->numneigh[i];
+  }
+  hoff[nlocal] = tot;
+  free_list(full);
+  return tot;
+}
+
+// PairSPHRhoSum: coeff semantics pair_sph_rhosum.cpp:239-263 (cut[i][j] = h, j>=i).
+// rho is nall long; owned entries are written; ghosts untouched (forward comm is the
+// caller's job -- nswap = 0 here).
+int ref_rhosum(int dim, int ntypes, int nlocal, int nghost, const double *x,
+               const int *type, const double *mass, const double *cut, const long *off,
+               const int *neigh, double *rho) {
+  World w(dim, ntypes, nlocal, nghost, 1, 0);
+  fill_atoms(w, x, NULL, rho, NULL, NULL, type, NULL);
+  for (int t = 0; t <= ntypes; t++) w.lmp->atom->mass[t] = mass[t];
+  HRhoSum *p = new HRhoSum(w.lmp);
+  p->nstep = 1;
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal; i++) rho[i] = w.lmp->atom->rho[i];
+  free_list(l);
+  return 0;
+}
+
+// PairSPHTaitwater / Morris: coeff semantics pair_sph_taitwater.cpp:238-276 including the
+// per-type "last write wins" of rho0/c0/B; here the caller passes per-type rho0/c0 and
+// per-pair visc/cut (j>=i), and B = c0^2 rho0 / 7 as coeff() computes it.
+static int run_tait(int morris, int dim, int ntypes, int nlocal, int nghost, int newton,
+                    const double *x, const double *vest, const double *rho, const int *type,
+                    const double *mass, const double *rho0, const double *c0,
+                    const double *visc, const double *cut, const long *off,
+                    const int *neigh, double *f, double *drho, double *de) {
+  World w(dim, ntypes, nlocal, nghost, newton, 0);
+  fill_atoms(w, x, vest, rho, NULL, NULL, type, NULL);
+  for (int t = 0; t <= ntypes; t++) w.lmp->atom->mass[t] = mass[t];
+  Pair *p;
+  if (morris) {
+    HMorris *q = new HMorris(w.lmp);
+    q->allocate();
+    for (int i = 1; i <= ntypes; i++) {
+      q->rho0[i] = rho0[i];
+      q->soundspeed[i] = c0[i];
+      q->B[i] = c0[i] * c0[i] * rho0[i] / 7.0;
+      for (int j = i; j <= ntypes; j++) {
+        q->viscosity[i][j] = visc[i * (ntypes + 1) + j];
+        q->cut[i][j] = cut[i * (ntypes + 1) + j];
+        q->setflag[i][j] = 1;
+      }
+    }
+    p = q;
+  } else {
+    HTait *q = new HTait(w.lmp);
+    q->allocate();
+    for (int i = 1; i <= ntypes; i++) {
+      q->rho0[i] = rho0[i];
+      q->soundspeed[i] = c0[i];
+      q->B[i] = c0[i] * c0[i] * rho0[i] / 7.0;
+      for (int j = i; j <= ntypes; j++) {
+        q->viscosity[i][j] = visc[i * (ntypes + 1) + j];
+        q->cut[i][j] = cut[i * (ntypes + 1) + j];
+        q->setflag[i][j] = 1;
+      }
+    }
+    p = q;
+  }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  Atom *a = w.lmp->atom;
+  for (int i = 0; i < nlocal + nghost; i++) {
+    for (int k = 0; k < 3; k++) f[3 * i + k] = a->f[i][k];
+    drho[i] = a->drho[i];
+    de[i] = a->de[i];
+  }
+  free_list(l);
+  return 0;
+}
+
+int ref_taitwater(int dim, int ntypes, int nlocal, int nghost, int newton, const double *x,
+                  const double *vest, const double *rho, const int *type, const double *mass,
+                  const double *rho0, const double *c0, const double *visc,
+                  const double *cut, const long *off, const int *neigh, double *f,
+                  double *drho, double *de) {
+  return run_tait(0, dim, ntypes, nlocal, nghost, newton, x, vest, rho, type, mass, rho0, c0,
+                  visc, cut, off, neigh, f, drho, de);
+}
+
+int ref_taitwater_morris(int dim, int ntypes, int nlocal, int nghost, int newton,
+                         const double *x, const double *vest, const double *rho,
+                         const int *type, const double *mass, const double *rho0,
+                         const double *c0, const double *visc, const double *cut,
+                         const long *off, const int *neigh, double *f, double *drho,
+                         double *de) {
+  return run_tait(1, dim, ntypes, nlocal, nghost, newton, x, vest, rho, type, mass, rho0, c0,
+                  visc, cut, off, neigh, f, drho, de);
+}
+
+// PairSPHHeatConduction: coeff pair_sph_heatconduction.cpp:(alpha, cut) for j>=i.
+int ref_heatconduction(int dim, int ntypes, int nlocal, int nghost, int newton,
+                       const double *x, const double *e, const double *rho, const int *type,
+                       const double *mass, const double *alpha, const double *cut,
+                       const long *off, const int *neigh, double *de) {
+  World w(dim, ntypes, nlocal, nghost, newton, 0);
+  fill_atoms(w, x, NULL, rho, e, NULL, type, NULL);
+  for (int t = 0; t <= ntypes; t++) w.lmp->atom->mass[t] = mass[t];
+  HHeat *p = new HHeat(w.lmp);
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->alpha[i][j] = alpha[i * (ntypes + 1) + j];
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal + nghost; i++) de[i] = w.lmp->atom->de[i];
+  free_list(l);
+  return 0;
+}
+
+// ---- multiphase styles (atom_style meso/multiphase: per-atom rmass) -------------------
+
+int ref_rhosum_multiphase(int dim, int ntypes, int nlocal, int nghost, const double *x,
+                          const int *type, const double *rmass, const double *cut,
+                          const long *off, const int *neigh, double *rho) {
+  World w(dim, ntypes, nlocal, nghost, 1, 1);
+  fill_atoms(w, x, NULL, rho, NULL, NULL, type, rmass);
+  HRhoMP *p = new HRhoMP(w.lmp);
+  p->nstep = 1;
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal; i++) rho[i] = w.lmp->atom->rho[i];
+  free_list(l);
+  return 0;
+}
+
+// coeff: pair_sph_taitwater_multiphase.cpp:225-262 (B = c^2 rho0 / gamma).
+int ref_taitwater_multiphase(int dim, int ntypes, int nlocal, int nghost, int newton,
+                             const double *x, const double *vest, const double *rho,
+                             const int *type, const double *rmass, const double *rho0,
+                             const double *c0, const double *gamma, const double *rbg,
+                             const double *visc, const double *cut, const long *off,
+                             const int *neigh, double *f) {
+  World w(dim, ntypes, nlocal, nghost, newton, 1);
+  fill_atoms(w, x, vest, rho, NULL, NULL, type, rmass);
+  HTaitMP *p = new HTaitMP(w.lmp);
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++) {
+    p->rho0[i] = rho0[i];
+    p->gamma[i] = gamma[i];
+    p->soundspeed[i] = c0[i];
+    p->B[i] = c0[i] * c0[i] * rho0[i] / gamma[i];
+    p->rbackground[i] = rbg[i];
+    for (int j = i; j <= ntypes; j++) {
+      p->viscosity[i][j] = visc[i * (ntypes + 1) + j];
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal + nghost; i++)
+    for (int k = 0; k < 3; k++) f[3 * i + k] = w.lmp->atom->f[i][k];
+  free_list(l);
+  return 0;
+}
+
+// coeff: pair_sph_heatconduction_phasechange.cpp:177-225.  fixflag/tc per pair (j>=i),
+// 0 meaning "no clamp" (the 4-arg form leaves them uninitialised: quirk A.6-4).
+int ref_heatconduction_phasechange(int dim, int ntypes, int nlocal, int nghost, int newton,
+                                   const double *x, const double *e, const double *cv,
+                                   const double *rho, const double *rmass, const int *type,
+                                   const double *alpha, const int *fixflag,
+                                   const double *tc, const double *cut, const long *off,
+                                   const int *neigh, double *de) {
+  World w(dim, ntypes, nlocal, nghost, newton, 1);
+  fill_atoms(w, x, NULL, rho, e, cv, type, rmass);
+  HHeatPC *p = new HHeatPC(w.lmp);
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->alpha[i][j] = alpha[i * (ntypes + 1) + j];
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->fixflag[i][j] = fixflag ? fixflag[i * (ntypes + 1) + j] : 0;
+      p->tc[i][j] = tc ? tc[i * (ntypes + 1) + j] : 0.0;
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal + nghost; i++) de[i] = w.lmp->atom->de[i];
+  free_list(l);
+  return 0;
+}
+
+int ref_colorgradient(int dim, int ntypes, int nlocal, int nghost, const double *x,
+                      const double *rho, const double *rmass, const int *type,
+                      const double *alpha, const double *cut, const long *off,
+                      const int *neigh, double *cg) {
+  World w(dim, ntypes, nlocal, nghost, 1, 1);
+  fill_atoms(w, x, NULL, rho, NULL, NULL, type, rmass);
+  HCG *p = new HCG(w.lmp);
+  p->nstep = 1;
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->alpha[i][j] = alpha[i * (ntypes + 1) + j];
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal; i++)
+    for (int k = 0; k < 3; k++) cg[3 * i + k] = w.lmp->atom->colorgradient[i][k];
+  free_list(l);
+  return 0;
+}
+
+double ref_kernel_quintic3d(double r);
+double ref_dw_quintic3d(double r);
+}
+
+#include "sph_kernel_quintic.h"
+extern "C" double ref_kernel_quintic3d(double r) { return sph_kernel_quintic3d(r); }
+extern "C" double ref_dw_quintic3d(double r) { return sph_dw_quintic3d(r); }
+extern "C" double ref_kernel_quintic2d(double r) { return sph_kernel_quintic2d(r); }
+extern "C" double ref_dw_quintic2d(double r) { return sph_dw_quintic2d(r); }

@@ -1,0 +1,200 @@
+/*
+ * sph_hip.h -- C ABI of the MI355X-native USER-SPH pair engine (libsph_hip.so).
+ *
+ * Two layers, both plain C (pointers + sizes, no torch/HIP types):
+ *
+ *  1. Pair-style layer (sph_hip_*): what a LAMMPS `sph/<style>/hip` Pair class calls from
+ *     its compute(), with LAMMPS' own host arrays and NeighList.  Replaces the CPU loops of
+ *       PairSPHRhoSum::compute          src/USER-SPH/pair_sph_rhosum.cpp:66-204
+ *       PairSPHTaitwater::compute       src/USER-SPH/pair_sph_taitwater.cpp:53-200
+ *       PairSPHTaitwaterMorris::compute src/USER-SPH/pair_sph_taitwater_morris.cpp:52-200
+ *       PairSPHHeatConduction::compute  src/USER-SPH/pair_sph_heatconduction.cpp:47-134
+ *     (paths relative to the reference tree).  Coefficients follow each style's coeff() /
+ *     init_one() semantics (tables already filled and symmetrised by LAMMPS).
+ *
+ *  2. Device-resident engine (sph_engine_*): the whole Verlet step of an SPH run
+ *     (FixMeso integrate, pbc, borders/ghost images, binned neighbor build, rhosum ->
+ *     forward comm -> taitwater[/morris] [+heatconduction], integrate) kept in HBM,
+ *     optionally sharded over several GPUs by brick decomposition with the halo carried on
+ *     RCCL.  Replaces, for device-resident runs, Verlet::run (src/verlet.cpp:207-309)
+ *     around the same pair styles; Neighbor::full_bin (src/neigh_full.cpp:241-344);
+ *     CommBrick::borders/forward_comm (src/comm_brick.cpp:444-506, 696-864);
+ *     FixMeso::initial/final_integrate (src/USER-SPH/fix_meso.cpp:91-180).
+ *
+ * Every function returns 0 on success and a negative SPH_HIP_E* code on failure;
+ * sph_hip_last_error() then describes the failure (thread-local).  As with the GPU
+ * package precedent (src/GPU/pair_lj_cut_gpu.cpp:114-115) the caller turns a failure into
+ * error->one(FLERR, ...).  There is no CPU fallback: without a usable HIP device every
+ * compute entry point fails with SPH_HIP_ENODEV.
+ *
+ * Array conventions (identical to LAMMPS): per-atom vectors are AoS double[n][3]
+ * (atom->x's contiguous backing, src/memory.h:124-137); per-type tables have ntypes+1
+ * entries and per-type-pair tables (ntypes+1)^2 entries, row-major, 1-based types.
+ */
+#ifndef SPH_HIP_H
+#define SPH_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPH_HIP_ABI_VERSION 1
+
+#define SPH_HIP_OK 0
+#define SPH_HIP_EINVAL (-1)   /* bad argument / not configured */
+#define SPH_HIP_ENODEV (-2)   /* no usable HIP device */
+#define SPH_HIP_ERUNTIME (-3) /* HIP runtime / kernel failure */
+#define SPH_HIP_ENOMEM (-4)   /* device allocation failed ("Insufficient memory on accelerator") */
+#define SPH_HIP_ECOMM (-5)    /* RCCL failure */
+#define SPH_HIP_EOVERFLOW (-6)/* neighbor / ghost capacity exceeded */
+
+/* list kinds, as NeighRequest half/full (src/neigh_request.h) */
+#define SPH_LIST_FULL 0
+#define SPH_LIST_HALF 1
+
+/* viscosity variants of sph/taitwater */
+#define SPH_VISC_MONAGHAN 0   /* sph/taitwater        (pair_sph_taitwater.cpp:162-169) */
+#define SPH_VISC_MORRIS 1     /* sph/taitwater/morris (pair_sph_taitwater_morris.cpp:163-167) */
+
+const char *sph_hip_last_error(void);
+int sph_hip_abi_version(void);
+/* number of visible HIP devices (0 without a GPU; never fails) */
+int sph_hip_device_count(void);
+
+/* ======================================================================================
+ * 1. Pair-style layer
+ * ==================================================================================== */
+typedef struct sph_hip_ctx sph_hip_ctx;
+
+/* One context per MPI rank / Pair instance set.  dim = domain->dimension, ntypes =
+   atom->ntypes, newton_pair = force->newton_pair. */
+int sph_hip_create(int device, int dim, int ntypes, int newton_pair, sph_hip_ctx **out);
+int sph_hip_destroy(sph_hip_ctx *ctx);
+
+/* PairSPHRhoSum::coeff/init_one: cut (nt+1)^2 (h per type pair), mass = atom->mass. */
+int sph_hip_rhosum_coeff(sph_hip_ctx *ctx, const double *cut, const double *mass);
+/* PairSPHTaitwater[Morris]::coeff/init_one: rho0, soundspeed, B per type (nt+1),
+   viscosity and cut per pair ((nt+1)^2). visc_variant = SPH_VISC_*. */
+int sph_hip_taitwater_coeff(sph_hip_ctx *ctx, int visc_variant, const double *rho0,
+                            const double *soundspeed, const double *B,
+                            const double *viscosity, const double *cut, const double *mass);
+/* PairSPHHeatConduction::coeff/init_one: alpha and cut per pair ((nt+1)^2). */
+int sph_hip_heatconduction_coeff(sph_hip_ctx *ctx, const double *alpha, const double *cut,
+                                 const double *mass);
+
+/* Stage per-atom inputs: nlocal owned then nghost ghost atoms (atom->x, atom->vest,
+   atom->rho, atom->e, atom->type).  vest/rho/e may be NULL when the next compute does
+   not read them. */
+int sph_hip_atoms(sph_hip_ctx *ctx, int nlocal, int nghost, const double *x,
+                  const double *vest, const double *rho, const double *e, const int *type);
+
+/* Stage a LAMMPS NeighList (list->inum, ilist, numneigh, firstneigh; NEIGHMASK bits are
+   stripped).  kind = SPH_LIST_FULL (gather-only kernels, nothing written to ghosts) or
+   SPH_LIST_HALF (Newton-3 scatter onto j with fp64 atomics, like the reference). */
+int sph_hip_list(sph_hip_ctx *ctx, int kind, int inum, const int *ilist,
+                 const int *numneigh, const int *const *firstneigh);
+/* Same, from a CSR list (row i = neigh[off[i]..off[i+1]) for owned atom i). */
+int sph_hip_list_csr(sph_hip_ctx *ctx, int kind, int inum, const int64_t *off,
+                     const int *neigh);
+
+/* rho[0..nlocal) <- self term + sum over list (pair_sph_rhosum.cpp:112-195).  The
+   forward_comm_pair of ghost rho stays with the caller (comm->forward_comm_pair). */
+int sph_hip_rhosum(sph_hip_ctx *ctx, double *rho);
+/* f (nall*3), drho, de (nall) are ACCUMULATED into (force_clear semantics stay with the
+   caller).  With a FULL list only owned entries change; with a HALF list ghosts receive
+   their Newton-3 share exactly as in the reference and need reverse_comm. virial may be
+   NULL, else 6 doubles accumulated in the ev_tally convention (pair.cpp:770-850). */
+int sph_hip_taitwater(sph_hip_ctx *ctx, double *f, double *drho, double *de,
+                      double *virial);
+int sph_hip_heatconduction(sph_hip_ctx *ctx, double *de);
+
+/* ======================================================================================
+ * 2. Device-resident engine
+ * ==================================================================================== */
+#define SPH_MAXTYPES 8
+
+typedef struct {
+  int dim;                     /* 2 or 3 */
+  int ntypes;                  /* <= SPH_MAXTYPES */
+  double boxlo[3], boxhi[3];   /* global box */
+  int periodic[3];
+  double skin;                 /* neighbor skin */
+  int neigh_every;             /* rebuild every N steps (neigh_modify every N check no) */
+  double dt;                   /* timestep (units lj: ftm2v = 1) */
+  double ftm2v;                /* force->ftm2v */
+  double mass[SPH_MAXTYPES + 1];
+  /* integrator: 0 = fix meso for all types, 1 = fix meso/stationary for type 2.. (bc) */
+  int stationary_mask;         /* bit t set: type t integrates with meso/stationary */
+  /* sph/rhosum: enabled if rhosum_nstep > 0 */
+  int rhosum_nstep;
+  double rhosum_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  /* sph/taitwater[/morris]: enabled if tait_on */
+  int tait_on;
+  int tait_visc;               /* SPH_VISC_* */
+  double rho0[SPH_MAXTYPES + 1], soundspeed[SPH_MAXTYPES + 1], B[SPH_MAXTYPES + 1];
+  double tait_visc_coef[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double tait_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  /* sph/heatconduction: enabled if heat_on */
+  int heat_on;
+  double heat_alpha[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double heat_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  /* body force per unit mass (fix gravity style), added in post_force: f += m*g */
+  double gravity[3];
+  /* brick decomposition (procgrid[0]*procgrid[1]*procgrid[2] ranks; 1 1 1 = serial) */
+  int procgrid[3];
+  int rank;                    /* my rank in the brick, x fastest */
+  /* spatially sort owned particles at every rebuild (atom->sort analogue) */
+  int sort;
+} sph_engine_config;
+
+typedef struct {
+  int64_t step;
+  int nlocal, nghost;
+  int64_t nbr_full;            /* entries in the device full list (owned rows) */
+  int nbr_builds;
+  int nbr_maxrow;
+  double ms_rhosum, ms_tait, ms_heat, ms_integrate, ms_comm, ms_neigh; /* event-timed */
+  int64_t n_rhosum, n_tait, n_heat, n_neigh;  /* launches timed */
+} sph_engine_stats;
+
+typedef struct sph_engine sph_engine;
+
+int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out);
+int sph_engine_destroy(sph_engine *e);
+
+/* RCCL communicator for procgrid runs: uid = ncclUniqueId bytes (128) produced by
+   sph_engine_comm_uid on rank 0 and distributed by the caller (MPI_Bcast / torch). */
+int sph_engine_comm_uid(void *uid128);
+int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank);
+
+/* Owned particles of this rank (tag order is the caller's order; results are returned in
+   the same order).  v is the velocity; vest is set from v at setup (FixMeso::setup_pre_force). */
+int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
+                         const int *type, const double *rho, const double *en,
+                         const double *cv);
+/* Verlet::setup: forced rebuild + forces at step 0. */
+int sph_engine_setup(sph_engine *e);
+/* Verlet::run(nsteps). */
+int sph_engine_run(sph_engine *e, int nsteps);
+/* Copy back owned particles in the set_atoms order (any pointer may be NULL). n is the
+   current nlocal (sph_engine_nlocal). */
+int sph_engine_nlocal(sph_engine *e);
+int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, double *en,
+                         double *f, double *drho, double *de, int *tag);
+/* per owned particle (set_atoms order): full-list count within cut+skin at last build */
+int sph_engine_neighbor_counts(sph_engine *e, int *numneigh);
+int sph_engine_stats_get(sph_engine *e, sph_engine_stats *s);
+/* enable/disable hipEvent timing of each kernel class (adds event records per launch) */
+int sph_engine_set_timing(sph_engine *e, int on);
+/* synchronise the engine's stream */
+int sph_engine_sync(sph_engine *e);
+/* run only the pair passes (rhosum + forward comm + taitwater [+heat]) n times on the
+   current state, no integration or rebuild: the kernel-roofline workload */
+int sph_engine_pair_passes(sph_engine *e, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPH_HIP_H */

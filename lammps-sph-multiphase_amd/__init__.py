@@ -1,0 +1,327 @@
+"""Python bindings of libsph_hip.so (include/sph_hip.h) -- the MI355X USER-SPH engine.
+
+This is host plumbing for tests and bench.py; the product is the C ABI.  There is no CPU
+fallback: if libsph_hip.so is missing, or no HIP device is usable, every compute call
+raises ``HipError``.
+
+Loaded by path because the directory name is not a Python identifier::
+
+    spec = importlib.util.spec_from_file_location("sph_amd", ".../lammps-sph-multiphase_amd/__init__.py")
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsph_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "sph_hip.h")
+
+SPH_LIST_FULL, SPH_LIST_HALF = 0, 1
+SPH_VISC_MONAGHAN, SPH_VISC_MORRIS = 0, 1
+SPH_MAXTYPES = 8
+_NT2 = (SPH_MAXTYPES + 1) ** 2
+
+ERRORS = {-1: "EINVAL", -2: "ENODEV", -3: "ERUNTIME", -4: "ENOMEM", -5: "ECOMM",
+          -6: "EOVERFLOW"}
+
+
+class HipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"sph_hip {ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_lp = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_i, _d, _vp = C.c_int, C.c_double, C.c_void_p
+
+_lib = None
+
+
+class EngineConfig(C.Structure):
+    _fields_ = [
+        ("dim", C.c_int), ("ntypes", C.c_int),
+        ("boxlo", C.c_double * 3), ("boxhi", C.c_double * 3), ("periodic", C.c_int * 3),
+        ("skin", C.c_double), ("neigh_every", C.c_int), ("dt", C.c_double),
+        ("ftm2v", C.c_double), ("mass", C.c_double * (SPH_MAXTYPES + 1)),
+        ("stationary_mask", C.c_int),
+        ("rhosum_nstep", C.c_int), ("rhosum_cut", C.c_double * _NT2),
+        ("tait_on", C.c_int), ("tait_visc", C.c_int),
+        ("rho0", C.c_double * (SPH_MAXTYPES + 1)),
+        ("soundspeed", C.c_double * (SPH_MAXTYPES + 1)),
+        ("B", C.c_double * (SPH_MAXTYPES + 1)),
+        ("tait_visc_coef", C.c_double * _NT2), ("tait_cut", C.c_double * _NT2),
+        ("heat_on", C.c_int), ("heat_alpha", C.c_double * _NT2), ("heat_cut", C.c_double * _NT2),
+        ("gravity", C.c_double * 3),
+        ("procgrid", C.c_int * 3), ("rank", C.c_int), ("sort", C.c_int),
+    ]
+
+
+class EngineStats(C.Structure):
+    _fields_ = [
+        ("step", C.c_int64), ("nlocal", C.c_int), ("nghost", C.c_int),
+        ("nbr_full", C.c_int64), ("nbr_builds", C.c_int), ("nbr_maxrow", C.c_int),
+        ("ms_rhosum", C.c_double), ("ms_tait", C.c_double), ("ms_heat", C.c_double),
+        ("ms_integrate", C.c_double), ("ms_comm", C.c_double), ("ms_neigh", C.c_double),
+        ("n_rhosum", C.c_int64), ("n_tait", C.c_int64), ("n_heat", C.c_int64),
+        ("n_neigh", C.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "sph_hip_last_error": (C.c_char_p, []),
+    "sph_hip_abi_version": (_i, []),
+    "sph_hip_device_count": (_i, []),
+    "sph_hip_create": (_i, [_i, _i, _i, _i, C.POINTER(_vp)]),
+    "sph_hip_destroy": (_i, [_vp]),
+    "sph_hip_rhosum_coeff": (_i, [_vp, _dp, _dp]),
+    "sph_hip_taitwater_coeff": (_i, [_vp, _i, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "sph_hip_heatconduction_coeff": (_i, [_vp, _dp, _dp, _dp]),
+    "sph_hip_atoms": (_i, [_vp, _i, _i, _dp, _vp, _vp, _vp, _ip]),
+    "sph_hip_list": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "sph_hip_list_csr": (_i, [_vp, _i, _i, _lp, _ip]),
+    "sph_hip_rhosum": (_i, [_vp, _dp]),
+    "sph_hip_taitwater": (_i, [_vp, _dp, _dp, _dp, _vp]),
+    "sph_hip_heatconduction": (_i, [_vp, _dp]),
+    "sph_engine_create": (_i, [_i, C.POINTER(EngineConfig), C.POINTER(_vp)]),
+    "sph_engine_destroy": (_i, [_vp]),
+    "sph_engine_comm_uid": (_i, [_vp]),
+    "sph_engine_comm_init": (_i, [_vp, _vp, _i, _i]),
+    "sph_engine_set_atoms": (_i, [_vp, _i, _dp, _dp, _ip, _dp, _vp, _vp]),
+    "sph_engine_setup": (_i, [_vp]),
+    "sph_engine_run": (_i, [_vp, _i]),
+    "sph_engine_nlocal": (_i, [_vp]),
+    "sph_engine_get_atoms": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sph_engine_neighbor_counts": (_i, [_vp, _ip]),
+    "sph_engine_stats_get": (_i, [_vp, C.POINTER(EngineStats)]),
+    "sph_engine_set_timing": (_i, [_vp, _i]),
+    "sph_engine_sync": (_i, [_vp]),
+    "sph_engine_pair_passes": (_i, [_vp, _i]),
+}
+
+
+def load() -> C.CDLL:
+    """Load libsph_hip.so (raises if it was not built -- there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipError(-2, f"{LIB_PATH} not built (run `make -C lammps-sph-multiphase_amd`)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _chk(rc: int):
+    if rc != 0:
+        raise HipError(rc, load().sph_hip_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    return load().sph_hip_device_count()
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+# ------------------------------------------------------------------------------------------
+# 1. Pair-style layer
+# ------------------------------------------------------------------------------------------
+class PairContext:
+    """One sph_hip_ctx: what the LAMMPS sph/<style>/hip Pair classes drive."""
+
+    def __init__(self, dim: int, ntypes: int, newton_pair: int = 1, device: int = 0):
+        self.L = load()
+        h = _vp()
+        _chk(self.L.sph_hip_create(device, dim, ntypes, newton_pair, C.byref(h)))
+        self.h = h
+        self.ntypes = ntypes
+        self.nlocal = self.nghost = 0
+
+    def close(self):
+        if self.h:
+            self.L.sph_hip_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _t(a):
+        return np.ascontiguousarray(a, dtype=np.float64).ravel()
+
+    def rhosum_coeff(self, cut, mass):
+        _chk(self.L.sph_hip_rhosum_coeff(self.h, self._t(cut), self._t(mass)))
+
+    def taitwater_coeff(self, rho0, c0, B, visc, cut, mass, morris=False):
+        _chk(self.L.sph_hip_taitwater_coeff(self.h, SPH_VISC_MORRIS if morris else SPH_VISC_MONAGHAN,
+                                            self._t(rho0), self._t(c0), self._t(B), self._t(visc),
+                                            self._t(cut), self._t(mass)))
+
+    def heatconduction_coeff(self, alpha, cut, mass):
+        _chk(self.L.sph_hip_heatconduction_coeff(self.h, self._t(alpha), self._t(cut),
+                                                 self._t(mass)))
+
+    def atoms(self, nlocal, nghost, x, type_, vest=None, rho=None, e=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        t = np.ascontiguousarray(type_, dtype=np.int32)
+        vest = None if vest is None else np.ascontiguousarray(vest, dtype=np.float64)
+        rho = None if rho is None else np.ascontiguousarray(rho, dtype=np.float64)
+        e = None if e is None else np.ascontiguousarray(e, dtype=np.float64)
+        _chk(self.L.sph_hip_atoms(self.h, nlocal, nghost, x, _ptr(vest), _ptr(rho), _ptr(e), t))
+        self._keep = (x, t, vest, rho, e)
+        self.nlocal, self.nghost = nlocal, nghost
+
+    def list_csr(self, kind, off, neigh):
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        neigh = np.ascontiguousarray(neigh if len(neigh) else np.zeros(1), dtype=np.int32)
+        _chk(self.L.sph_hip_list_csr(self.h, kind, len(off) - 1, off, neigh))
+
+    def list_lammps(self, kind, ilist, numneigh, firstneigh_rows):
+        """LAMMPS NeighList form: ilist, numneigh (per atom), list of per-atom int32 rows."""
+        ilist = np.ascontiguousarray(ilist, dtype=np.int32)
+        numneigh = np.ascontiguousarray(numneigh, dtype=np.int32)
+        rows = [np.ascontiguousarray(r, dtype=np.int32) for r in firstneigh_rows]
+        ptrs = (C.c_void_p * max(len(rows), 1))(*[r.ctypes.data for r in rows])
+        _chk(self.L.sph_hip_list(self.h, kind, len(ilist), ilist.ctypes.data,
+                                 numneigh.ctypes.data, C.cast(ptrs, C.c_void_p)))
+
+    def rhosum(self, rho):
+        _chk(self.L.sph_hip_rhosum(self.h, rho))
+        return rho
+
+    def taitwater(self, f, drho, de, virial=None):
+        _chk(self.L.sph_hip_taitwater(self.h, f, drho, de, _ptr(virial)))
+
+    def heatconduction(self, de):
+        _chk(self.L.sph_hip_heatconduction(self.h, de))
+
+
+# ------------------------------------------------------------------------------------------
+# 2. Device-resident engine
+# ------------------------------------------------------------------------------------------
+def _pair_table(dst, tab, ntypes):
+    tab = np.asarray(tab, dtype=np.float64)
+    for i in range(ntypes + 1):
+        for j in range(ntypes + 1):
+            dst[i * (SPH_MAXTYPES + 1) + j] = float(tab[i, j])
+
+
+def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every=10,
+                rhosum=None, tait=None, heat=None, gravity=(0.0, 0.0, 0.0),
+                stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0) -> EngineConfig:
+    """rhosum = dict(nstep, cut); tait = dict(rho0, c0, visc, cut, morris[, B]);
+    heat = dict(alpha, cut); per-type arrays (ntypes+1), per-pair (ntypes+1, ntypes+1)."""
+    c = EngineConfig()
+    c.dim, c.ntypes = dim, ntypes
+    for k in range(3):
+        c.boxlo[k], c.boxhi[k], c.periodic[k] = float(boxlo[k]), float(boxhi[k]), int(periodic[k])
+        c.gravity[k] = float(gravity[k])
+        c.procgrid[k] = int(procgrid[k])
+    c.rank = rank
+    c.skin, c.dt, c.neigh_every, c.ftm2v = skin, dt, neigh_every, 1.0
+    for t in range(ntypes + 1):
+        c.mass[t] = float(mass[t])
+    c.stationary_mask = stationary_mask
+    c.sort = sort
+    if rhosum:
+        c.rhosum_nstep = int(rhosum.get("nstep", 1))
+        _pair_table(c.rhosum_cut, rhosum["cut"], ntypes)
+    if tait:
+        c.tait_on = 1
+        c.tait_visc = SPH_VISC_MORRIS if tait.get("morris") else SPH_VISC_MONAGHAN
+        rho0 = np.asarray(tait["rho0"], dtype=np.float64)
+        c0 = np.asarray(tait["c0"], dtype=np.float64)
+        B = np.asarray(tait["B"], dtype=np.float64) if "B" in tait else c0 * c0 * rho0 / 7.0
+        for t in range(ntypes + 1):
+            c.rho0[t], c.soundspeed[t], c.B[t] = float(rho0[t]), float(c0[t]), float(B[t])
+        _pair_table(c.tait_visc_coef, tait["visc"], ntypes)
+        _pair_table(c.tait_cut, tait["cut"], ntypes)
+    if heat:
+        c.heat_on = 1
+        _pair_table(c.heat_alpha, heat["alpha"], ntypes)
+        _pair_table(c.heat_cut, heat["cut"], ntypes)
+    return c
+
+
+class Engine:
+    def __init__(self, cfg: EngineConfig, device: int = 0):
+        self.L = load()
+        h = _vp()
+        self.cfg = cfg
+        _chk(self.L.sph_engine_create(device, C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.L.sph_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_atoms(self, x, v, type_, rho, e=None, cv=None):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        t = np.ascontiguousarray(type_, dtype=np.int32)
+        rho = np.ascontiguousarray(rho, dtype=np.float64)
+        e = None if e is None else np.ascontiguousarray(e, dtype=np.float64)
+        cv = None if cv is None else np.ascontiguousarray(cv, dtype=np.float64)
+        _chk(self.L.sph_engine_set_atoms(self.h, x.shape[0], x, v, t, rho, _ptr(e), _ptr(cv)))
+
+    def setup(self):
+        _chk(self.L.sph_engine_setup(self.h))
+
+    def run(self, n):
+        _chk(self.L.sph_engine_run(self.h, n))
+
+    def pair_passes(self, n):
+        _chk(self.L.sph_engine_pair_passes(self.h, n))
+
+    def sync(self):
+        _chk(self.L.sph_engine_sync(self.h))
+
+    def set_timing(self, on):
+        _chk(self.L.sph_engine_set_timing(self.h, 1 if on else 0))
+
+    @property
+    def nlocal(self):
+        return self.L.sph_engine_nlocal(self.h)
+
+    def get_atoms(self):
+        n = self.nlocal
+        out = {k: np.zeros((n, 3)) for k in ("x", "v", "f")}
+        out.update({k: np.zeros(n) for k in ("rho", "e", "drho", "de")})
+        _chk(self.L.sph_engine_get_atoms(self.h, out["x"].ctypes.data, out["v"].ctypes.data,
+                                         out["rho"].ctypes.data, out["e"].ctypes.data,
+                                         out["f"].ctypes.data, out["drho"].ctypes.data,
+                                         out["de"].ctypes.data, None))
+        return out
+
+    def neighbor_counts(self):
+        c = np.zeros(self.nlocal, dtype=np.int32)
+        _chk(self.L.sph_engine_neighbor_counts(self.h, c))
+        return c
+
+    def stats(self) -> dict:
+        s = EngineStats()
+        _chk(self.L.sph_engine_stats_get(self.h, C.byref(s)))
+        return s.as_dict()

@@ -1,0 +1,753 @@
+// sph_engine.hip -- device-resident engine of the C ABI (include/sph_hip.h, section 2).
+//
+// One engine = one rank's share of an SPH run, resident in HBM.  A step is Verlet::run's
+// sequence (src/verlet.cpp:222-308) specialised to the USER-SPH hot path:
+//   initial_integrate -> [rebuild: pbc, spatial sort, borders, bins, full list]
+//   | forward comm -> rhosum (+EOS) -> forward rho -> taitwater[/morris][+heat] ->
+//   final_integrate
+// Full lists are walked gather-only, so the reverse communication of the reference
+// (comm->reverse_comm, verlet.cpp:290-293) has nothing to carry and is skipped.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "sph_coef.h"
+#include "sph_dispatch.h"
+#include "sph_engine_kernels.h"
+#include "sph_util.h"
+
+using namespace sph;
+
+namespace {
+
+constexpr int BLK = 256;
+inline unsigned blocks(long n) { return (unsigned)((n + BLK - 1) / BLK); }
+
+enum TimerClass { T_RHO, T_TAIT, T_HEAT, T_INT, T_COMM, T_NEIGH, T_NCLASS };
+
+}  // namespace
+
+struct sph_engine {
+  int device = 0;
+  hipStream_t s = nullptr;
+  sph_engine_config cfg{};
+  Coefs hc{};
+  Coefs *dc = nullptr;
+  Box box{};
+  double sublo[3], subhi[3];
+  double cutneighmax = 0.0, cutghost = 0.0;
+  StepConst sc{};
+  int force_mode = 0;  // M_TAIT | M_HEAT
+
+  int nlocal = 0, nghost = 0;
+  int64_t step = 0;
+  bool setup_done = false;
+  int last_build = 0;
+
+  // atoms (owned first, then ghosts)
+  DBuf<double4> xt, vr;
+  DBuf<double2> aux;
+  // owned only
+  DBuf<double4> vel, fo;
+  DBuf<double> de;
+  DBuf<int> tag;
+  // sort scratch
+  DBuf<double4> xt2, vr2, vel2, fo2;
+  DBuf<double2> aux2;
+  DBuf<double> de2;
+  DBuf<int> tag2;
+  // ghosts
+  DBuf<int> gowner, gimg;
+  // borders scratch
+  DBuf<unsigned char> flags;
+  DBuf<int> sel, nsel;
+  // bins
+  Bins bn{};
+  int nbins = 0;
+  DBuf<unsigned> bkey, bkey2;
+  DBuf<int> bidx, bidx2, bstart, bend;
+  // neighbor list
+  DBuf<int> cnt, off, nbr;
+  int64_t nbr_total = 0;
+  int nbr_builds = 0, nbr_maxrow = 0;
+  // cub scratch
+  DBuf<unsigned char> tmp;
+  // pinned host scalar
+  int *h_scalar = nullptr;
+
+  // timing
+  bool timing = false;
+  struct EvPair {
+    hipEvent_t a, b;
+    int cls;
+  };
+  std::vector<EvPair> pending;
+  std::vector<hipEvent_t> evpool;
+  double ms[T_NCLASS] = {0, 0, 0, 0, 0, 0};
+  int64_t nlaunch[T_NCLASS] = {0, 0, 0, 0, 0, 0};
+
+  hipEvent_t get_ev() {
+    if (!evpool.empty()) {
+      hipEvent_t e = evpool.back();
+      evpool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    SPH_HIP_TRY(hipEventCreate(&e));
+    return e;
+  }
+  struct Scope {
+    sph_engine *e;
+    EvPair p;
+    Scope(sph_engine *eng, int cls) : e(eng) {
+      if (!e->timing) return;
+      p.a = e->get_ev();
+      p.b = e->get_ev();
+      p.cls = cls;
+      SPH_HIP_TRY(hipEventRecord(p.a, e->s));
+    }
+    ~Scope() {
+      if (!e->timing) return;
+      (void)hipEventRecord(p.b, e->s);
+      e->pending.push_back(p);
+    }
+  };
+  void harvest() {
+    if (pending.empty()) return;
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    for (auto &p : pending) {
+      float t = 0.f;
+      SPH_HIP_TRY(hipEventElapsedTime(&t, p.a, p.b));
+      ms[p.cls] += t;
+      nlaunch[p.cls] += 1;
+      evpool.push_back(p.a);
+      evpool.push_back(p.b);
+    }
+    pending.clear();
+  }
+
+  void tmp_reserve(size_t b) { tmp.reserve(b); }
+
+  void ensure_atoms(size_t nall, bool keep) {
+    xt.reserve(nall, keep, s);
+    vr.reserve(nall, keep, s);
+    aux.reserve(nall, keep, s);
+  }
+
+  // ------------------------------------------------------------------------------------
+  void sort_owned() {
+    if (!cfg.sort || nlocal < 2) return;
+    const int n = nlocal;
+    bkey.reserve(n);
+    bkey2.reserve(n);
+    bidx.reserve(n);
+    bidx2.reserve(n);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, bn, xt.p, bkey.p, bidx.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
+    xt2.reserve(xt.cap);
+    vr2.reserve(vr.cap);
+    aux2.reserve(aux.cap);
+    vel2.reserve(n);
+    fo2.reserve(n);
+    de2.reserve(n);
+    tag2.reserve(n);
+    hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, xt.p, vr.p,
+                       aux.p, vel.p, tag.p, fo.p, de.p, xt2.p, vr2.p, aux2.p, vel2.p, tag2.p,
+                       fo2.p, de2.p);
+    std::swap(xt, xt2);
+    std::swap(vr, vr2);
+    std::swap(aux, aux2);
+    std::swap(vel, vel2);
+    std::swap(fo, fo2);
+    std::swap(de, de2);
+    std::swap(tag, tag2);
+  }
+
+  int read_scalar(const int *dptr) {
+    SPH_HIP_TRY(hipMemcpyAsync(h_scalar, dptr, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    return *h_scalar;
+  }
+
+  // CommBrick::setup slabs (comm_brick.cpp:330-380) + borders (:696-864) on one process
+  void borders() {
+    nghost = 0;
+    int nall = nlocal;
+    const int ndim = cfg.dim;
+    nsel.reserve(1);
+    for (int d = 0; d < ndim; d++) {
+      if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
+      const int nlast = nall;
+      for (int ineed = 0; ineed < 2; ineed++) {
+        double lo, hi, shift;
+        int pbc;
+        if (ineed == 0) {
+          lo = -1.0e20;
+          hi = sublo[d] + cutghost;
+          pbc = 1;
+        } else {
+          lo = subhi[d] - cutghost;
+          hi = 1.0e20;
+          pbc = -1;
+        }
+        shift = pbc * box.prd[d];
+        flags.reserve(nlast);
+        sel.reserve(nlast);
+        hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d, lo, hi, xt.p, flags.p);
+        hipcub::CountingInputIterator<int> it(0);
+        size_t tb = 0;
+        SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flags.p, sel.p, nsel.p, nlast, s));
+        tmp_reserve(tb);
+        SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flags.p, sel.p, nsel.p, nlast, s));
+        const int ns = read_scalar(nsel.p);
+        if (ns == 0) continue;
+        ensure_atoms((size_t)nall + ns, true);
+        gowner.reserve((size_t)nall + ns - nlocal, true, s);
+        gimg.reserve((size_t)nall + ns - nlocal, true, s);
+        hipLaunchKernelGGL(k_append_ghosts, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sel.p,
+                           nlocal, nall, d, pbc, shift, xt.p, vr.p, aux.p, gowner.p, gimg.p);
+        nall += ns;
+      }
+    }
+    nghost = nall - nlocal;
+  }
+
+  void setup_bins_geometry() {
+    for (int k = 0; k < 3; k++) {
+      double lo = sublo[k], hi = subhi[k];
+      if (k < cfg.dim) {
+        lo -= cutghost;
+        hi += cutghost;
+        const double ext = hi - lo;
+        int nb = (int)(ext / cutneighmax);
+        if (nb < 1) nb = 1;
+        if (nb > 4096) nb = 4096;
+        bn.lo[k] = lo;
+        bn.nb[k] = nb;
+        bn.inv[k] = nb / ext;
+      } else {
+        bn.lo[k] = lo;
+        bn.nb[k] = 1;
+        bn.inv[k] = 0.0;
+      }
+    }
+    nbins = bn.nb[0] * bn.nb[1] * bn.nb[2];
+  }
+
+  void build_bins() {
+    const int nall = nlocal + nghost;
+    bkey.reserve(nall);
+    bkey2.reserve(nall);
+    bidx.reserve(nall);
+    bidx2.reserve(nall);
+    bstart.reserve(nbins);
+    bend.reserve(nbins);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bn, xt.p, bkey.p, bidx.p);
+    int endbit = 1;
+    while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
+    SPH_HIP_TRY(hipMemsetAsync(bstart.p, 0, nbins * sizeof(int), s));
+    SPH_HIP_TRY(hipMemsetAsync(bend.p, 0, nbins * sizeof(int), s));
+    hipLaunchKernelGGL(k_bin_bounds, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bkey2.p, bstart.p, bend.p);
+  }
+
+  void build_list() {
+    constexpr int G = 8;
+    const int n = nlocal;
+    cnt.reserve(n + 1);
+    off.reserve(n + 1);
+    dim3 grid(grid_for_rows(n, G)), block(BLK);
+    if (n > 0)
+      hipLaunchKernelGGL((k_neigh<G, false>), grid, block, 0, s, n, bn, cfg.dim, xt.p, bidx2.p,
+                         bstart.p, bend.p, dc, cnt.p, (const int *)nullptr, (int *)nullptr);
+    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, cnt.p, off.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, off.p, off.p, n + 1, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, off.p, off.p, n + 1, s));
+    // total (int32 offsets: SPH_HIP_EOVERFLOW beyond 2^31-1 entries)
+    const int tot = read_scalar(off.p + n);
+    SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
+    nbr.reserve(tot > 0 ? tot : 1);
+    if (n > 0)
+      hipLaunchKernelGGL((k_neigh<G, true>), grid, block, 0, s, n, bn, cfg.dim, xt.p, bidx2.p,
+                         bstart.p, bend.p, dc, (int *)nullptr, off.p, nbr.p);
+    nbr_total = tot;
+    nbr_builds++;
+  }
+
+  void rebuild() {
+    Scope t(this, T_NEIGH);
+    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xt.p);
+    sort_owned();
+    borders();
+    build_bins();
+    build_list();
+  }
+
+  void forward() {
+    if (nghost == 0) return;
+    Scope t(this, T_COMM);
+    hipLaunchKernelGGL(k_forward, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal, box,
+                       gowner.p, gimg.p, xt.p, vr.p, aux.p);
+  }
+
+  void pair_compute(bool do_rhosum, bool setup = false) {
+    const int nall = nlocal + nghost;
+    if (do_rhosum) {
+      {
+        Scope t(this, T_RHO);
+        launch_rhosum(cfg.dim, true, s, nlocal, nullptr, off.p, nbr.p, xt.p, vr.p, aux.p,
+                      nullptr, dc);
+      }
+      if (nghost) {
+        Scope t(this, T_COMM);
+        hipLaunchKernelGGL(k_forward_rho, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost,
+                           nlocal, gowner.p, vr.p, aux.p);
+      }
+    } else if (force_mode & M_TAIT) {
+      hipLaunchKernelGGL(k_eos, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xt.p, vr.p, aux.p, dc);
+    }
+    if (force_mode && setup) {
+      setup_forces_half();
+    } else if (force_mode) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      ForceArgs a{};
+      a.inum = nlocal;
+      a.nlocal = nlocal;
+      a.newton = 1;
+      a.ilist = nullptr;
+      a.off = off.p;
+      a.nbr = nbr.p;
+      a.xt = xt.p;
+      a.vr = vr.p;
+      a.aux = aux.p;
+      a.fo = fo.p;
+      a.de = de.p;
+      a.accum = 0;
+      a.cf = dc;
+      a.gx = cfg.gravity[0];
+      a.gy = cfg.gravity[1];
+      a.gz = cfg.gravity[2];
+      a.virial = nullptr;
+      launch_force(cfg.dim, s, cfg.tait_visc, force_mode, a);
+    } else {
+      SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, nlocal * sizeof(double4), s));
+      SPH_HIP_TRY(hipMemsetAsync(de.p, 0, nlocal * sizeof(double), s));
+    }
+  }
+
+  // Force pass of Verlet::setup with the reference's half-list ownership (see
+  // k_half_from_full): exact even though ghost vest is stale at this point.
+  void setup_forces_half() {
+    const int n = nlocal, nall = nlocal + nghost;
+    if (force_mode == 0 || n == 0) return;
+    DBuf<int> hcnt, hoff, hnbr;
+    hcnt.reserve(n + 1);
+    hoff.reserve(n + 1);
+    hipLaunchKernelGGL((k_half_from_full<false>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
+                       nbr.p, xt.p, hcnt.p, (const int *)nullptr, (int *)nullptr);
+    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, hcnt.p, hoff.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hoff.p, hoff.p, n + 1, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, hoff.p, hoff.p, n + 1, s));
+    const int tot = read_scalar(hoff.p + n);
+    hnbr.reserve(tot > 0 ? tot : 1);
+    hipLaunchKernelGGL((k_half_from_full<true>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
+                       nbr.p, xt.p, (int *)nullptr, hoff.p, hnbr.p);
+    fo.reserve(nall, true, s);
+    de.reserve(nall, true, s);
+    SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, nall * sizeof(double4), s));
+    SPH_HIP_TRY(hipMemsetAsync(de.p, 0, nall * sizeof(double), s));
+    ForceArgs a{};
+    a.inum = n;
+    a.nlocal = n;
+    a.newton = 1;
+    a.off = hoff.p;
+    a.nbr = hnbr.p;
+    a.xt = xt.p;
+    a.vr = vr.p;
+    a.aux = aux.p;
+    a.fo = fo.p;
+    a.de = de.p;
+    a.cf = dc;
+    launch_force(cfg.dim, s, cfg.tait_visc, force_mode | M_HALF, a);
+    if (nghost)
+      hipLaunchKernelGGL(k_reverse, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, n, gowner.p,
+                         fo.p, de.p);
+    // post_force body force (fix gravity style), as the full-list kernel applies it
+    if (cfg.gravity[0] != 0.0 || cfg.gravity[1] != 0.0 || cfg.gravity[2] != 0.0)
+      hipLaunchKernelGGL(k_add_gravity, dim3(blocks(n)), dim3(BLK), 0, s, n, sc,
+                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], xt.p, fo.p);
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // scratch lists are freed on return
+    hcnt.release();
+    hoff.release();
+    hnbr.release();
+  }
+
+  bool rhosum_due() const {
+    return cfg.rhosum_nstep > 0 && (step % cfg.rhosum_nstep) == 0;
+  }
+
+  // Verlet::setup (verlet.cpp:88-139)
+  void setup() {
+    step = 0;
+    Scope t(this, T_NEIGH);
+    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xt.p);
+    sort_owned();
+    borders();      // ghosts carry vest as it was before setup_pre_force (reference order)
+    build_bins();
+    build_list();
+    hipLaunchKernelGGL(k_vest_from_v, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
+                       cfg.stationary_mask, xt.p, vel.p, vr.p);
+    pair_compute(rhosum_due(), /*setup=*/true);
+    last_build = 0;
+    setup_done = true;
+  }
+
+  // Verlet::run (verlet.cpp:222-308)
+  void run(int nsteps) {
+    for (int k = 0; k < nsteps; k++) {
+      step++;
+      {
+        Scope t(this, T_INT);
+        hipLaunchKernelGGL(k_initial_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
+                           sc, xt.p, vr.p, aux.p, vel.p, fo.p, de.p);
+      }
+      const int every = cfg.neigh_every > 0 ? cfg.neigh_every : 1;
+      if ((step - last_build) % every == 0) {
+        rebuild();
+        last_build = (int)step;
+      } else {
+        forward();
+      }
+      pair_compute(rhosum_due());
+      {
+        Scope t(this, T_INT);
+        hipLaunchKernelGGL(k_final_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
+                           sc, xt.p, vr.p, aux.p, vel.p, fo.p, de.p);
+      }
+      if (timing && pending.size() > 4096) harvest();
+    }
+    SPH_HIP_TRY(hipGetLastError());
+  }
+};
+
+extern "C" {
+
+int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(cfg && out, SPH_HIP_EINVAL, "sph_engine_create: NULL argument");
+  SPH_REQUIRE(cfg->dim == 2 || cfg->dim == 3, SPH_HIP_EINVAL, "dimension must be 2 or 3");
+  SPH_REQUIRE(cfg->ntypes >= 1 && cfg->ntypes <= SPH_MAXTYPES, SPH_HIP_EINVAL,
+              "ntypes %d outside [1,%d]", cfg->ntypes, SPH_MAXTYPES);
+  const int pg = cfg->procgrid[0] * cfg->procgrid[1] * cfg->procgrid[2];
+  SPH_REQUIRE(pg == 1 || pg == 0, SPH_HIP_EINVAL,
+              "procgrid %dx%dx%d: multi-rank bricks go through sph_engine_comm_init",
+              cfg->procgrid[0], cfg->procgrid[1], cfg->procgrid[2]);
+  require_device(device);
+  sph_engine *e = new sph_engine;
+  try {
+    e->device = device;
+    e->cfg = *cfg;
+    const int nt = cfg->ntypes;
+    Coefs &c = e->hc;
+    c.ntypes = nt;
+    c.dim = cfg->dim;
+    for (int t = 0; t <= nt; t++) c.mass[t] = cfg->mass[t];
+    // per-type-pair tables are passed in the engine's fixed (SPH_MAXTYPES+1)^2 layout
+    auto repack = [&](const double *src, std::vector<double> &dst) {
+      dst.assign((nt + 1) * (nt + 1), 0.0);
+      for (int i = 0; i <= nt; i++)
+        for (int j = 0; j <= nt; j++) dst[i * (nt + 1) + j] = src[i * (SPH_MAXTYPES + 1) + j];
+    };
+    std::vector<double> cutmax((nt + 1) * (nt + 1), 0.0), tmpv, tmpc;
+    if (cfg->rhosum_nstep > 0) {
+      repack(cfg->rhosum_cut, tmpc);
+      coef_rhosum(c, cfg->dim, nt, tmpc.data(), cfg->mass);
+      for (size_t k = 0; k < cutmax.size(); k++) cutmax[k] = std::max(cutmax[k], tmpc[k]);
+    }
+    if (cfg->tait_on) {
+      repack(cfg->tait_cut, tmpc);
+      repack(cfg->tait_visc_coef, tmpv);
+      coef_tait(c, cfg->dim, nt, cfg->tait_visc, cfg->rho0, cfg->soundspeed, cfg->B,
+                tmpv.data(), tmpc.data(), cfg->mass);
+      for (size_t k = 0; k < cutmax.size(); k++) cutmax[k] = std::max(cutmax[k], tmpc[k]);
+      e->force_mode |= M_TAIT;
+    }
+    if (cfg->heat_on) {
+      repack(cfg->heat_cut, tmpc);
+      repack(cfg->heat_alpha, tmpv);
+      coef_heat(c, cfg->dim, nt, tmpv.data(), tmpc.data(), cfg->mass);
+      for (size_t k = 0; k < cutmax.size(); k++) cutmax[k] = std::max(cutmax[k], tmpc[k]);
+      e->force_mode |= M_HEAT;
+    }
+    // mirror upper triangle into a symmetric max-cut table (init_one semantics)
+    for (int i = 1; i <= nt; i++)
+      for (int j = 1; j < i; j++) cutmax[i * (nt + 1) + j] = cutmax[j * (nt + 1) + i];
+    e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin);
+    SPH_REQUIRE(e->cutneighmax > 0.0, SPH_HIP_EINVAL, "no pair style enabled / zero cutoff");
+    e->cutghost = e->cutneighmax;  // CommBrick::setup: cutghost = cutneighmax (:166)
+    for (int k = 0; k < 3; k++) {
+      e->box.lo[k] = cfg->boxlo[k];
+      e->box.hi[k] = cfg->boxhi[k];
+      e->box.prd[k] = cfg->boxhi[k] - cfg->boxlo[k];
+      e->box.periodic[k] = (k < cfg->dim) ? cfg->periodic[k] : 0;
+      e->sublo[k] = cfg->boxlo[k];
+      e->subhi[k] = cfg->boxhi[k];
+      if (e->box.periodic[k])
+        SPH_REQUIRE(e->cutghost < e->box.prd[k], SPH_HIP_EINVAL,
+                    "ghost cutoff %g >= box length %g in dim %d (multi-hop borders unsupported)",
+                    e->cutghost, e->box.prd[k], k);
+    }
+    e->sc.dtv = cfg->dt;
+    e->sc.dtf = 0.5 * cfg->dt * (cfg->ftm2v > 0 ? cfg->ftm2v : 1.0);  // fix_meso.cpp:63-66
+    for (int t = 0; t <= nt; t++) e->sc.mass[t] = cfg->mass[t];
+    e->sc.stationary_mask = cfg->stationary_mask;
+    e->setup_bins_geometry();
+    SPH_HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
+    SPH_HIP_TRY(hipMalloc(&e->dc, sizeof(Coefs)));
+    SPH_HIP_TRY(hipMemcpy(e->dc, &e->hc, sizeof(Coefs), hipMemcpyHostToDevice));
+    SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));
+  } catch (...) {
+    delete e;
+    throw;
+  }
+  *out = e;
+  SPH_API_END
+}
+
+int sph_engine_destroy(sph_engine *e) {
+  if (!e) return SPH_HIP_OK;
+  (void)hipSetDevice(e->device);
+  if (e->s) (void)hipStreamSynchronize(e->s);
+  for (auto *b : {&e->xt, &e->vr, &e->vel, &e->fo, &e->xt2, &e->vr2, &e->vel2, &e->fo2})
+    b->release();
+  e->aux.release();
+  e->aux2.release();
+  e->de.release();
+  e->de2.release();
+  for (auto *b : {&e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel, &e->bidx,
+                  &e->bidx2, &e->bstart, &e->bend, &e->cnt, &e->off, &e->nbr})
+    b->release();
+  e->bkey.release();
+  e->bkey2.release();
+  e->flags.release();
+  e->tmp.release();
+  for (auto &p : e->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto ev : e->evpool) (void)hipEventDestroy(ev);
+  if (e->h_scalar) (void)hipHostFree(e->h_scalar);
+  if (e->dc) (void)hipFree(e->dc);
+  if (e->s) (void)hipStreamDestroy(e->s);
+  delete e;
+  return SPH_HIP_OK;
+}
+
+int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
+                         const int *type, const double *rho, const double *en,
+                         const double *cv) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && n >= 0 && (n == 0 || (x && v && type && rho)), SPH_HIP_EINVAL,
+              "sph_engine_set_atoms: bad argument");
+  (void)cv;  // cv is carried only by the multiphase heat styles (not in this engine yet)
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  for (int i = 0; i < n; i++)
+    SPH_REQUIRE(type[i] >= 1 && type[i] <= e->cfg.ntypes, SPH_HIP_EINVAL,
+                "atom %d has type %d outside [1,%d]", i, type[i], e->cfg.ntypes);
+  e->nlocal = n;
+  e->nghost = 0;
+  e->ensure_atoms(n > 0 ? n : 1, false);
+  e->vel.reserve(n > 0 ? n : 1);
+  e->fo.reserve(n > 0 ? n : 1);
+  e->de.reserve(n > 0 ? n : 1);
+  e->tag.reserve(n > 0 ? n : 1);
+  std::vector<double4> hx(n), hv(n), hvel(n);
+  std::vector<double2> ha(n);
+  std::vector<int> ht(n);
+  for (int i = 0; i < n; i++) {
+    hx[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], type_bits(type[i]));
+    hv[i] = make_double4(0.0, 0.0, 0.0, rho[i]);  // vest = 0 until setup_pre_force
+    hvel[i] = make_double4(v[3 * i], v[3 * i + 1], v[3 * i + 2], 0.0);
+    ha[i] = make_double2(0.0, en ? en[i] : 0.0);
+    ht[i] = i;
+  }
+  if (n > 0) {
+    SPH_HIP_TRY(hipMemcpyAsync(e->xt.p, hx.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->vr.p, hv.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->vel.p, hvel.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->aux.p, ha.data(), n * sizeof(double2), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->tag.p, ht.data(), n * sizeof(int), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemsetAsync(e->fo.p, 0, n * sizeof(double4), e->s));
+    SPH_HIP_TRY(hipMemsetAsync(e->de.p, 0, n * sizeof(double), e->s));
+  }
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  e->setup_done = false;
+  SPH_API_END
+}
+
+int sph_engine_setup(sph_engine *e) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_setup: NULL engine");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  e->setup();
+  SPH_HIP_TRY(hipGetLastError());
+  SPH_API_END
+}
+
+int sph_engine_run(sph_engine *e, int nsteps) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && nsteps >= 0, SPH_HIP_EINVAL, "sph_engine_run: bad argument");
+  SPH_REQUIRE(e->setup_done, SPH_HIP_EINVAL, "sph_engine_run: call sph_engine_setup first");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  e->run(nsteps);
+  SPH_API_END
+}
+
+int sph_engine_pair_passes(sph_engine *e, int n) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && n >= 0, SPH_HIP_EINVAL, "sph_engine_pair_passes: bad argument");
+  SPH_REQUIRE(e->setup_done, SPH_HIP_EINVAL, "sph_engine_pair_passes: call setup first");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  for (int k = 0; k < n; k++) e->pair_compute(e->cfg.rhosum_nstep > 0);
+  SPH_HIP_TRY(hipGetLastError());
+  SPH_API_END
+}
+
+int sph_engine_nlocal(sph_engine *e) { return e ? e->nlocal : 0; }
+
+int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, double *en,
+                         double *f, double *drho, double *de, int *tag) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_get_atoms: NULL engine");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  const int n = e->nlocal;
+  if (n == 0) return SPH_HIP_OK;
+  std::vector<double4> hx(n), hv(n), hvel(n), hf(n);
+  std::vector<double2> ha(n);
+  std::vector<double> hde(n);
+  std::vector<int> ht(n);
+  SPH_HIP_TRY(hipMemcpyAsync(hx.data(), e->xt.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hv.data(), e->vr.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hvel.data(), e->vel.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hf.data(), e->fo.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(ha.data(), e->aux.p, n * sizeof(double2), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hde.data(), e->de.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  for (int i = 0; i < n; i++) {
+    const int t = ht[i];
+    SPH_REQUIRE(t >= 0 && t < n, SPH_HIP_ERUNTIME, "corrupt tag %d", t);
+    if (x) {
+      x[3 * t] = hx[i].x;
+      x[3 * t + 1] = hx[i].y;
+      x[3 * t + 2] = hx[i].z;
+    }
+    if (v) {
+      v[3 * t] = hvel[i].x;
+      v[3 * t + 1] = hvel[i].y;
+      v[3 * t + 2] = hvel[i].z;
+    }
+    if (rho) rho[t] = hv[i].w;
+    if (en) en[t] = ha[i].y;
+    if (f) {
+      f[3 * t] = hf[i].x;
+      f[3 * t + 1] = hf[i].y;
+      f[3 * t + 2] = hf[i].z;
+    }
+    if (drho) drho[t] = hf[i].w;
+    if (de) de[t] = hde[i];
+    if (tag) tag[i] = t;
+  }
+  SPH_API_END
+}
+
+int sph_engine_neighbor_counts(sph_engine *e, int *numneigh) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && numneigh, SPH_HIP_EINVAL, "sph_engine_neighbor_counts: bad argument");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  const int n = e->nlocal;
+  if (n == 0) return SPH_HIP_OK;
+  std::vector<int> hc(n), ht(n);
+  SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->cnt.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  for (int i = 0; i < n; i++) numneigh[ht[i]] = hc[i];
+  SPH_API_END
+}
+
+int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && st, SPH_HIP_EINVAL, "sph_engine_stats_get: bad argument");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  e->harvest();
+  st->step = e->step;
+  st->nlocal = e->nlocal;
+  st->nghost = e->nghost;
+  st->nbr_full = e->nbr_total;
+  st->nbr_builds = e->nbr_builds;
+  st->nbr_maxrow = e->nbr_maxrow;
+  st->ms_rhosum = e->ms[T_RHO];
+  st->ms_tait = e->ms[T_TAIT];
+  st->ms_heat = e->ms[T_HEAT];
+  st->ms_integrate = e->ms[T_INT];
+  st->ms_comm = e->ms[T_COMM];
+  st->ms_neigh = e->ms[T_NEIGH];
+  st->n_rhosum = e->nlaunch[T_RHO];
+  st->n_tait = e->nlaunch[T_TAIT];
+  st->n_heat = e->nlaunch[T_HEAT];
+  st->n_neigh = e->nlaunch[T_NEIGH];
+  SPH_API_END
+}
+
+int sph_engine_set_timing(sph_engine *e, int on) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_set_timing: NULL engine");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  e->harvest();
+  e->timing = on != 0;
+  for (int k = 0; k < T_NCLASS; k++) {
+    e->ms[k] = 0.0;
+    e->nlaunch[k] = 0;
+  }
+  SPH_API_END
+}
+
+int sph_engine_sync(sph_engine *e) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_sync: NULL engine");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  SPH_API_END
+}
+
+int sph_engine_comm_uid(void *uid128) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(false, SPH_HIP_ECOMM, "RCCL brick decomposition not built in this library yet");
+  (void)uid128;
+  SPH_API_END
+}
+
+int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank) {
+  SPH_API_BEGIN
+  (void)e;
+  (void)uid128;
+  (void)nranks;
+  (void)rank;
+  SPH_REQUIRE(false, SPH_HIP_ECOMM, "RCCL brick decomposition not built in this library yet");
+  SPH_API_END
+}
+
+}  // extern "C"

@@ -338,3 +338,158 @@ def reverse_comm(g: Ghosted, f=None, drho=None, de=None):
                            None if f is None else f.ctypes.data,
                            None if drho is None else drho.ctypes.data,
                            None if de is None else de.ctypes.data)
+
+
+# ---------------------------------------------------------------------------------------
+# Reference-faithful Verlet driver over the C restatement (one process, newton on, half
+# lists derived from full ones, reverse comm of ghost forces) -- the CPU twin of the
+# device engine's step, used as the multi-step parity oracle.
+#   Verlet::setup  src/verlet.cpp:88-139      Verlet::run  src/verlet.cpp:222-308
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Physics:
+    """Hybrid/overlay pair stack of the BASELINE configs (per-type (nt+1), per-pair
+    (nt+1,nt+1) tables, 1-based)."""
+
+    skin: float = 0.3
+    dt: float = 1e-3
+    every: int = 10
+    rhosum_nstep: int = 1
+    rhosum_cut: np.ndarray | None = None
+    tait: bool = True
+    morris: bool = False
+    rho0: np.ndarray | None = None
+    c0: np.ndarray | None = None
+    visc: np.ndarray | None = None
+    tait_cut: np.ndarray | None = None
+    heat: bool = False
+    alpha: np.ndarray | None = None
+    heat_cut: np.ndarray | None = None
+
+    def cutmax(self, nt):
+        cm = np.zeros((nt + 1, nt + 1))
+        for on, c in ((self.rhosum_nstep > 0, self.rhosum_cut), (self.tait, self.tait_cut),
+                      (self.heat, self.heat_cut)):
+            if on and c is not None:
+                cm = np.maximum(cm, np.asarray(c))
+        # init_one mirrors the upper triangle
+        for i in range(nt + 1):
+            for j in range(i):
+                cm[i, j] = cm[j, i]
+        return cm
+
+
+def c2_physics(h=3.0) -> Physics:
+    """rhosum(nstep 1, h) + taitwater(rho0 1, c0 10, visc 0.1, h), m=1."""
+    t = np.zeros((2, 2))
+    t[1, 1] = h
+    v = np.zeros((2, 2))
+    v[1, 1] = 0.1
+    return Physics(rhosum_cut=t.copy(), rho0=np.array([0.0, 1.0]), c0=np.array([0.0, 10.0]),
+                   visc=v, tait_cut=t.copy())
+
+
+def c3_physics(h=3.0) -> Physics:
+    """two types, taitwater/morris (rho0 1|0.5, c0 10, visc 0.01, h) +
+    heatconduction (D 0.1, h); no rhosum."""
+    t = np.zeros((3, 3))
+    t[1:, 1:] = h
+    v = np.zeros((3, 3))
+    v[1:, 1:] = 0.01
+    a = np.zeros((3, 3))
+    a[1:, 1:] = 0.1
+    return Physics(rhosum_nstep=0, rhosum_cut=None, morris=True, rho0=np.array([0.0, 1.0, 0.5]),
+                   c0=np.array([0.0, 10.0, 10.0]), visc=v, tait_cut=t.copy(), heat=True,
+                   alpha=a, heat_cut=t.copy())
+
+
+class RefRun:
+    """Owned state + the reference's per-step sequence, computed by the C restatement."""
+
+    def __init__(self, sysm: System, ph: Physics):
+        self.s = sysm.copy()
+        self.ph = ph
+        nt = sysm.ntypes
+        self.cns, self.cutneighmax = cutneighsq(nt, ph.cutmax(nt), ph.skin)
+        n = sysm.n
+        self.vest = np.zeros((n, 3))          # AtomVecMeso::create_atom: vest = 0
+        self.f = np.zeros((n, 3))
+        self.drho = np.zeros(n)
+        self.de = np.zeros(n)
+        self.step = 0
+        self.last_build = 0
+        self.dtf = 0.5 * ph.dt
+        self.B = None if ph.rho0 is None else ph.c0 * ph.c0 * ph.rho0 / 7.0
+
+    # -- helpers -------------------------------------------------------------------------
+    def _build(self):
+        s = self.s
+        lib().orc_pbc(C.byref(s.domain()), s.n, s.x)
+        self.g = borders(s, self.cutneighmax)
+        self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
+        self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
+        # ghost copies of the border-packed per-atom fields
+        self.vest_all = self.g.gather(self.vest)
+        self.rho_all = self.g.gather(s.rho)
+        self.e_all = self.g.gather(s.e)
+
+    def _forward(self):
+        g, s = self.g, self.s
+        d = s.domain()
+        xa = g.x
+        xa[:s.n] = s.x
+        self.vest_all = self.g.gather(self.vest)
+        self.rho_all = self.g.gather(s.rho)
+        self.e_all = self.g.gather(s.e)
+        lib().orc_forward_comm(C.byref(d), g.nlocal, g.nghost, g.owner,
+                               np.ascontiguousarray(g.image.ravel()), xa, None, None, None)
+
+    def _force(self):
+        s, g, ph = self.s, self.g, self.ph
+        nt = s.ntypes
+        nall = g.nall
+        g.x[:s.n] = s.x
+        if ph.rhosum_nstep > 0 and self.step % ph.rhosum_nstep == 0:
+            s.rho[:] = rhosum(s.dim, g, nt, s.mass, ph.rhosum_cut, self.foff, self.fnb)
+            self.rho_all = g.gather(s.rho)       # forward_comm_pair
+        f = np.zeros((nall, 3))
+        drho = np.zeros(nall)
+        de = np.zeros(nall)
+        if ph.tait:
+            f, drho, de = taitwater(s.dim, g, nt, 1, self.vest_all, self.rho_all, s.mass, ph.rho0,
+                                    ph.c0, ph.visc, ph.tait_cut, self.hoff, self.hnb,
+                                    morris=ph.morris, B=self.B)
+        if ph.heat:
+            de += heatconduction(s.dim, g, nt, 1, self.e_all, self.rho_all, s.mass, ph.alpha,
+                                 ph.heat_cut, self.hoff, self.hnb)
+        reverse_comm(g, f, drho, de)
+        self.f = f[:s.n].copy()
+        self.drho = drho[:s.n].copy()
+        self.de = de[:s.n].copy()
+
+    # -- Verlet --------------------------------------------------------------------------
+    def setup(self):
+        self.step = 0
+        self._build()                             # borders before setup_pre_force
+        self.vest[:] = self.s.v                   # FixMeso::setup_pre_force (owned only;
+        self.vest_all[:self.s.n] = self.vest      # ghosts keep their border-time vest)
+        self._force()
+        self.last_build = 0
+
+    def run(self, nsteps):
+        s, L = self.s, lib()
+        for _ in range(nsteps):
+            self.step += 1
+            L.orc_meso_initial(s.n, self.ph.dt, self.dtf, s.type, s.mass, None, s.x, s.v,
+                               self.f, self.vest, s.rho, self.drho, s.e, self.de)
+            if (self.step - self.last_build) % self.ph.every == 0:
+                self._build()
+                self.last_build = self.step
+            else:
+                self._forward()
+            self._force()
+            L.orc_meso_final(s.n, self.dtf, s.type, s.mass, None, s.v, self.f, s.rho,
+                             self.drho, s.e, self.de)
+
+    def numneigh_full(self):
+        return np.diff(self.foff).astype(np.int32)

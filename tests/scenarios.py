@@ -1,0 +1,54 @@
+"""Standard systems of the parity tests (shrunk to sizes the oracle
+finishes in seconds) and the oracle evaluations the HIP path is compared against."""
+from __future__ import annotations
+
+import numpy as np
+
+import pyoracle as po
+
+
+def c2_system(n=8, seed=12345, dim=3):
+    return po.cubic_lattice(n, seed=seed, dim=dim)
+
+
+def c3_system(n=8, seed=12345):
+    return po.cubic_lattice(n, seed=seed, ntypes=2, type2_frac=0.5, mass=(1.0, 0.5),
+                            rho=(1.0, 0.5), e=(1.0, 2.0))
+
+
+def prepared(sysm, ph: po.Physics, rho_jitter=0.02, vseed=7):
+    """Owned+ghost atoms, full and half lists, and per-atom fields with some spread in rho
+    and e (so the EOS / heat terms are exercised), as the pair styles see them."""
+    nt = sysm.ntypes
+    cns, cmax = po.cutneighsq(nt, ph.cutmax(nt), ph.skin)
+    g = po.borders(sysm, cmax)
+    foff, fnb = po.neigh_full(sysm.dim, g, nt, cns)
+    hoff, hnb = po.half_from_full(g, foff, fnb)
+    rng = np.random.default_rng(vseed)
+    rho = sysm.rho * (1.0 + rho_jitter * rng.uniform(-1, 1, sysm.n))
+    e = sysm.e + 0.1 * rng.uniform(-1, 1, sysm.n)
+    vest = sysm.v + 0.05 * rng.normal(size=sysm.v.shape)
+    if sysm.dim == 2:
+        vest[:, 2] = 0.0
+    return dict(g=g, foff=foff, fnb=fnb, hoff=hoff, hnb=hnb, cns=cns, cmax=cmax,
+                rho_all=g.gather(rho), e_all=g.gather(e), vest_all=g.gather(vest))
+
+
+def oracle_forces(sysm, ph: po.Physics, P, newton=1, reverse=True):
+    """Reference semantics: half list, Newton-3 scatter, then reverse comm into owners."""
+    g = P["g"]
+    nt = sysm.ntypes
+    B = ph.c0 * ph.c0 * ph.rho0 / 7.0
+    f = np.zeros((g.nall, 3))
+    drho = np.zeros(g.nall)
+    de = np.zeros(g.nall)
+    if ph.tait:
+        f, drho, de = po.taitwater(sysm.dim, g, nt, newton, P["vest_all"], P["rho_all"],
+                                   sysm.mass, ph.rho0, ph.c0, ph.visc, ph.tait_cut, P["hoff"],
+                                   P["hnb"], morris=ph.morris, B=B)
+    if ph.heat:
+        de = de + po.heatconduction(sysm.dim, g, nt, newton, P["e_all"], P["rho_all"], sysm.mass,
+                                    ph.alpha, ph.heat_cut, P["hoff"], P["hnb"])
+    if reverse:
+        po.reverse_comm(g, f, drho, de)
+    return f, drho, de

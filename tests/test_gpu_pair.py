@@ -1,0 +1,152 @@
+"""GPU parity of the pair-style layer (sph_hip_* C ABI): the kernels run on LAMMPS-shaped
+inputs (owned+ghost arrays and a NeighList) and must reproduce the reference loops
+(pair_sph_rhosum.cpp:66-204, pair_sph_taitwater.cpp:53-200,
+pair_sph_taitwater_morris.cpp:52-200, pair_sph_heatconduction.cpp:47-134) as restated in
+oracle/sph_oracle.c.  Tolerance: 1e-10 normwise relative (BASELINE.json north_star);
+the FULL-list path changes only the summation order, the HALF path adds atomic ordering."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+from conftest import elem_rel_err, rel_err
+from scenarios import c2_system, c3_system, oracle_forces, prepared
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def _ctx(sph_amd, sysm, ph, P, newton=1):
+    ctx = sph_amd.PairContext(sysm.dim, sysm.ntypes, newton)
+    g = P["g"]
+    ctx.atoms(g.nlocal, g.nghost, g.x, g.type, vest=P["vest_all"], rho=P["rho_all"], e=P["e_all"])
+    if ph.rhosum_nstep > 0:
+        ctx.rhosum_coeff(ph.rhosum_cut, sysm.mass)
+    if ph.tait:
+        ctx.taitwater_coeff(ph.rho0, ph.c0, ph.c0 * ph.c0 * ph.rho0 / 7.0, ph.visc, ph.tait_cut,
+                            sysm.mass, morris=ph.morris)
+    if ph.heat:
+        ctx.heatconduction_coeff(ph.alpha, ph.heat_cut, sysm.mass)
+    return ctx
+
+
+@pytest.mark.parametrize("dim", [3, 2])
+def test_rhosum_full_list(gpu, sph_amd, dim):
+    s = c2_system(8 if dim == 3 else 24, dim=dim)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, P["foff"], P["fnb"])
+    rho = ctx.rhosum(np.zeros(P["g"].nall))[:s.n]
+    want = po.rhosum(dim, P["g"], 1, s.mass, ph.rhosum_cut, P["foff"], P["fnb"])
+    assert rel_err(rho, want) < 1e-13
+    assert elem_rel_err(rho, want) < 1e-13
+
+
+@pytest.mark.parametrize("dim", [3, 2])
+def test_taitwater_full_list(gpu, sph_amd, dim):
+    s = c2_system(8 if dim == 3 else 24, dim=dim)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, P["foff"], P["fnb"])
+    nall = P["g"].nall
+    f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    ctx.taitwater(f, drho, de)
+    wf, wd, we = oracle_forces(s, ph, P)
+    n = s.n
+    assert rel_err(f[:n], wf[:n]) < TOL
+    assert rel_err(drho[:n], wd[:n]) < TOL
+    assert rel_err(de[:n], we[:n]) < TOL
+    # full list: ghosts untouched
+    assert not f[n:].any() and not drho[n:].any() and not de[n:].any()
+
+
+def test_taitwater_half_list_newton_scatter(gpu, sph_amd):
+    """HALF list (LAMMPS' default request): ghosts receive their Newton-3 share exactly as
+    in the reference, before reverse comm."""
+    s = c2_system(8)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_csr(sph_amd.SPH_LIST_HALF, P["hoff"], P["hnb"])
+    nall = P["g"].nall
+    f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    vir = np.zeros(6)
+    ctx.taitwater(f, drho, de, virial=vir)
+    wf, wd, we = oracle_forces(s, ph, P, reverse=False)
+    assert rel_err(f, wf) < TOL
+    assert rel_err(drho, wd) < TOL
+    assert rel_err(de, we) < TOL
+    _, _, _, wvir = po.taitwater(3, P["g"], 1, 1, P["vest_all"], P["rho_all"], s.mass, ph.rho0,
+                                 ph.c0, ph.visc, ph.tait_cut, P["hoff"], P["hnb"], virial=True)
+    assert rel_err(vir, wvir) < TOL
+
+
+def test_morris_heat_two_types(gpu, sph_amd):
+    s = c3_system(8)
+    ph = po.c3_physics(3.0)
+    P = prepared(s, ph)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, P["foff"], P["fnb"])
+    nall = P["g"].nall
+    f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    ctx.taitwater(f, drho, de)
+    ctx.heatconduction(de)
+    wf, wd, we = oracle_forces(s, ph, P)
+    n = s.n
+    assert rel_err(f[:n], wf[:n]) < TOL
+    assert rel_err(drho[:n], wd[:n]) < TOL
+    assert rel_err(de[:n], we[:n]) < TOL
+
+
+def test_heat_half_list(gpu, sph_amd):
+    s = c3_system(7)
+    ph = po.c3_physics(3.0)
+    P = prepared(s, ph)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_csr(sph_amd.SPH_LIST_HALF, P["hoff"], P["hnb"])
+    nall = P["g"].nall
+    de = np.zeros(nall)
+    ctx.heatconduction(de)
+    want = po.heatconduction(3, P["g"], 2, 1, P["e_all"], P["rho_all"], s.mass, ph.alpha,
+                             ph.heat_cut, P["hoff"], P["hnb"])
+    assert rel_err(de, want) < TOL
+
+
+def test_lammps_neighlist_form(gpu, sph_amd):
+    """sph_hip_list with ilist/numneigh/firstneigh (+ NEIGHMASK bits set) == CSR path."""
+    s = c2_system(6)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    foff, fnb = P["foff"], P["fnb"]
+    n = s.n
+    ilist = np.arange(n - 1, -1, -1, dtype=np.int32)  # non-identity ilist
+    numneigh = np.diff(foff).astype(np.int32)
+    rows = [(fnb[foff[i]:foff[i + 1]] | (1 << 30)).astype(np.int32) for i in range(n)]
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.list_lammps(sph_amd.SPH_LIST_FULL, ilist, numneigh, rows)
+    rho = ctx.rhosum(np.zeros(P["g"].nall))[:n]
+    want = po.rhosum(3, P["g"], 1, s.mass, ph.rhosum_cut, foff, fnb)
+    assert rel_err(rho, want) < 1e-13
+
+
+def test_edge_cases(gpu, sph_amd):
+    ph = po.c2_physics(3.0)
+    ctx = sph_amd.PairContext(3, 1, 1)
+    # empty system
+    ctx.atoms(0, 0, np.zeros((0, 3)), np.zeros(0, np.int32))
+    ctx.rhosum_coeff(ph.rhosum_cut, np.array([0.0, 1.0]))
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, np.zeros(1, np.int64), np.zeros(0, np.int32))
+    ctx.rhosum(np.zeros(1))
+    # isolated atoms: rho = self term only, zero forces
+    x = np.array([[0.0, 0.0, 0.0], [50.0, 0.0, 0.0]])
+    ctx.atoms(2, 0, x, np.ones(2, np.int32), vest=np.zeros((2, 3)), rho=np.ones(2), e=np.zeros(2))
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, np.zeros(3, np.int64), np.zeros(0, np.int32))
+    rho = ctx.rhosum(np.zeros(2))
+    assert np.allclose(rho, 2.1541870227086614782 / 27.0, rtol=1e-15)
+    # bad inputs fail loudly with EINVAL
+    with pytest.raises(sph_amd.HipError) as ei:
+        ctx.atoms(1, 0, np.zeros((1, 3)), np.array([5], np.int32))
+    assert ei.value.code == -1
+    with pytest.raises(sph_amd.HipError):
+        ctx.list_csr(sph_amd.SPH_LIST_FULL, np.array([0, 1], np.int64), np.array([7], np.int32))

@@ -1,0 +1,189 @@
+"""Benchmark of the MI355X USER-SPH engine on BASELINE.json's headline workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 100] [--no-cpu]
+
+Workload (BASELINE.json configs[1]): 1M particles on a jittered 100^3 cubic lattice,
+periodic, hybrid/overlay sph/rhosum (nstep 1, h 3) + sph/taitwater (rho0 1, c0 10,
+visc 0.1, h 3), skin 0.3, neighbor rebuild every 10 steps, dt 1e-3, fix meso.  A "step"
+is one full Verlet step of the device-resident engine (integrate, forward comm or
+rebuild, rhosum, forward rho, taitwater, integrate) with everything already in HBM.
+
+N > 1 ranks (torch.distributed.run) each advance their own 1M-particle box on their own
+GPU (weak scaling; see DESIGN.md "Multi-GPU" for the status of the brick decomposition).
+Rank 0 prints ONE JSON line.  `roofline` covers the dominant kernel (the taitwater force
+pass), timed live with HIP events recorded on the engine's stream; `cpu_baseline` is the
+oracle's C restatement timed on this host on a bounded sample (rank 0, N = 1 only).
+"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def load_pkg():
+    spec = importlib.util.spec_from_file_location(
+        "sph_amd", os.path.join(ROOT, "lammps-sph-multiphase_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["sph_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def make_system(n, seed):
+    """Same construction as oracle/pyoracle.cubic_lattice."""
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij"), -1)
+    g = g.reshape(-1, 3)
+    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]
+    x = g.astype(np.float64)
+    x += np.random.default_rng(seed).uniform(-0.1, 0.1, size=x.shape)
+    v = np.random.default_rng(4928459).normal(0.0, 0.01, size=x.shape)
+    N = x.shape[0]
+    return x, v, np.ones(N, np.int32), np.ones(N), np.zeros(N), np.ones(N)
+
+
+def c2_config(sph, n):
+    h = 3.0
+    cut = np.zeros((2, 2))
+    cut[1, 1] = h
+    visc = np.zeros((2, 2))
+    visc[1, 1] = 0.1
+    return sph.make_config(3, 1, [0.0, 0.0, 0.0], [float(n)] * 3, [1, 1, 1], [0.0, 1.0], 0.3,
+                           1e-3, neigh_every=10, rhosum=dict(nstep=1, cut=cut),
+                           tait=dict(rho0=np.array([0.0, 1.0]), c0=np.array([0.0, 10.0]),
+                                     visc=visc, cut=cut))
+
+
+def cpu_baseline(n_cpu, steps=2):
+    """Oracle C restatement (single core) on the same workload at n_cpu^3 particles:
+    `steps` non-rebuild steps + one neighbor rebuild amortised over 10 steps."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    s = po.cubic_lattice(n_cpu)
+    run = po.RefRun(s, po.c2_physics())
+    run.setup()
+    t0 = time.perf_counter()
+    run.run(steps)                       # steps 1..steps: forward comm, no rebuild
+    t_steps = (time.perf_counter() - t0) / steps
+    t0 = time.perf_counter()
+    run._build()
+    t_build = time.perf_counter() - t0
+    per_step = t_steps + t_build / 10.0
+    return {"value": s.n / per_step, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/sph_oracle.c (scalar C restatement) on {s.n} particles "
+                      f"(same C2 physics): {steps} steps timed ({t_steps:.3f} s/step) + one "
+                      f"neighbor rebuild ({t_build:.2f} s) amortised over neigh_every=10"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--n", type=int, default=100, help="lattice edge (n^3 particles per GPU)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-n", type=int, default=100)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    sph = load_pkg()
+    ndev = sph.device_count()
+    assert ndev > 0, "bench.py needs a HIP device"
+    dev = local % ndev
+
+    x, v, t, rho, e, cv = make_system(args.n, 12345 + rank)
+    eng = sph.Engine(c2_config(sph, args.n), device=dev)
+    eng.set_atoms(x, v, t, rho, e, cv)
+    eng.setup()
+    eng.run(args.warmup)
+    eng.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    eng.sync()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    eng.run(args.steps)
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    st = eng.stats()
+
+    nloc = st["nlocal"]
+    total_ps = nloc * world * args.steps / elapsed
+    n_full = st["nbr_full"] / max(nloc, 1)
+    n_half = n_full / 2.0
+    # algorithmic bytes per particle per pass (half-list CSR, int32, fp64)
+    bytes_tait = 104.0 + 4.0 * n_half
+    bytes_rho = 40.0 + 4.0 * n_half
+    ms_tait = st["ms_tait"] / max(st["n_tait"], 1)
+    ms_rho = st["ms_rhosum"] / max(st["n_rhosum"], 1)
+    ach_tait = bytes_tait * nloc / (ms_tait * 1e-3) / 1e9
+    ach_rho = bytes_rho * nloc / (ms_rho * 1e-3) / 1e9
+    ach_pair = (bytes_tait + bytes_rho) * nloc / ((ms_tait + ms_rho) * 1e-3) / 1e9
+
+    out = {
+        "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
+        "value": total_ps,
+        "unit": "particle-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (jittered sc lattice, gaussian velocities, seeded)",
+        "config": {"workload": f"C2: {nloc} particles/GPU cubic lattice, sph/rhosum + sph/taitwater, "
+                               "periodic, skin 0.3, rebuild every 10",
+                   "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
+                   "n_full_per_particle": n_full, "n_half_per_particle": n_half,
+                   "parallelism": f"{world} independent 1M boxes (one per GPU)"},
+        "roofline": {"bound": "hbm", "kernel": "k_force<TAIT> (sph/taitwater pass)",
+                     "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,
+                     "bytes_per_particle": bytes_tait, "ms_per_launch": ms_tait},
+        "kernels": {"rhosum": {"ms_per_launch": ms_rho, "achieved_GBs": ach_rho,
+                               "bytes_per_particle": bytes_rho},
+                    "rhosum+taitwater": {"achieved_GBs": ach_pair,
+                                         "frac": ach_pair / PEAK_HBM_GBS,
+                                         "kernel_particle_steps_per_s":
+                                             nloc / ((ms_tait + ms_rho) * 1e-3)},
+                    "neighbor_build_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
+                    "integrate_ms_per_step": st["ms_integrate"] / args.steps,
+                    "comm_ms_per_step": st["ms_comm"] / args.steps},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_n)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

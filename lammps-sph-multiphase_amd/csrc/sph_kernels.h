@@ -109,17 +109,25 @@ k_rhosum(int inum, const int *__restrict__ ilist, const int *__restrict__ off,
   const RhoPair *crow = s_c + it * nt1;
   const int beg = off[row], end = off[row + 1];
   double acc = 0.0;
-  for (int k = beg + lane; k < end; k += G) {
-    const int j = nbr[k];
-    const double4 xj = xt[j];
-    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    const RhoPair c = crow[type_of(xj.w)];
-    if (rsq < c.cutsq) {
-      double wf = 1.0 - rsq * c.ihsq;
-      wf = wf * wf;
-      wf = wf * wf;
-      acc += c.mK * wf;
+  constexpr int U = 4;
+  for (int k0 = beg + lane; k0 < end; k0 += G * U) {
+    int jv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) jv[u] = nbr[min(k0 + u * G, end - 1)];
+    double4 xj[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) xj[u] = xt[jv[u]];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      const RhoPair c = crow[type_of(xj[u].w)];
+      if (k0 + u * G < end && rsq < c.cutsq) {
+        double wf = 1.0 - rsq * c.ihsq;
+        wf = wf * wf;
+        wf = wf * wf;
+        acc += c.mK * wf;
+      }
     }
   }
   acc = group_sum<G>(acc);
@@ -149,6 +157,33 @@ static __global__ void k_eos(int n, const double4 *__restrict__ xt, const double
 // ------------------------------------------------------------------------------------
 enum { M_TAIT = 1, M_HEAT = 2, M_HALF = 4 };
 
+// neighbors processed per lane per iteration: all U index loads, then all U gathers are
+// issued before the first use, so a row costs ~2 dependent memory round trips per U
+// neighbors instead of 3 per neighbor (index -> position -> velocity/rho).
+constexpr int UNROLL = 4;
+
+// 1/b to ~1 ulp: v_rcp_f64 seed + two Newton steps (no IEEE fix-up path; operands here
+// are positive normal numbers).
+__device__ __forceinline__ double fast_rcp(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = fma(-b, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-b, y, 1.0);
+  return fma(y, e, y);
+}
+// sqrt(x) for x >= 0 (normal or zero) to ~1 ulp: v_rsq_f64 seed + Goldschmidt step +
+// correction, without the denormal rescaling of the libm path.
+__device__ __forceinline__ double fast_sqrt(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  const double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return x > 0.0 ? g : 0.0;
+}
+
 template <int G, int DIM, int VISC, int MODE>
 __global__ void __launch_bounds__(256)
 k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
@@ -160,6 +195,7 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr bool HALF = (MODE & M_HALF) != 0;
+  constexpr int U = UNROLL;
   __shared__ TaitPair s_t[TAIT ? NT2 : 1];
   __shared__ HeatPair s_h[HEAT ? NT2 : 1];
   __shared__ double s_mass[MAXT + 1];
@@ -181,87 +217,98 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
   const int beg = off[row], end = off[row + 1];
   double fx = 0.0, fy = 0.0, fz = 0.0, drho = 0.0, dE = 0.0;
   double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0, v4 = 0.0, v5 = 0.0;
-  for (int k = beg + lane; k < end; k += G) {
-    const int j = nbr[k];
-    const double4 xj = xt[j];
-    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    const int jt = type_of(xj.w);
-    const int pidx = it * nt1 + jt;
-    bool hit_t = false, hit_h = false;
-    if (TAIT) hit_t = rsq < s_t[pidx].cutsq;
-    if (HEAT) hit_h = rsq < s_h[pidx].cutsq;
-    if (!(hit_t || hit_h)) continue;
-    const double4 vj = vr[j];
-    const double2 aj = aux[j];
-    const double r = sqrt(rsq);
-    double jfx = 0.0, jfy = 0.0, jfz = 0.0, jdrho = 0.0, jdE = 0.0;
-    if (TAIT && hit_t) {
-      const TaitPair c = s_t[pidx];
-      double wfd = c.h - r;
-      wfd = c.wK * (wfd * wfd);
-      const double velx = vi.x - vj.x, vely = vi.y - vj.y, velz = vi.z - vj.z;
-      const double dvdr = dx * velx + dy * vely + dz * velz;
-      double fpair, deltaE, fvx = 0.0, fvy = 0.0, fvz = 0.0;
-      if (VISC == SPH_VISC_MONAGHAN) {
-        double fvisc = 0.0;
-        if (dvdr < 0.) {
-          const double mu = c.h * dvdr / (rsq + c.eps);
-          fvisc = c.viscC * mu / (vi.w + vj.w);
+  for (int k0 = beg + lane; k0 < end; k0 += G * U) {
+    int jv[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) jv[u] = nbr[min(k0 + u * G, end - 1)];
+    double4 xj[U], vj[U];
+    double2 aj[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      xj[u] = xt[jv[u]];
+      vj[u] = vr[jv[u]];
+      aj[u] = aux[jv[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int j = jv[u];
+      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      const int pidx = it * nt1 + type_of(xj[u].w);
+      const bool ok = k0 + u * G < end;
+      bool hit_t = false, hit_h = false;
+      if (TAIT) hit_t = ok && rsq < s_t[pidx].cutsq;
+      if (HEAT) hit_h = ok && rsq < s_h[pidx].cutsq;
+      if (!(hit_t || hit_h)) continue;
+      const double r = fast_sqrt(rsq);
+      double jfx = 0.0, jfy = 0.0, jfz = 0.0, jdrho = 0.0, jdE = 0.0;
+      if (TAIT && hit_t) {
+        const TaitPair c = s_t[pidx];
+        double wfd = c.h - r;
+        wfd = c.wK * (wfd * wfd);
+        const double velx = vi.x - vj[u].x, vely = vi.y - vj[u].y, velz = vi.z - vj[u].z;
+        const double dvdr = dx * velx + dy * vely + dz * velz;
+        double fpair, deltaE, fvx = 0.0, fvy = 0.0, fvz = 0.0;
+        if (VISC == SPH_VISC_MONAGHAN) {
+          // mu = h dvdr/(rsq+0.01h^2); fvisc = -visc (c_i+c_j) mu/(rho_i+rho_j), dvdr < 0
+          const double q = (c.viscC * c.h * dvdr) * fast_rcp((rsq + c.eps) * (vi.w + vj[u].w));
+          const double fvisc = dvdr < 0. ? q : 0.0;
+          fpair = c.mm * (ai.x + aj[u].x + fvisc) * wfd;
+          deltaE = -0.5 * fpair * dvdr;
+        } else {
+          // fvisc = 2 visc/(rho_i rho_j) * m_i m_j wfd
+          double fvisc = c.viscC * fast_rcp(vi.w * vj[u].w);
+          fvisc *= (-c.mm) * wfd;
+          fpair = c.mm * (ai.x + aj[u].x) * wfd;
+          deltaE = -0.5 * (fpair * dvdr + fvisc * (velx * velx + vely * vely + velz * velz));
+          fvx = velx * fvisc;
+          fvy = vely * fvisc;
+          fvz = velz * fvisc;
         }
-        fpair = c.mm * (ai.x + aj.x + fvisc) * wfd;
-        deltaE = -0.5 * fpair * dvdr;
-      } else {
-        double fvisc = c.viscC / (vi.w * vj.w);
-        fvisc *= (-c.mm) * wfd;
-        fpair = c.mm * (ai.x + aj.x) * wfd;
-        deltaE = -0.5 * (fpair * dvdr + fvisc * (velx * velx + vely * vely + velz * velz));
-        fvx = velx * fvisc;
-        fvy = vely * fvisc;
-        fvz = velz * fvisc;
+        const double tx = dx * fpair + fvx, ty = dy * fpair + fvy, tz = dz * fpair + fvz;
+        fx += tx;
+        fy += ty;
+        fz += tz;
+        drho += c.mj * dvdr * wfd;
+        dE += deltaE;
+        if (HALF) {
+          jfx = -tx;
+          jfy = -ty;
+          jfz = -tz;
+          jdrho = c.mi * dvdr * wfd;
+          jdE = deltaE;
+        }
+        if (virial) {
+          const double s = (!HALF || newton || j < nlocal) ? 1.0 : 0.5;
+          const double sf = HALF ? s * fpair : 0.5 * fpair;
+          v0 += sf * dx * dx;
+          v1 += sf * dy * dy;
+          v2 += sf * dz * dz;
+          v3 += sf * dx * dy;
+          v4 += sf * dx * dz;
+          v5 += sf * dy * dz;
+        }
       }
-      const double tx = dx * fpair + fvx, ty = dy * fpair + fvy, tz = dz * fpair + fvz;
-      fx += tx;
-      fy += ty;
-      fz += tz;
-      drho += c.mj * dvdr * wfd;
-      dE += deltaE;
-      if (HALF) {
-        jfx = -tx;
-        jfy = -ty;
-        jfz = -tz;
-        jdrho = c.mi * dvdr * wfd;
-        jdE = deltaE;
+      if (HEAT && hit_h) {
+        // 2 m_i m_j/(m_i+m_j) (rho_i+rho_j)/(rho_i rho_j) D (e_i-e_j) wfd
+        const HeatPair c = s_h[pidx];
+        double wfd = c.h - r;
+        wfd = c.wK * (wfd * wfd);
+        double deltaE = c.hmD;
+        deltaE *= (vi.w + vj[u].w) * fast_rcp(vi.w * vj[u].w);
+        deltaE *= (ai.y - aj[u].y) * wfd;
+        dE += deltaE;
+        if (HALF) jdE -= deltaE;
       }
-      if (virial) {
-        const double s = (!HALF || newton || j < nlocal) ? 1.0 : 0.5;
-        const double sf = HALF ? s * fpair : 0.5 * fpair;
-        v0 += sf * dx * dx;
-        v1 += sf * dy * dy;
-        v2 += sf * dz * dz;
-        v3 += sf * dx * dy;
-        v4 += sf * dx * dz;
-        v5 += sf * dy * dz;
+      if (HALF && (newton || j < nlocal)) {
+        if (TAIT) {
+          atomicAdd(&fo[j].x, jfx);
+          atomicAdd(&fo[j].y, jfy);
+          atomicAdd(&fo[j].z, jfz);
+          atomicAdd(&fo[j].w, jdrho);
+        }
+        atomicAdd(&de[j], jdE);
       }
-    }
-    if (HEAT && hit_h) {
-      const HeatPair c = s_h[pidx];
-      double wfd = c.h - r;
-      wfd = c.wK * (wfd * wfd);
-      double deltaE = c.hmD;
-      deltaE *= (vi.w + vj.w) / (vi.w * vj.w);
-      deltaE *= (ai.y - aj.y) * wfd;
-      dE += deltaE;
-      if (HALF) jdE -= deltaE;
-    }
-    if (HALF && (newton || j < nlocal)) {
-      if (TAIT) {
-        atomicAdd(&fo[j].x, jfx);
-        atomicAdd(&fo[j].y, jfy);
-        atomicAdd(&fo[j].z, jfz);
-        atomicAdd(&fo[j].w, jdrho);
-      }
-      atomicAdd(&de[j], jdE);
     }
   }
   if (TAIT) {

@@ -1,0 +1,33 @@
+"""Time the pair kernels (rhosum, taitwater) on the C2 1M workload for one engine config.
+Run once per SPH_GROUP value (the group width is read once per process)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    sph = bench.load_pkg()
+    x, v, t, rho, e, cv = bench.make_system(n, 12345)
+    eng = sph.Engine(bench.c2_config(sph, n))
+    eng.set_atoms(x, v, t, rho, e, cv)
+    eng.setup()
+    eng.run(5)
+    eng.pair_passes(3)
+    eng.sync()
+    eng.set_timing(True)
+    eng.pair_passes(reps)
+    st = eng.stats()
+    print(json.dumps({"group": os.environ.get("SPH_GROUP", "8"),
+                      "rhosum_ms": st["ms_rhosum"] / st["n_rhosum"],
+                      "tait_ms": st["ms_tait"] / st["n_tait"],
+                      "comm_ms": st["ms_comm"] / max(st["n_rhosum"], 1)}))
+
+
+if __name__ == "__main__":
+    main()

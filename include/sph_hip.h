@@ -147,6 +147,9 @@ typedef struct {
   int rank;                    /* my rank in the brick, x fastest */
   /* spatially sort owned particles at every rebuild (atom->sort analogue) */
   int sort;
+  /* pair-pass kernels: 0 = LDS-staged bins + 16-bit slot lists (default; needs sort),
+     1 = CSR rows with global gathers (the pair-style layer's kernels) */
+  int kernel_path;
 } sph_engine_config;
 
 typedef struct {
@@ -154,7 +157,9 @@ typedef struct {
   int nlocal, nghost;
   int64_t nbr_full;            /* entries in the device full list (owned rows) */
   int nbr_builds;
-  int nbr_maxrow;
+  int nbr_maxrow;              /* staged path: max owned atoms in one bin */
+  int staged;                  /* 1 if the last build produced LDS-staged lists */
+  int stage_max;               /* staged path: max atoms staged by one bin workgroup */
   double ms_rhosum, ms_tait, ms_heat, ms_integrate, ms_comm, ms_neigh; /* event-timed */
   int64_t n_rhosum, n_tait, n_heat, n_neigh;  /* launches timed */
 } sph_engine_stats;

@@ -58,6 +58,7 @@ class EngineConfig(C.Structure):
         ("heat_on", C.c_int), ("heat_alpha", C.c_double * _NT2), ("heat_cut", C.c_double * _NT2),
         ("gravity", C.c_double * 3),
         ("procgrid", C.c_int * 3), ("rank", C.c_int), ("sort", C.c_int),
+        ("kernel_path", C.c_int),
     ]
 
 
@@ -65,6 +66,7 @@ class EngineStats(C.Structure):
     _fields_ = [
         ("step", C.c_int64), ("nlocal", C.c_int), ("nghost", C.c_int),
         ("nbr_full", C.c_int64), ("nbr_builds", C.c_int), ("nbr_maxrow", C.c_int),
+        ("staged", C.c_int), ("stage_max", C.c_int),
         ("ms_rhosum", C.c_double), ("ms_tait", C.c_double), ("ms_heat", C.c_double),
         ("ms_integrate", C.c_double), ("ms_comm", C.c_double), ("ms_neigh", C.c_double),
         ("n_rhosum", C.c_int64), ("n_tait", C.c_int64), ("n_heat", C.c_int64),
@@ -224,7 +226,8 @@ def _pair_table(dst, tab, ntypes):
 
 def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every=10,
                 rhosum=None, tait=None, heat=None, gravity=(0.0, 0.0, 0.0),
-                stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0) -> EngineConfig:
+                stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0,
+                kernel_path=0) -> EngineConfig:
     """rhosum = dict(nstep, cut); tait = dict(rho0, c0, visc, cut, morris[, B]);
     heat = dict(alpha, cut); per-type arrays (ntypes+1), per-pair (ntypes+1, ntypes+1)."""
     c = EngineConfig()
@@ -239,6 +242,7 @@ def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every
         c.mass[t] = float(mass[t])
     c.stationary_mask = stationary_mask
     c.sort = sort
+    c.kernel_path = kernel_path
     if rhosum:
         c.rhosum_nstep = int(rhosum.get("nstep", 1))
         _pair_table(c.rhosum_cut, rhosum["cut"], ntypes)

@@ -53,7 +53,7 @@ inline void coef_tait(Coefs &c, int dim, int nt, int visc_variant, const double 
       t.mj = mass[j];
       t.mi = mass[i];
       const double v = upper(visc, nt, i, j);
-      t.viscC = (visc_variant == SPH_VISC_MONAGHAN) ? -v * (c0[i] + c0[j]) : 2 * v;
+      t.viscC = (visc_variant == SPH_VISC_MONAGHAN) ? -v * (c0[i] + c0[j]) * h : 2 * v;
       t.eps = 0.01 * h * h;
     }
 }

@@ -1,4 +1,4 @@
-// sph_dispatch.h -- runtime -> template dispatch for the pair kernels.
+// sph_dispatch.h -- runtime -> template dispatch for the CSR pair kernels.
 #pragma once
 #include "sph_kernels.h"
 #include "sph_util.h"
@@ -12,41 +12,52 @@ inline unsigned grid_for_rows(long rows, int G, int block = 256) {
   return (unsigned)((rows * (long)G + block - 1) / block);
 }
 
+struct RhoArgs {
+  int inum;
+  const int *ilist, *off, *nbr;
+  double4 *xf;
+  const int *ty;
+  double4 *vr;
+  double *rho_out;
+  const Coefs *cf;
+};
+
+template <int G, int DIM, bool EOS, bool NT1>
+inline void launch_rhosum_t(hipStream_t s, const RhoArgs &a) {
+  hipLaunchKernelGGL((k_rhosum<G, DIM, EOS, NT1>), dim3(grid_for_rows(a.inum, G)), dim3(256),
+                     0, s, a.inum, a.ilist, a.off, a.nbr, a.xf, a.ty, a.vr, a.rho_out, a.cf);
+}
+
 template <int G>
-inline void launch_rhosum_g(int dim, bool eos, hipStream_t s, int inum, const int *ilist,
-                            const int *off, const int *nbr, const double4 *xt, double4 *vr,
-                            double2 *aux, double *rho_out, const Coefs *cf) {
-  dim3 grid(grid_for_rows(inum, G)), block(256);
-  if (dim == 3) {
-    if (eos)
-      hipLaunchKernelGGL((k_rhosum<G, 3, true>), grid, block, 0, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf);
-    else
-      hipLaunchKernelGGL((k_rhosum<G, 3, false>), grid, block, 0, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf);
-  } else {
-    if (eos)
-      hipLaunchKernelGGL((k_rhosum<G, 2, true>), grid, block, 0, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf);
-    else
-      hipLaunchKernelGGL((k_rhosum<G, 2, false>), grid, block, 0, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf);
+inline void launch_rhosum_g(int dim, bool eos, bool nt1, hipStream_t s, const RhoArgs &a) {
+  const int code = (dim == 3 ? 4 : 0) | (eos ? 2 : 0) | (nt1 ? 1 : 0);
+  switch (code) {
+    case 7: launch_rhosum_t<G, 3, true, true>(s, a); break;
+    case 6: launch_rhosum_t<G, 3, true, false>(s, a); break;
+    case 5: launch_rhosum_t<G, 3, false, true>(s, a); break;
+    case 4: launch_rhosum_t<G, 3, false, false>(s, a); break;
+    case 3: launch_rhosum_t<G, 2, true, true>(s, a); break;
+    case 2: launch_rhosum_t<G, 2, true, false>(s, a); break;
+    case 1: launch_rhosum_t<G, 2, false, true>(s, a); break;
+    default: launch_rhosum_t<G, 2, false, false>(s, a); break;
   }
 }
 
-inline void launch_rhosum(int dim, bool eos, hipStream_t s, int inum, const int *ilist,
-                          const int *off, const int *nbr, const double4 *xt, double4 *vr,
-                          double2 *aux, double *rho_out, const Coefs *cf) {
-  if (inum <= 0) return;
+inline void launch_rhosum(int dim, bool eos, bool nt1, hipStream_t s, const RhoArgs &a) {
+  if (a.inum <= 0) return;
   switch (group_lanes()) {
-    case 4: launch_rhosum_g<4>(dim, eos, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf); break;
-    case 16: launch_rhosum_g<16>(dim, eos, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf); break;
-    case 32: launch_rhosum_g<32>(dim, eos, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf); break;
-    default: launch_rhosum_g<8>(dim, eos, s, inum, ilist, off, nbr, xt, vr, aux, rho_out, cf); break;
+    case 4: launch_rhosum_g<4>(dim, eos, nt1, s, a); break;
+    case 16: launch_rhosum_g<16>(dim, eos, nt1, s, a); break;
+    default: launch_rhosum_g<8>(dim, eos, nt1, s, a); break;
   }
 }
 
 struct ForceArgs {
   int inum, nlocal, newton;
   const int *ilist, *off, *nbr;
-  const double4 *xt, *vr;
-  const double2 *aux;
+  const double4 *xf, *vr;
+  const int *ty;
+  const double *en;
   double4 *fo;
   double *de;
   int accum;
@@ -55,51 +66,58 @@ struct ForceArgs {
   double *virial;
 };
 
-template <int G, int DIM, int VISC, int MODE>
+template <int G, int DIM, int VISC, int MODE, bool NT1>
 inline void launch_force_t(hipStream_t s, const ForceArgs &a) {
-  dim3 grid(grid_for_rows(a.inum, G)), block(256);
-  hipLaunchKernelGGL((k_force<G, DIM, VISC, MODE>), grid, block, 0, s, a.inum, a.nlocal, a.newton,
-                     a.ilist, a.off, a.nbr, a.xt, a.vr, a.aux, a.fo, a.de, a.accum, a.cf, a.gx,
-                     a.gy, a.gz, a.virial);
+  hipLaunchKernelGGL((k_force<G, DIM, VISC, MODE, NT1>), dim3(grid_for_rows(a.inum, G)),
+                     dim3(256), 0, s, a.inum, a.nlocal, a.newton, a.ilist, a.off, a.nbr, a.xf,
+                     a.vr, a.ty, a.en, a.fo, a.de, a.accum, a.cf, a.gx, a.gy, a.gz, a.virial);
 }
 
-template <int G, int DIM>
-inline void launch_force_gd(hipStream_t s, int visc, int mode, const ForceArgs &a) {
-  // supported mode combinations
-  if (mode == M_TAIT) {
-    if (visc == SPH_VISC_MORRIS) launch_force_t<G, DIM, 1, M_TAIT>(s, a);
-    else launch_force_t<G, DIM, 0, M_TAIT>(s, a);
-  } else if (mode == (M_TAIT | M_HEAT)) {
-    if (visc == SPH_VISC_MORRIS) launch_force_t<G, DIM, 1, M_TAIT | M_HEAT>(s, a);
-    else launch_force_t<G, DIM, 0, M_TAIT | M_HEAT>(s, a);
-  } else if (mode == M_HEAT) {
-    launch_force_t<G, DIM, 0, M_HEAT>(s, a);
-  } else if (mode == (M_TAIT | M_HALF)) {
-    if (visc == SPH_VISC_MORRIS) launch_force_t<G, DIM, 1, M_TAIT | M_HALF>(s, a);
-    else launch_force_t<G, DIM, 0, M_TAIT | M_HALF>(s, a);
-  } else if (mode == (M_TAIT | M_HEAT | M_HALF)) {
-    if (visc == SPH_VISC_MORRIS) launch_force_t<G, DIM, 1, M_TAIT | M_HEAT | M_HALF>(s, a);
-    else launch_force_t<G, DIM, 0, M_TAIT | M_HEAT | M_HALF>(s, a);
-  } else if (mode == (M_HEAT | M_HALF)) {
-    launch_force_t<G, DIM, 0, M_HEAT | M_HALF>(s, a);
-  } else {
-    SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", mode);
+template <int G, int DIM, bool NT1>
+inline void launch_force_gdn(hipStream_t s, int visc, int mode, const ForceArgs &a) {
+  const bool mor = visc == SPH_VISC_MORRIS;
+  switch (mode) {
+    case M_TAIT:
+      if (mor) launch_force_t<G, DIM, 1, M_TAIT, NT1>(s, a);
+      else launch_force_t<G, DIM, 0, M_TAIT, NT1>(s, a);
+      break;
+    case M_TAIT | M_HEAT:
+      if (mor) launch_force_t<G, DIM, 1, M_TAIT | M_HEAT, NT1>(s, a);
+      else launch_force_t<G, DIM, 0, M_TAIT | M_HEAT, NT1>(s, a);
+      break;
+    case M_HEAT: launch_force_t<G, DIM, 0, M_HEAT, NT1>(s, a); break;
+    case M_TAIT | M_HALF:
+      if (mor) launch_force_t<G, DIM, 1, M_TAIT | M_HALF, NT1>(s, a);
+      else launch_force_t<G, DIM, 0, M_TAIT | M_HALF, NT1>(s, a);
+      break;
+    case M_TAIT | M_HEAT | M_HALF:
+      if (mor) launch_force_t<G, DIM, 1, M_TAIT | M_HEAT | M_HALF, NT1>(s, a);
+      else launch_force_t<G, DIM, 0, M_TAIT | M_HEAT | M_HALF, NT1>(s, a);
+      break;
+    case M_HEAT | M_HALF: launch_force_t<G, DIM, 0, M_HEAT | M_HALF, NT1>(s, a); break;
+    default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", mode);
   }
 }
 
 template <int G>
-inline void launch_force_g(int dim, hipStream_t s, int visc, int mode, const ForceArgs &a) {
-  if (dim == 3) launch_force_gd<G, 3>(s, visc, mode, a);
-  else launch_force_gd<G, 2>(s, visc, mode, a);
+inline void launch_force_g(int dim, bool nt1, hipStream_t s, int visc, int mode,
+                           const ForceArgs &a) {
+  if (dim == 3) {
+    if (nt1) launch_force_gdn<G, 3, true>(s, visc, mode, a);
+    else launch_force_gdn<G, 3, false>(s, visc, mode, a);
+  } else {
+    if (nt1) launch_force_gdn<G, 2, true>(s, visc, mode, a);
+    else launch_force_gdn<G, 2, false>(s, visc, mode, a);
+  }
 }
 
-inline void launch_force(int dim, hipStream_t s, int visc, int mode, const ForceArgs &a) {
+inline void launch_force(int dim, bool nt1, hipStream_t s, int visc, int mode,
+                         const ForceArgs &a) {
   if (a.inum <= 0) return;
   switch (group_lanes()) {
-    case 4: launch_force_g<4>(dim, s, visc, mode, a); break;
-    case 16: launch_force_g<16>(dim, s, visc, mode, a); break;
-    case 32: launch_force_g<32>(dim, s, visc, mode, a); break;
-    default: launch_force_g<8>(dim, s, visc, mode, a); break;
+    case 4: launch_force_g<4>(dim, nt1, s, visc, mode, a); break;
+    case 16: launch_force_g<16>(dim, nt1, s, visc, mode, a); break;
+    default: launch_force_g<8>(dim, nt1, s, visc, mode, a); break;
   }
 }
 

@@ -16,6 +16,7 @@
 
 #include "sph_coef.h"
 #include "sph_dispatch.h"
+#include "sph_bin_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_util.h"
 
@@ -47,18 +48,18 @@ struct sph_engine {
   bool setup_done = false;
   int last_build = 0;
 
-  // atoms (owned first, then ghosts)
-  DBuf<double4> xt, vr;
-  DBuf<double2> aux;
+  // atoms (owned first, then ghosts): layout of sph_kernels.h
+  DBuf<double4> xf, vr;
+  DBuf<double> en;
+  DBuf<int> ty;
   // owned only
   DBuf<double4> vel, fo;
   DBuf<double> de;
   DBuf<int> tag;
   // sort scratch
-  DBuf<double4> xt2, vr2, vel2, fo2;
-  DBuf<double2> aux2;
-  DBuf<double> de2;
-  DBuf<int> tag2;
+  DBuf<double4> xf2, vr2, vel2;
+  DBuf<double> en2;
+  DBuf<int> ty2, tag2;
   // ghosts
   DBuf<int> gowner, gimg;
   // borders scratch
@@ -73,6 +74,16 @@ struct sph_engine {
   DBuf<int> cnt, off, nbr;
   int64_t nbr_total = 0;
   int nbr_builds = 0, nbr_maxrow = 0;
+  // LDS-staged bin path
+  bool staged = false;
+  int stage_max = 0, rows_max = 0;
+  size_t lds_neigh = 0, lds_rho = 0, lds_force = 0;
+  DBuf<unsigned> okey, gkey;
+  DBuf<int> obeg, gbeg, binE, binS, mx, ccnt;
+  DBuf<long long> blen, boff;
+  DBuf<unsigned short> nbr16;
+  DBuf<int> gowner2, gimg2;
+  long long *h_total = nullptr;
   // cub scratch
   DBuf<unsigned char> tmp;
   // pinned host scalar
@@ -132,41 +143,144 @@ struct sph_engine {
   void tmp_reserve(size_t b) { tmp.reserve(b); }
 
   void ensure_atoms(size_t nall, bool keep) {
-    xt.reserve(nall, keep, s);
+    xf.reserve(nall, keep, s);
     vr.reserve(nall, keep, s);
-    aux.reserve(nall, keep, s);
+    en.reserve(nall, keep, s);
+    ty.reserve(nall, keep, s);
   }
+  bool nt1() const { return cfg.ntypes == 1; }
 
   // ------------------------------------------------------------------------------------
   void sort_owned() {
-    if (!cfg.sort || nlocal < 2) return;
+    if (nlocal < 1) return;
     const int n = nlocal;
     bkey.reserve(n);
     bkey2.reserve(n);
     bidx.reserve(n);
     bidx2.reserve(n);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, bn, xt.p, bkey.p, bidx.p);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p, bidx.p);
     size_t tb = 0;
     SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
     tmp_reserve(tb);
     SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
-    xt2.reserve(xt.cap);
+    xf2.reserve(xf.cap);
     vr2.reserve(vr.cap);
-    aux2.reserve(aux.cap);
-    vel2.reserve(n);
-    fo2.reserve(n);
-    de2.reserve(n);
-    tag2.reserve(n);
-    hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, xt.p, vr.p,
-                       aux.p, vel.p, tag.p, fo.p, de.p, xt2.p, vr2.p, aux2.p, vel2.p, tag2.p,
-                       fo2.p, de2.p);
-    std::swap(xt, xt2);
+    en2.reserve(en.cap);
+    ty2.reserve(ty.cap);
+    vel2.reserve(vel.cap);
+    tag2.reserve(tag.cap);
+    hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, xf.p, vr.p,
+                       en.p, ty.p, vel.p, tag.p, xf2.p, vr2.p, en2.p, ty2.p, vel2.p, tag2.p);
+    std::swap(xf, xf2);
     std::swap(vr, vr2);
-    std::swap(aux, aux2);
+    std::swap(en, en2);
+    std::swap(ty, ty2);
     std::swap(vel, vel2);
-    std::swap(fo, fo2);
-    std::swap(de, de2);
     std::swap(tag, tag2);
+    okey.reserve(n);
+    SPH_HIP_TRY(hipMemcpyAsync(okey.p, bkey2.p, n * sizeof(unsigned), hipMemcpyDeviceToDevice, s));
+  }
+
+  bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2; }
+
+  // order the ghost segment by bin too (the staged ranges need it contiguous)
+  void sort_ghosts() {
+    const int ng = nghost;
+    if (ng == 0) return;
+    bkey.reserve(ng);
+    bkey2.reserve(ng);
+    bidx.reserve(ng);
+    bidx2.reserve(ng);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p, bkey.p, bidx.p);
+    int endbit = 1;
+    while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, endbit, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, endbit, s));
+    xf2.reserve(ng);
+    vr2.reserve(ng);
+    en2.reserve(ng);
+    ty2.reserve(ng);
+    gowner2.reserve(ng);
+    gimg2.reserve(ng);
+    hipLaunchKernelGGL(k_permute_ghosts, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bidx2.p,
+                       xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p, xf2.p, vr2.p, en2.p, ty2.p,
+                       gowner2.p, gimg2.p);
+    SPH_HIP_TRY(hipMemcpyAsync(xf.p + nlocal, xf2.p, ng * sizeof(double4), hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(vr.p + nlocal, vr2.p, ng * sizeof(double4), hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(en.p + nlocal, en2.p, ng * sizeof(double), hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(ty.p + nlocal, ty2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(gowner.p, gowner2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(gimg.p, gimg2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
+    gkey.reserve(ng);
+    SPH_HIP_TRY(hipMemcpyAsync(gkey.p, bkey2.p, ng * sizeof(unsigned), hipMemcpyDeviceToDevice, s));
+  }
+
+  BinCtx bin_ctx() const {
+    BinCtx c;
+    c.bn = bn;
+    c.dim = cfg.dim;
+    c.nbins = nbins;
+    c.nlocal = nlocal;
+    c.obeg = obeg.p;
+    c.gbeg = gbeg.p;
+    return c;
+  }
+
+  // LDS-staged full list (16-bit slots, thread-major per bin); false if it does not fit
+  bool build_staged() {
+    const int n = nlocal, ng = nghost;
+    obeg.reserve(nbins + 1);
+    gbeg.reserve(nbins + 1);
+    binE.reserve(nbins + 1);
+    binS.reserve(nbins + 1);
+    blen.reserve(nbins + 1);
+    boff.reserve(nbins + 1);
+    mx.reserve(2);
+    cnt.reserve(n + 1);
+    gkey.reserve(ng > 0 ? ng : 1);
+    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, n, 0, okey.p, obeg.p);
+    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, ng, n, gkey.p, gbeg.p);
+    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 2 * sizeof(int), s));
+    const BinCtx c = bin_ctx();
+    hipLaunchKernelGGL(k_bin_sizes, dim3(blocks(nbins)), dim3(BLK), 0, s, c, binS.p, mx.p);
+    int hm[2];
+    SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    stage_max = hm[0];
+    rows_max = hm[1];
+    const bool nt = nt1(), heat = (force_mode & M_HEAT) != 0;
+    lds_neigh = kFixedBytes + kNeighCoefBytes + (size_t)stage_max * neigh_atom_bytes();
+    lds_rho = kFixedBytes + (nt ? 0 : kRhoCoefBytes) + (size_t)stage_max * rho_atom_bytes(nt);
+    lds_force = kFixedBytes + (nt ? 0 : kForceCoefBytes) + (size_t)stage_max * force_atom_bytes(heat, nt);
+    const size_t lds_cap = 160 * 1024;
+    if (rows_max > MAXROWS || stage_max >= 65535 || lds_neigh > lds_cap || lds_rho > lds_cap ||
+        lds_force > lds_cap)
+      return false;
+    hipLaunchKernelGGL((k_bin_neigh<false>), dim3(nbins), dim3(BT), lds_neigh, s, c, xf.p, ty.p,
+                       dc, cnt.p, binE.p, binS.p, (const long long *)nullptr,
+                       (unsigned short *)nullptr);
+    hipLaunchKernelGGL(k_bin_listlen, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, binE.p, blen.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, blen.p, boff.p, nbins + 1, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, blen.p, boff.p, nbins + 1, s));
+    SPH_HIP_TRY(hipMemcpyAsync(h_total, boff.p + nbins, sizeof(long long), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    const long long tot = *h_total;
+    nbr16.reserve(tot > 0 ? (size_t)tot : 1);
+    hipLaunchKernelGGL((k_bin_neigh<true>), dim3(nbins), dim3(BT), lds_neigh, s, c, xf.p, ty.p,
+                       dc, cnt.p, binE.p, binS.p, boff.p, nbr16.p);
+    // entries proper (without padding) = sum of row counts
+    size_t tb2 = 0;
+    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tb2, binE.p, mx.p, nbins, s));
+    tmp_reserve(tb2);
+    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(tmp.p, tb2, binE.p, mx.p, nbins, s));
+    nbr_total = read_scalar(mx.p);
+    nbr_maxrow = rows_max;
+    nbr_builds++;
+    return true;
   }
 
   int read_scalar(const int *dptr) {
@@ -199,7 +313,7 @@ struct sph_engine {
         shift = pbc * box.prd[d];
         flags.reserve(nlast);
         sel.reserve(nlast);
-        hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d, lo, hi, xt.p, flags.p);
+        hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d, lo, hi, xf.p, flags.p);
         hipcub::CountingInputIterator<int> it(0);
         size_t tb = 0;
         SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flags.p, sel.p, nsel.p, nlast, s));
@@ -211,7 +325,7 @@ struct sph_engine {
         gowner.reserve((size_t)nall + ns - nlocal, true, s);
         gimg.reserve((size_t)nall + ns - nlocal, true, s);
         hipLaunchKernelGGL(k_append_ghosts, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sel.p,
-                           nlocal, nall, d, pbc, shift, xt.p, vr.p, aux.p, gowner.p, gimg.p);
+                           nlocal, nall, d, pbc, shift, xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p);
         nall += ns;
       }
     }
@@ -248,7 +362,7 @@ struct sph_engine {
     bidx2.reserve(nall);
     bstart.reserve(nbins);
     bend.reserve(nbins);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bn, xt.p, bkey.p, bidx.p);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, bn, xf.p, bkey.p, bidx.p);
     int endbit = 1;
     while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
     size_t tb = 0;
@@ -263,13 +377,13 @@ struct sph_engine {
   void build_list() {
     constexpr int G = 8;
     const int n = nlocal;
-    cnt.reserve(n + 1);
+    ccnt.reserve(n + 1);
     off.reserve(n + 1);
     dim3 grid(grid_for_rows(n, G)), block(BLK);
     if (n > 0)
-      hipLaunchKernelGGL((k_neigh<G, false>), grid, block, 0, s, n, bn, cfg.dim, xt.p, bidx2.p,
-                         bstart.p, bend.p, dc, cnt.p, (const int *)nullptr, (int *)nullptr);
-    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, cnt.p, off.p);
+      hipLaunchKernelGGL((k_neigh<G, false>), grid, block, 0, s, n, bn, cfg.dim, xf.p, ty.p, bidx2.p,
+                         bstart.p, bend.p, dc, ccnt.p, (const int *)nullptr, (int *)nullptr);
+    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
     size_t tb = 0;
     SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, off.p, off.p, n + 1, s));
     tmp_reserve(tb);
@@ -279,26 +393,86 @@ struct sph_engine {
     SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
     nbr.reserve(tot > 0 ? tot : 1);
     if (n > 0)
-      hipLaunchKernelGGL((k_neigh<G, true>), grid, block, 0, s, n, bn, cfg.dim, xt.p, bidx2.p,
+      hipLaunchKernelGGL((k_neigh<G, true>), grid, block, 0, s, n, bn, cfg.dim, xf.p, ty.p, bidx2.p,
                          bstart.p, bend.p, dc, (int *)nullptr, off.p, nbr.p);
-    nbr_total = tot;
-    nbr_builds++;
+    if (!staged) {
+      nbr_total = tot;
+      nbr_builds++;
+    }
+  }
+
+  template <int DIM, bool NT1>
+  void bin_rhosum_t() {
+    auto k = k_bin_rhosum<DIM, NT1>;
+    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rho));
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_rho, s, bin_ctx(), xf.p, ty.p, vr.p, cnt.p,
+                       boff.p, nbr16.p, dc);
+  }
+  void launch_bin_rhosum() {
+    if (cfg.dim == 3) {
+      if (nt1()) bin_rhosum_t<3, true>(); else bin_rhosum_t<3, false>();
+    } else {
+      if (nt1()) bin_rhosum_t<2, true>(); else bin_rhosum_t<2, false>();
+    }
+  }
+  template <int DIM, int VISC, int MODE, bool NT1>
+  void bin_force_t() {
+    auto k = k_bin_force<DIM, VISC, MODE, NT1>;
+    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_force, s, bin_ctx(), xf.p, vr.p, ty.p,
+                       en.p, cnt.p, boff.p, nbr16.p, dc, fo.p, de.p, cfg.gravity[0],
+                       cfg.gravity[1], cfg.gravity[2]);
+  }
+  template <int DIM, bool NT1>
+  void bin_force_d() {
+    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
+    switch (force_mode) {
+      case M_TAIT:
+        if (mor) bin_force_t<DIM, 1, M_TAIT, NT1>(); else bin_force_t<DIM, 0, M_TAIT, NT1>();
+        break;
+      case M_TAIT | M_HEAT:
+        if (mor) bin_force_t<DIM, 1, M_TAIT | M_HEAT, NT1>();
+        else bin_force_t<DIM, 0, M_TAIT | M_HEAT, NT1>();
+        break;
+      case M_HEAT: bin_force_t<DIM, 0, M_HEAT, NT1>(); break;
+      default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", force_mode);
+    }
+  }
+  void launch_bin_force() {
+    if (cfg.dim == 3) {
+      if (nt1()) bin_force_d<3, true>(); else bin_force_d<3, false>();
+    } else {
+      if (nt1()) bin_force_d<2, true>(); else bin_force_d<2, false>();
+    }
+  }
+
+  // pbc + sort + borders + list(s); `need_csr` also builds the global-index CSR list
+  void build_all(bool need_csr) {
+    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
+    const bool st = want_staged();
+    if (st || cfg.sort) sort_owned();
+    borders();
+    staged = false;
+    if (st) {
+      sort_ghosts();
+      staged = build_staged();
+    }
+    if (!staged || need_csr) {
+      build_bins();
+      build_list();
+    }
   }
 
   void rebuild() {
     Scope t(this, T_NEIGH);
-    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xt.p);
-    sort_owned();
-    borders();
-    build_bins();
-    build_list();
+    build_all(false);
   }
 
   void forward() {
     if (nghost == 0) return;
     Scope t(this, T_COMM);
     hipLaunchKernelGGL(k_forward, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal, box,
-                       gowner.p, gimg.p, xt.p, vr.p, aux.p);
+                       gowner.p, gimg.p, xf.p, vr.p, en.p);
   }
 
   void pair_compute(bool do_rhosum, bool setup = false) {
@@ -306,19 +480,26 @@ struct sph_engine {
     if (do_rhosum) {
       {
         Scope t(this, T_RHO);
-        launch_rhosum(cfg.dim, true, s, nlocal, nullptr, off.p, nbr.p, xt.p, vr.p, aux.p,
-                      nullptr, dc);
+        if (staged) {
+          launch_bin_rhosum();
+        } else {
+          RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
+          launch_rhosum(cfg.dim, true, nt1(), s, ra);
+        }
       }
       if (nghost) {
         Scope t(this, T_COMM);
         hipLaunchKernelGGL(k_forward_rho, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost,
-                           nlocal, gowner.p, vr.p, aux.p);
+                           nlocal, gowner.p, xf.p, vr.p);
       }
     } else if (force_mode & M_TAIT) {
-      hipLaunchKernelGGL(k_eos, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xt.p, vr.p, aux.p, dc);
+      hipLaunchKernelGGL(k_eos, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vr.p, ty.p, dc);
     }
     if (force_mode && setup) {
       setup_forces_half();
+    } else if (force_mode && staged) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      launch_bin_force();
     } else if (force_mode) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       ForceArgs a{};
@@ -328,9 +509,10 @@ struct sph_engine {
       a.ilist = nullptr;
       a.off = off.p;
       a.nbr = nbr.p;
-      a.xt = xt.p;
+      a.xf = xf.p;
       a.vr = vr.p;
-      a.aux = aux.p;
+      a.ty = ty.p;
+      a.en = en.p;
       a.fo = fo.p;
       a.de = de.p;
       a.accum = 0;
@@ -339,7 +521,7 @@ struct sph_engine {
       a.gy = cfg.gravity[1];
       a.gz = cfg.gravity[2];
       a.virial = nullptr;
-      launch_force(cfg.dim, s, cfg.tait_visc, force_mode, a);
+      launch_force(cfg.dim, nt1(), s, cfg.tait_visc, force_mode, a);
     } else {
       SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, nlocal * sizeof(double4), s));
       SPH_HIP_TRY(hipMemsetAsync(de.p, 0, nlocal * sizeof(double), s));
@@ -355,7 +537,7 @@ struct sph_engine {
     hcnt.reserve(n + 1);
     hoff.reserve(n + 1);
     hipLaunchKernelGGL((k_half_from_full<false>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
-                       nbr.p, xt.p, hcnt.p, (const int *)nullptr, (int *)nullptr);
+                       nbr.p, xf.p, hcnt.p, (const int *)nullptr, (int *)nullptr);
     hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, hcnt.p, hoff.p);
     size_t tb = 0;
     SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hoff.p, hoff.p, n + 1, s));
@@ -364,7 +546,7 @@ struct sph_engine {
     const int tot = read_scalar(hoff.p + n);
     hnbr.reserve(tot > 0 ? tot : 1);
     hipLaunchKernelGGL((k_half_from_full<true>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
-                       nbr.p, xt.p, (int *)nullptr, hoff.p, hnbr.p);
+                       nbr.p, xf.p, (int *)nullptr, hoff.p, hnbr.p);
     fo.reserve(nall, true, s);
     de.reserve(nall, true, s);
     SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, nall * sizeof(double4), s));
@@ -375,20 +557,21 @@ struct sph_engine {
     a.newton = 1;
     a.off = hoff.p;
     a.nbr = hnbr.p;
-    a.xt = xt.p;
+    a.xf = xf.p;
     a.vr = vr.p;
-    a.aux = aux.p;
+    a.ty = ty.p;
+    a.en = en.p;
     a.fo = fo.p;
     a.de = de.p;
     a.cf = dc;
-    launch_force(cfg.dim, s, cfg.tait_visc, force_mode | M_HALF, a);
+    launch_force(cfg.dim, nt1(), s, cfg.tait_visc, force_mode | M_HALF, a);
     if (nghost)
       hipLaunchKernelGGL(k_reverse, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, n, gowner.p,
                          fo.p, de.p);
     // post_force body force (fix gravity style), as the full-list kernel applies it
     if (cfg.gravity[0] != 0.0 || cfg.gravity[1] != 0.0 || cfg.gravity[2] != 0.0)
       hipLaunchKernelGGL(k_add_gravity, dim3(blocks(n)), dim3(BLK), 0, s, n, sc,
-                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], xt.p, fo.p);
+                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], ty.p, fo.p);
     SPH_HIP_TRY(hipStreamSynchronize(s));  // scratch lists are freed on return
     hcnt.release();
     hoff.release();
@@ -403,13 +586,11 @@ struct sph_engine {
   void setup() {
     step = 0;
     Scope t(this, T_NEIGH);
-    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xt.p);
-    sort_owned();
-    borders();      // ghosts carry vest as it was before setup_pre_force (reference order)
-    build_bins();
-    build_list();
+    // borders() runs before setup_pre_force: ghosts carry vest as it was (reference order);
+    // the setup force pass needs the global-index list for its half-list walk
+    build_all(true);
     hipLaunchKernelGGL(k_vest_from_v, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                       cfg.stationary_mask, xt.p, vel.p, vr.p);
+                       cfg.stationary_mask, ty.p, vel.p, vr.p);
     pair_compute(rhosum_due(), /*setup=*/true);
     last_build = 0;
     setup_done = true;
@@ -422,7 +603,7 @@ struct sph_engine {
       {
         Scope t(this, T_INT);
         hipLaunchKernelGGL(k_initial_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                           sc, xt.p, vr.p, aux.p, vel.p, fo.p, de.p);
+                           sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
       }
       const int every = cfg.neigh_every > 0 ? cfg.neigh_every : 1;
       if ((step - last_build) % every == 0) {
@@ -435,7 +616,7 @@ struct sph_engine {
       {
         Scope t(this, T_INT);
         hipLaunchKernelGGL(k_final_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                           sc, xt.p, vr.p, aux.p, vel.p, fo.p, de.p);
+                           sc, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
       }
       if (timing && pending.size() > 4096) harvest();
     }
@@ -519,6 +700,7 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     SPH_HIP_TRY(hipMalloc(&e->dc, sizeof(Coefs)));
     SPH_HIP_TRY(hipMemcpy(e->dc, &e->hc, sizeof(Coefs), hipMemcpyHostToDevice));
     SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));
+    SPH_HIP_TRY(hipHostMalloc(&e->h_total, sizeof(long long)));
   } catch (...) {
     delete e;
     throw;
@@ -531,13 +713,11 @@ int sph_engine_destroy(sph_engine *e) {
   if (!e) return SPH_HIP_OK;
   (void)hipSetDevice(e->device);
   if (e->s) (void)hipStreamSynchronize(e->s);
-  for (auto *b : {&e->xt, &e->vr, &e->vel, &e->fo, &e->xt2, &e->vr2, &e->vel2, &e->fo2})
-    b->release();
-  e->aux.release();
-  e->aux2.release();
+  for (auto *b : {&e->xf, &e->vr, &e->vel, &e->fo, &e->xf2, &e->vr2, &e->vel2}) b->release();
+  e->en.release();
+  e->en2.release();
   e->de.release();
-  e->de2.release();
-  for (auto *b : {&e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel, &e->bidx,
+  for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel, &e->bidx,
                   &e->bidx2, &e->bstart, &e->bend, &e->cnt, &e->off, &e->nbr})
     b->release();
   e->bkey.release();
@@ -550,6 +730,14 @@ int sph_engine_destroy(sph_engine *e) {
   }
   for (auto ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->h_scalar) (void)hipHostFree(e->h_scalar);
+  if (e->h_total) (void)hipHostFree(e->h_total);
+  for (auto *b : {&e->obeg, &e->gbeg, &e->binE, &e->binS, &e->mx, &e->ccnt, &e->gowner2, &e->gimg2})
+    b->release();
+  e->okey.release();
+  e->gkey.release();
+  e->blen.release();
+  e->boff.release();
+  e->nbr16.release();
   if (e->dc) (void)hipFree(e->dc);
   if (e->s) (void)hipStreamDestroy(e->s);
   delete e;
@@ -575,20 +763,22 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   e->de.reserve(n > 0 ? n : 1);
   e->tag.reserve(n > 0 ? n : 1);
   std::vector<double4> hx(n), hv(n), hvel(n);
-  std::vector<double2> ha(n);
-  std::vector<int> ht(n);
+  std::vector<double> he(n);
+  std::vector<int> ht(n), hty(n);
   for (int i = 0; i < n; i++) {
-    hx[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], type_bits(type[i]));
+    hx[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
     hv[i] = make_double4(0.0, 0.0, 0.0, rho[i]);  // vest = 0 until setup_pre_force
     hvel[i] = make_double4(v[3 * i], v[3 * i + 1], v[3 * i + 2], 0.0);
-    ha[i] = make_double2(0.0, en ? en[i] : 0.0);
+    he[i] = en ? en[i] : 0.0;
     ht[i] = i;
+    hty[i] = type[i];
   }
   if (n > 0) {
-    SPH_HIP_TRY(hipMemcpyAsync(e->xt.p, hx.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->xf.p, hx.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
     SPH_HIP_TRY(hipMemcpyAsync(e->vr.p, hv.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
     SPH_HIP_TRY(hipMemcpyAsync(e->vel.p, hvel.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
-    SPH_HIP_TRY(hipMemcpyAsync(e->aux.p, ha.data(), n * sizeof(double2), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->en.p, he.data(), n * sizeof(double), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->ty.p, hty.data(), n * sizeof(int), hipMemcpyHostToDevice, e->s));
     SPH_HIP_TRY(hipMemcpyAsync(e->tag.p, ht.data(), n * sizeof(int), hipMemcpyHostToDevice, e->s));
     SPH_HIP_TRY(hipMemsetAsync(e->fo.p, 0, n * sizeof(double4), e->s));
     SPH_HIP_TRY(hipMemsetAsync(e->de.p, 0, n * sizeof(double), e->s));
@@ -636,14 +826,13 @@ int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, doubl
   const int n = e->nlocal;
   if (n == 0) return SPH_HIP_OK;
   std::vector<double4> hx(n), hv(n), hvel(n), hf(n);
-  std::vector<double2> ha(n);
-  std::vector<double> hde(n);
+  std::vector<double> hen(n), hde(n);
   std::vector<int> ht(n);
-  SPH_HIP_TRY(hipMemcpyAsync(hx.data(), e->xt.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hx.data(), e->xf.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(hv.data(), e->vr.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(hvel.data(), e->vel.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(hf.data(), e->fo.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
-  SPH_HIP_TRY(hipMemcpyAsync(ha.data(), e->aux.p, n * sizeof(double2), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hen.data(), e->en.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(hde.data(), e->de.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
@@ -661,7 +850,7 @@ int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, doubl
       v[3 * t + 2] = hvel[i].z;
     }
     if (rho) rho[t] = hv[i].w;
-    if (en) en[t] = ha[i].y;
+    if (en) en[t] = hen[i];
     if (f) {
       f[3 * t] = hf[i].x;
       f[3 * t + 1] = hf[i].y;
@@ -681,7 +870,8 @@ int sph_engine_neighbor_counts(sph_engine *e, int *numneigh) {
   const int n = e->nlocal;
   if (n == 0) return SPH_HIP_OK;
   std::vector<int> hc(n), ht(n);
-  SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->cnt.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->staged ? e->cnt.p : e->ccnt.p, n * sizeof(int),
+                             hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
   for (int i = 0; i < n; i++) numneigh[ht[i]] = hc[i];
@@ -699,6 +889,8 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->nbr_full = e->nbr_total;
   st->nbr_builds = e->nbr_builds;
   st->nbr_maxrow = e->nbr_maxrow;
+  st->staged = e->staged ? 1 : 0;
+  st->stage_max = e->stage_max;
   st->ms_rhosum = e->ms[T_RHO];
   st->ms_tait = e->ms[T_TAIT];
   st->ms_heat = e->ms[T_HEAT];

@@ -1,6 +1,7 @@
 // sph_engine_kernels.h -- streaming kernels of the device-resident step: FixMeso
-// integrate, Domain::pbc, CommBrick borders/forward comm on one process, binning and the
-// binned full-list build (Neighbor::full_bin semantics: rsq <= cutneighsq, j != i).
+// integrate, Domain::pbc, CommBrick borders/forward comm on one process, binning, the
+// spatial sort, and the binned full-list build (Neighbor::full_bin membership:
+// rsq <= cutneighsq, j != i).  Layout as in sph_kernels.h (xf, vr, ty, en).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -15,20 +16,21 @@ struct StepConst {
 };
 
 // FixMeso::initial_integrate (fix_meso.cpp:91-140) / FixMesoStationary (:71-90)
-static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restrict__ xt,
-                                    double4 *__restrict__ vr, double2 *__restrict__ aux,
-                                    double4 *__restrict__ vel, const double4 *__restrict__ fo,
-                                    const double *__restrict__ de) {
+static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restrict__ xf,
+                                           double4 *__restrict__ vr, double *__restrict__ en,
+                                           const int *__restrict__ ty,
+                                           double4 *__restrict__ vel,
+                                           const double4 *__restrict__ fo,
+                                           const double *__restrict__ de) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double4 x = xt[i];
-  const int t = type_of(x.w);
+  const int t = ty[i];
   double4 vv = vr[i];       // vest, rho
-  double2 a = aux[i];       // p/rho^2, e
   const double4 f = fo[i];  // fx, fy, fz, drho
-  a.y += sc.dtf * de[i];
+  en[i] += sc.dtf * de[i];
   vv.w += sc.dtf * f.w;
   if (!((sc.stationary_mask >> t) & 1)) {
+    double4 x = xf[i];
     double4 v = vel[i];
     const double dtfm = sc.dtf / sc.mass[t];
     vv.x = v.x + 2.0 * dtfm * f.x;
@@ -41,20 +43,20 @@ static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restr
     x.y += sc.dtv * v.y;
     x.z += sc.dtv * v.z;
     vel[i] = v;
-    xt[i] = x;
+    xf[i] = x;
   }
   vr[i] = vv;
-  aux[i] = a;
 }
 
 // FixMeso::final_integrate (fix_meso.cpp:144-180) / FixMesoStationary (:94-112)
-static __global__ void k_final_integrate(int n, StepConst sc, const double4 *__restrict__ xt,
-                                  double4 *__restrict__ vr, double2 *__restrict__ aux,
-                                  double4 *__restrict__ vel, const double4 *__restrict__ fo,
-                                  const double *__restrict__ de) {
+static __global__ void k_final_integrate(int n, StepConst sc, double4 *__restrict__ vr,
+                                         double *__restrict__ en, const int *__restrict__ ty,
+                                         double4 *__restrict__ vel,
+                                         const double4 *__restrict__ fo,
+                                         const double *__restrict__ de) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int t = type_of(xt[i].w);
+  const int t = ty[i];
   const double4 f = fo[i];
   if (!((sc.stationary_mask >> t) & 1)) {
     double4 v = vel[i];
@@ -64,17 +66,18 @@ static __global__ void k_final_integrate(int n, StepConst sc, const double4 *__r
     v.z += dtfm * f.z;
     vel[i] = v;
   }
-  aux[i].y += sc.dtf * de[i];
+  en[i] += sc.dtf * de[i];
   vr[i].w += sc.dtf * f.w;
 }
 
 // FixMeso::setup_pre_force: vest = v (fix_meso.cpp:68-85)
-static __global__ void k_vest_from_v(int n, int stationary_mask, const double4 *__restrict__ xt,
-                              const double4 *__restrict__ vel, double4 *__restrict__ vr) {
+static __global__ void k_vest_from_v(int n, int stationary_mask, const int *__restrict__ ty,
+                                     const double4 *__restrict__ vel,
+                                     double4 *__restrict__ vr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   // meso/stationary has no setup_pre_force: its vest stays as it was
-  if ((stationary_mask >> type_of(xt[i].w)) & 1) return;
+  if ((stationary_mask >> ty[i]) & 1) return;
   const double4 v = vel[i];
   double4 r = vr[i];
   r.x = v.x;
@@ -89,10 +92,10 @@ struct Box {
 };
 
 // Domain::pbc (domain.cpp:478-560), orthogonal box
-static __global__ void k_pbc(int n, Box b, double4 *__restrict__ xt) {
+static __global__ void k_pbc(int n, Box b, double4 *__restrict__ xf) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double4 x = xt[i];
+  double4 x = xf[i];
   double c[3] = {x.x, x.y, x.z};
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -106,15 +109,16 @@ static __global__ void k_pbc(int n, Box b, double4 *__restrict__ xt) {
   x.x = c[0];
   x.y = c[1];
   x.z = c[2];
-  xt[i] = x;
+  xf[i] = x;
 }
 
 // ---- borders (one process: the left/right neighbor is this rank itself) -------------
 static __global__ void k_slab_flags(int n, int dim, double lo, double hi,
-                             const double4 *__restrict__ xt, unsigned char *__restrict__ flag) {
+                                    const double4 *__restrict__ xf,
+                                    unsigned char *__restrict__ flag) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double4 x = xt[i];
+  const double4 x = xf[i];
   const double c = dim == 0 ? x.x : (dim == 1 ? x.y : x.z);
   flag[i] = (c >= lo && c <= hi) ? 1 : 0;
 }
@@ -130,21 +134,23 @@ __host__ __device__ __forceinline__ int img_add(int img, int k, int d) {
 
 // append the selected atoms as ghosts shifted by `shift` along `dim`
 // (comm_brick.cpp:820-860 -> atom_vec_meso.cpp:422-480 pack/unpack_border)
-static __global__ void k_append_ghosts(int nsel, const int *__restrict__ sel, int nlocal, int nall,
-                                int dim, int pbc, double shift, double4 *__restrict__ xt,
-                                double4 *__restrict__ vr, double2 *__restrict__ aux,
-                                int *__restrict__ gowner, int *__restrict__ gimg) {
+static __global__ void k_append_ghosts(int nsel, const int *__restrict__ sel, int nlocal,
+                                       int nall, int dim, int pbc, double shift,
+                                       double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                       double *__restrict__ en, int *__restrict__ ty,
+                                       int *__restrict__ gowner, int *__restrict__ gimg) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nsel) return;
   const int s = sel[k];
   const int g = nall + k;
-  double4 x = xt[s];
+  double4 x = xf[s];
   if (dim == 0) x.x = x.x + shift;
   else if (dim == 1) x.y = x.y + shift;
   else x.z = x.z + shift;
-  xt[g] = x;
+  xf[g] = x;
   vr[g] = vr[s];
-  aux[g] = aux[s];
+  en[g] = en[s];
+  ty[g] = ty[s];
   int own, img;
   if (s < nlocal) {
     own = s;
@@ -158,32 +164,32 @@ static __global__ void k_append_ghosts(int nsel, const int *__restrict__ sel, in
 }
 
 // forward_comm (atom_vec_meso.cpp:246-288): ghost <- owner (+image*prd on x), vest, rho, e
-// (and p/rho^2, which the engine keeps beside e).  One add per coordinate, as each hop adds
-// exactly one periodic shift to its own coordinate.
+// (and p/rho^2, carried in xf.w).  One add per coordinate: each hop adds exactly one
+// periodic shift to its own coordinate.
 static __global__ void k_forward(int nghost, int nlocal, Box b, const int *__restrict__ gowner,
-                          const int *__restrict__ gimg, double4 *__restrict__ xt,
-                          double4 *__restrict__ vr, double2 *__restrict__ aux) {
+                                 const int *__restrict__ gimg, double4 *__restrict__ xf,
+                                 double4 *__restrict__ vr, double *__restrict__ en) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nghost) return;
   const int o = gowner[g], img = gimg[g];
-  double4 x = xt[o];
+  double4 x = xf[o];
   const int ix = img_get(img, 0), iy = img_get(img, 1), iz = img_get(img, 2);
   if (ix) x.x = x.x + ix * b.prd[0];
   if (iy) x.y = x.y + iy * b.prd[1];
   if (iz) x.z = x.z + iz * b.prd[2];
-  xt[nlocal + g] = x;
+  xf[nlocal + g] = x;
   vr[nlocal + g] = vr[o];
-  aux[nlocal + g] = aux[o];
+  en[nlocal + g] = en[o];
 }
 
 // forward_comm_pair after rhosum (pair_sph_rhosum.cpp:203, 290-313): rho (+ p/rho^2)
 static __global__ void k_forward_rho(int nghost, int nlocal, const int *__restrict__ gowner,
-                              double4 *__restrict__ vr, double2 *__restrict__ aux) {
+                                     double4 *__restrict__ xf, double4 *__restrict__ vr) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nghost) return;
   const int o = gowner[g];
   vr[nlocal + g].w = vr[o].w;
-  aux[nlocal + g].x = aux[o].x;
+  xf[nlocal + g].w = xf[o].w;
 }
 
 // ---- binning ----------------------------------------------------------------------------
@@ -198,21 +204,21 @@ __device__ __forceinline__ int bin_coord(double x, double lo, double inv, int nb
   return c < 0 ? 0 : (c >= nb ? nb - 1 : c);
 }
 
-static __global__ void k_bin_keys(int n, Bins bn, const double4 *__restrict__ xt,
-                           unsigned *__restrict__ key, int *__restrict__ idx) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const double4 x = xt[i];
+static __global__ void k_bin_keys(int n, int first, Bins bn, const double4 *__restrict__ xf,
+                                  unsigned *__restrict__ key, int *__restrict__ idx) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double4 x = xf[first + k];
   const int cx = bin_coord(x.x, bn.lo[0], bn.inv[0], bn.nb[0]);
   const int cy = bin_coord(x.y, bn.lo[1], bn.inv[1], bn.nb[1]);
   const int cz = bin_coord(x.z, bn.lo[2], bn.inv[2], bn.nb[2]);
-  key[i] = (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
-  idx[i] = i;
+  key[k] = (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
+  idx[k] = first + k;
 }
 
 // bin start/end from sorted keys
-static __global__ void k_bin_bounds(int n, const unsigned *__restrict__ skey, int *__restrict__ bstart,
-                             int *__restrict__ bend) {
+static __global__ void k_bin_bounds(int n, const unsigned *__restrict__ skey,
+                                    int *__restrict__ bstart, int *__restrict__ bend) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const unsigned k = skey[p];
@@ -221,42 +227,41 @@ static __global__ void k_bin_bounds(int n, const unsigned *__restrict__ skey, in
 }
 
 // permutation gather for the spatial sort of owned atoms (atom->sort analogue)
-static __global__ void k_permute(int n, const int *__restrict__ perm, const double4 *__restrict__ xt,
-                          const double4 *__restrict__ vr, const double2 *__restrict__ aux,
-                          const double4 *__restrict__ vel, const int *__restrict__ tag,
-                          const double4 *__restrict__ fo, const double *__restrict__ de,
-                          double4 *__restrict__ xt2, double4 *__restrict__ vr2,
-                          double2 *__restrict__ aux2, double4 *__restrict__ vel2,
-                          int *__restrict__ tag2, double4 *__restrict__ fo2,
-                          double *__restrict__ de2) {
+static __global__ void k_permute(int n, const int *__restrict__ perm,
+                                 const double4 *__restrict__ xf, const double4 *__restrict__ vr,
+                                 const double *__restrict__ en, const int *__restrict__ ty,
+                                 const double4 *__restrict__ vel, const int *__restrict__ tag,
+                                 double4 *__restrict__ xf2, double4 *__restrict__ vr2,
+                                 double *__restrict__ en2, int *__restrict__ ty2,
+                                 double4 *__restrict__ vel2, int *__restrict__ tag2) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int s = perm[i];
-  xt2[i] = xt[s];
+  xf2[i] = xf[s];
   vr2[i] = vr[s];
-  aux2[i] = aux[s];
+  en2[i] = en[s];
+  ty2[i] = ty[s];
   vel2[i] = vel[s];
   tag2[i] = tag[s];
-  fo2[i] = fo[s];
-  de2[i] = de[s];
 }
 
 // ---- binned full list: count pass and fill pass (G lanes per owned atom) ----------------
 template <int G, bool FILL>
 __global__ void __launch_bounds__(256)
-k_neigh(int nlocal, Bins bn, int dim, const double4 *__restrict__ xt,
-        const int *__restrict__ bidx, const int *__restrict__ bstart,
-        const int *__restrict__ bend, const Coefs *__restrict__ cf, int *__restrict__ cnt,
-        const int *__restrict__ off, int *__restrict__ nbr) {
+k_neigh(int nlocal, Bins bn, int dim, const double4 *__restrict__ xf,
+        const int *__restrict__ ty, const int *__restrict__ bidx,
+        const int *__restrict__ bstart, const int *__restrict__ bend,
+        const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
+        int *__restrict__ nbr) {
   __shared__ double s_cns[NT2];
   const int nt1 = cf->ntypes + 1;
   for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
   __syncthreads();
-  const int i = (int)((blockIdx.x * (unsigned)blockDim.x + threadIdx.x) / G);
+  const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (i >= nlocal) return;
-  const double4 xi = xt[i];
-  const double *crow = s_cns + type_of(xi.w) * nt1;
+  const double4 xi = xf[i];
+  const double *crow = s_cns + ty[i] * nt1;
   const int cx = bin_coord(xi.x, bn.lo[0], bn.inv[0], bn.nb[0]);
   const int cy = bin_coord(xi.y, bn.lo[1], bn.inv[1], bn.nb[1]);
   const int cz = bin_coord(xi.z, bn.lo[2], bn.inv[2], bn.nb[2]);
@@ -291,10 +296,10 @@ k_neigh(int nlocal, Bins bn, int dim, const double4 *__restrict__ xt,
         if (p < e) {
           j = bidx[p];
           if (j != i) {
-            const double4 xj = xt[j];
+            const double4 xj = xf[j];
             const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
             const double rsq = dx * dx + dy * dy + dz * dz;
-            hit = rsq <= crow[type_of(xj.w)];
+            hit = rsq <= crow[ty[j]];
           }
         }
         if (FILL) {
@@ -319,10 +324,6 @@ static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__
   if (i == n) off[i] = 0;
 }
 
-}  // namespace sph
-
-namespace sph {
-
 // ---- setup-step forces with the reference's half-list ownership --------------------------
 // On the first run after atoms are created, ghosts carry the vest they had at borders()
 // (zero for new atoms) while owned atoms already have vest = v (Verlet::setup calls
@@ -344,17 +345,17 @@ __device__ __forceinline__ bool half_keep(int i, int j, int nlocal, const double
 
 template <bool FILL>
 static __global__ void k_half_from_full(int nlocal, const int *__restrict__ off,
-                                 const int *__restrict__ nbr, const double4 *__restrict__ xt,
-                                 int *__restrict__ hcnt, const int *__restrict__ hoff,
-                                 int *__restrict__ hnbr) {
+                                        const int *__restrict__ nbr,
+                                        const double4 *__restrict__ xf, int *__restrict__ hcnt,
+                                        const int *__restrict__ hoff, int *__restrict__ hnbr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nlocal) return;
-  const double4 xi = xt[i];
+  const double4 xi = xf[i];
   int n = 0;
   int pos = FILL ? hoff[i] : 0;
   for (int k = off[i]; k < off[i + 1]; k++) {
     const int j = nbr[k];
-    if (half_keep(i, j, nlocal, xi, xt[j])) {
+    if (half_keep(i, j, nlocal, xi, xf[j])) {
       if (FILL) hnbr[pos++] = j;
       n++;
     }
@@ -364,7 +365,7 @@ static __global__ void k_half_from_full(int nlocal, const int *__restrict__ off,
 
 // comm->reverse_comm (atom_vec_meso.cpp:387-418): owner += ghost (f, drho, de)
 static __global__ void k_reverse(int nghost, int nlocal, const int *__restrict__ gowner,
-                          double4 *__restrict__ fo, double *__restrict__ de) {
+                                 double4 *__restrict__ fo, double *__restrict__ de) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nghost) return;
   const int o = gowner[g];
@@ -376,17 +377,15 @@ static __global__ void k_reverse(int nghost, int nlocal, const int *__restrict__
   atomicAdd(&de[o], de[nlocal + g]);
 }
 
-}  // namespace sph
-
-namespace sph {
 // fix gravity-style post_force body force: f += m g (owned)
 static __global__ void k_add_gravity(int n, StepConst sc, double gx, double gy, double gz,
-                                     const double4 *__restrict__ xt, double4 *__restrict__ fo) {
+                                     const int *__restrict__ ty, double4 *__restrict__ fo) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double m = sc.mass[type_of(xt[i].w)];
+  const double m = sc.mass[ty[i]];
   fo[i].x += m * gx;
   fo[i].y += m * gy;
   fo[i].z += m * gz;
 }
+
 }  // namespace sph

@@ -28,7 +28,7 @@ int group_lanes() {
   static int g = [] {
     const char *s = getenv("SPH_GROUP");
     int v = s ? atoi(s) : 8;
-    if (v != 4 && v != 8 && v != 16 && v != 32) v = 8;
+    if (v != 4 && v != 8 && v != 16) v = 8;
     return v;
   }();
   return g;
@@ -58,12 +58,10 @@ struct sph_hip_ctx {
   int tait_visc = SPH_VISC_MONAGHAN;
   int nlocal = 0, nghost = 0;
   int list_kind = -1, inum = 0;
-  DBuf<double4> xt, vr, fo;
-  DBuf<double2> aux;
-  DBuf<double> de, rho_out, virial;
-  DBuf<int> ilist, off, nbr;
+  DBuf<double4> xf, vr, fo;
+  DBuf<double> en, de, rho_out, virial;
+  DBuf<int> ty, ilist, off, nbr;
   std::vector<double4> h4;
-  std::vector<double2> h2;
   std::vector<double> h1;
   std::vector<int> hoff, hnbr, hilist;
   bool coef_dirty = true;
@@ -109,10 +107,11 @@ int sph_hip_destroy(sph_hip_ctx *c) {
   if (!c) return SPH_HIP_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->xt.release();
+  c->xf.release();
   c->vr.release();
   c->fo.release();
-  c->aux.release();
+  c->en.release();
+  c->ty.release();
   c->de.release();
   c->rho_out.release();
   c->virial.release();
@@ -176,21 +175,24 @@ int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const
   for (size_t i = 0; i < nall; i++)
     SPH_REQUIRE(type[i] >= 1 && type[i] <= c->ntypes, SPH_HIP_EINVAL,
                 "atom %zu has type %d outside [1,%d]", i, type[i], c->ntypes);
-  c->xt.reserve(nall);
+  c->xf.reserve(nall);
   c->vr.reserve(nall);
-  c->aux.reserve(nall);
+  c->en.reserve(nall);
+  c->ty.reserve(nall);
   c->h4.resize(nall);
   for (size_t i = 0; i < nall; i++)
-    c->h4[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], type_bits(type[i]));
-  SPH_HIP_TRY(hipMemcpyAsync(c->xt.p, c->h4.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
+    c->h4[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
+  SPH_HIP_TRY(hipMemcpyAsync(c->xf.p, c->h4.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
+  SPH_HIP_TRY(hipMemcpyAsync(c->ty.p, type, nall * sizeof(int), hipMemcpyHostToDevice, c->stream));
   std::vector<double4> hv(nall);
   for (size_t i = 0; i < nall; i++)
     hv[i] = make_double4(vest ? vest[3 * i] : 0.0, vest ? vest[3 * i + 1] : 0.0,
                          vest ? vest[3 * i + 2] : 0.0, rho ? rho[i] : 0.0);
   SPH_HIP_TRY(hipMemcpyAsync(c->vr.p, hv.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
-  c->h2.resize(nall);
-  for (size_t i = 0; i < nall; i++) c->h2[i] = make_double2(0.0, e ? e[i] : 0.0);
-  SPH_HIP_TRY(hipMemcpyAsync(c->aux.p, c->h2.data(), nall * sizeof(double2), hipMemcpyHostToDevice, c->stream));
+  c->h1.assign(nall, 0.0);
+  if (e)
+    for (size_t i = 0; i < nall; i++) c->h1[i] = e[i];
+  SPH_HIP_TRY(hipMemcpyAsync(c->en.p, c->h1.data(), nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
   // staging vectors must outlive the async copies
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   SPH_API_END
@@ -269,8 +271,9 @@ int sph_hip_rhosum(sph_hip_ctx *c, double *rho) {
   const int nall = c->nlocal + c->nghost;
   if (c->inum == 0 || nall == 0) return SPH_HIP_OK;
   c->rho_out.reserve(nall);
-  launch_rhosum(c->dim, false, c->stream, c->inum, c->ilist.p, c->off.p, c->nbr.p, c->xt.p,
-                c->vr.p, c->aux.p, c->rho_out.p, c->dc);
+  RhoArgs ra{c->inum, c->ilist.p, c->off.p, c->nbr.p, c->xf.p, c->ty.p, c->vr.p, c->rho_out.p,
+             c->dc};
+  launch_rhosum(c->dim, false, c->ntypes == 1, c->stream, ra);
   SPH_HIP_TRY(hipGetLastError());
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->rho_out.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -297,8 +300,8 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
     SPH_HIP_TRY(hipMemsetAsync(c->virial.p, 0, 6 * sizeof(double), c->stream));
   }
   if (mode & M_TAIT)  // p/rho^2 of every atom (owned + ghost) from the staged rho
-    hipLaunchKernelGGL(k_eos, dim3((nall + 255) / 256), dim3(256), 0, c->stream, nall, c->xt.p,
-                       c->vr.p, c->aux.p, c->dc);
+    hipLaunchKernelGGL(k_eos, dim3((nall + 255) / 256), dim3(256), 0, c->stream, nall, c->xf.p,
+                       c->vr.p, c->ty.p, c->dc);
   ForceArgs a{};
   a.inum = c->inum;
   a.nlocal = c->nlocal;
@@ -306,16 +309,17 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
   a.ilist = c->ilist.p;
   a.off = c->off.p;
   a.nbr = c->nbr.p;
-  a.xt = c->xt.p;
+  a.xf = c->xf.p;
   a.vr = c->vr.p;
-  a.aux = c->aux.p;
+  a.ty = c->ty.p;
+  a.en = c->en.p;
   a.fo = c->fo.p;
   a.de = c->de.p;
   a.accum = 0;
   a.cf = c->dc;
   a.virial = virial ? c->virial.p : nullptr;
   if (c->list_kind == SPH_LIST_HALF) mode |= M_HALF;
-  launch_force(c->dim, c->stream, c->tait_visc, mode, a);
+  launch_force(c->dim, c->ntypes == 1, c->stream, c->tait_visc, mode, a);
   SPH_HIP_TRY(hipGetLastError());
   double hv[6] = {0, 0, 0, 0, 0, 0};
   if (mode & M_TAIT) {

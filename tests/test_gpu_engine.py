@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-10
 
 
-def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None):
+def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None, kernel_path=0):
     nt = s.ntypes
     kw = {}
     if ph.rhosum_nstep > 0:
@@ -26,7 +26,8 @@ def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None):
     if ph.heat:
         kw["heat"] = dict(alpha=ph.alpha, cut=ph.heat_cut)
     cfg = sph_amd.make_config(s.dim, nt, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
-                              neigh_every=every or ph.every, sort=sort, **kw)
+                              neigh_every=every or ph.every, sort=sort,
+                              kernel_path=kernel_path, **kw)
     eng = sph_amd.Engine(cfg)
     eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)
     return eng
@@ -46,14 +47,16 @@ def compare(eng, ref, tol=TOL):
     return got
 
 
-@pytest.mark.parametrize("sort", [0, 1])
-def test_setup_c2(gpu, sph_amd, sort):
+@pytest.mark.parametrize("sort,path", [(1, 0), (0, 1), (1, 1)])
+def test_setup_c2(gpu, sph_amd, sort, path):
+    """path 0 = LDS-staged bins (16-bit slot lists), 1 = CSR rows with global gathers."""
     s = c2_system(12)
     ph = po.c2_physics()
     ref = po.RefRun(s, ph)
     ref.setup()
-    eng = engine_for(sph_amd, s, ph, sort=sort)
+    eng = engine_for(sph_amd, s, ph, sort=sort, kernel_path=path)
     eng.setup()
+    assert eng.stats()["staged"] == (1 if path == 0 else 0)
     # neighbor membership: bit-exact counts per particle
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     st = eng.stats()
@@ -63,13 +66,14 @@ def test_setup_c2(gpu, sph_amd, sort):
     assert elem_rel_err(got["rho"], ref.s.rho) < 1e-13
 
 
-def test_run_c2_with_rebuilds(gpu, sph_amd):
+@pytest.mark.parametrize("path", [0, 1])
+def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     s = c2_system(12)
     ph = po.c2_physics()
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(25)                                # rebuilds at steps 10 and 20
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(25)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())

@@ -14,7 +14,9 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     sph = bench.load_pkg()
     x, v, t, rho, e, cv = bench.make_system(n, 12345)
-    eng = sph.Engine(bench.c2_config(sph, n))
+    cfg = bench.c2_config(sph, n)
+    cfg.kernel_path = int(os.environ.get("SPH_PATH", "0"))
+    eng = sph.Engine(cfg)
     eng.set_atoms(x, v, t, rho, e, cv)
     eng.setup()
     eng.run(5)
@@ -23,7 +25,9 @@ def main():
     eng.set_timing(True)
     eng.pair_passes(reps)
     st = eng.stats()
-    print(json.dumps({"group": os.environ.get("SPH_GROUP", "8"),
+    print(json.dumps({"group": os.environ.get("SPH_GROUP", "8"), "path": cfg.kernel_path,
+                      "staged": st["staged"], "stage_max": st["stage_max"],
+                      "rows_max": st["nbr_maxrow"],
                       "rhosum_ms": st["ms_rhosum"] / st["n_rhosum"],
                       "tait_ms": st["ms_tait"] / st["n_tait"],
                       "comm_ms": st["ms_comm"] / max(st["n_rhosum"], 1)}))

@@ -12,6 +12,11 @@
 // list load of a wave is one coalesced 128-B access.  Row sums are folded into LDS
 // accumulators (fp64 LDS atomics) where a thread's run crosses a row boundary.
 //
+// Everything a workgroup needs before its pair loop (its 18 staged ranges, slot prefix,
+// rows, list length) is precomputed once per rebuild into a 192-B bin descriptor, and the
+// rows' list offsets into a per-atom array, so a pair pass costs each workgroup one
+// descriptor load, one burst of independent staging loads, and the pair loop.
+//
 // Membership is exactly Neighbor::full_bin's (rsq <= cutneighsq, j != i,
 // src/neigh_full.cpp:241-344); the physics is that of sph_kernels.h.
 #pragma once
@@ -33,7 +38,19 @@ struct BinCtx {
   const int *gbeg;  // [nbins+1] first sorted ghost atom (absolute index) of bin b
 };
 
-// Staged ranges of bin b (called by threads 0..MAXR-1, one range each).
+// 192-B per-bin descriptor (48 ints), written at rebuild
+struct BinDesc {
+  int rs[MAXR];       // first atom of each staged range
+  int pre[MAXR + 1];  // slot prefix; pre[MAXR] = S (staged atoms)
+  int row0, nrows;    // the bin's own owned atoms = its rows
+  int slot0;          // slot of row 0
+  int E, L;           // list entries, entries per thread = ceil(E/BT)
+  int pad[6];
+};
+static_assert(sizeof(BinDesc) == 192, "BinDesc is 48 ints");
+constexpr int kDescInts = 48;
+
+// Staged range r of bin b.
 __device__ __forceinline__ void bin_range(const BinCtx &c, int b, int r, int &start,
                                           int &count) {
   const int nbx = c.bn.nb[0], nby = c.bn.nb[1], nbz = c.bn.nb[2];
@@ -59,18 +76,14 @@ __device__ __forceinline__ void bin_range(const BinCtx &c, int b, int r, int &st
 // the center x-row's owned range (row dy = dz = 0) holds the bin's own rows
 __device__ __forceinline__ int center_range(int dim) { return ((dim == 3) ? 4 : 1) * 2; }
 
-struct StageHdr {
-  int rs[MAXR], pre[MAXR + 1], cnt[MAXR];
-  int nrows, row0, slot0, E, L;
-};
-
 // All LDS of the bin kernels is one dynamic array carved at 16-B aligned offsets
 // (cdna_hip_programming.md Guideline 17: no static __shared__ in front of the dynamic base).
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
-constexpr int kHdrBytes = align16((int)sizeof(StageHdr));
+constexpr int kHdrBytes = (int)sizeof(BinDesc);
 constexpr int kRowoffBytes = align16((MAXROWS + 4) * 4);
-constexpr int kAccBytes = 5 * MAXROWS * 8;
-constexpr int kFixedBytes = kHdrBytes + kRowoffBytes + kAccBytes;
+constexpr int kFixedNeigh = kHdrBytes + kRowoffBytes;
+constexpr int kFixedRho = kFixedNeigh + MAXROWS * 8;
+constexpr int kFixedForce = kFixedNeigh + 5 * MAXROWS * 8;
 // coefficient tables (multi-type only) and per-staged-atom bytes, per kernel
 constexpr int kNeighCoefBytes = align16(8 * NT2);
 constexpr int kRhoCoefBytes = align16((int)sizeof(RhoPair) * NT2);
@@ -81,37 +94,84 @@ __host__ __device__ constexpr int force_atom_bytes(bool heat, bool nt1) {
   return 64 + (heat ? 8 : 0) + (nt1 ? 0 : 4);
 }
 
-// thread 0..MAXR-1 compute ranges; returns after a barrier with hdr filled
-__device__ __forceinline__ void stage_header(const BinCtx &c, int b, StageHdr &h) {
-  const int t = threadIdx.x;
-  if (t < MAXR) {
-    int st, cn;
-    bin_range(c, b, t, st, cn);
-    h.rs[t] = st;
-    h.cnt[t] = cn;
+// descriptor of every bin; device maxima of staged size and rows into mx[0], mx[1]
+static __global__ void k_bin_desc(BinCtx c, int *__restrict__ desc, int *__restrict__ mx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= c.nbins) return;
+  BinDesc d{};
+  d.row0 = c.obeg[b];
+  d.nrows = c.obeg[b + 1] - d.row0;
+  int S = 0;
+  for (int r = 0; r < MAXR; r++) {
+    int st = 0, cn = 0;
+    if (d.nrows > 0) bin_range(c, b, r, st, cn);
+    d.rs[r] = st;
+    d.pre[r] = S;
+    S += cn;
   }
-  __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int r = 0; r < MAXR; r++) {
-      h.pre[r] = acc;
-      acc += h.cnt[r];
-    }
-    h.pre[MAXR] = acc;
-    const int cr = center_range(c.dim);
-    h.row0 = c.obeg[b];
-    h.nrows = c.obeg[b + 1] - h.row0;
-    h.slot0 = h.pre[cr] + (h.row0 - h.rs[cr]);
-  }
+  d.pre[MAXR] = S;
+  const int cr = center_range(c.dim);
+  d.slot0 = d.pre[cr] + (d.row0 - d.rs[cr]);
+  const int *src = reinterpret_cast<const int *>(&d);
+  int4 *dst = reinterpret_cast<int4 *>(desc + (size_t)b * kDescInts);
+#pragma unroll
+  for (int k = 0; k < kDescInts / 4; k++)
+    dst[k] = make_int4(src[4 * k], src[4 * k + 1], src[4 * k + 2], src[4 * k + 3]);
+  atomicMax(&mx[0], S);
+  atomicMax(&mx[1], d.nrows);
+}
+
+// descriptor -> LDS (threads 0..47), then a barrier
+__device__ __forceinline__ void load_desc(const int *__restrict__ desc, int b, BinDesc &h) {
+  if (threadIdx.x < kDescInts)
+    reinterpret_cast<int *>(&h)[threadIdx.x] = desc[(size_t)b * kDescInts + threadIdx.x];
   __syncthreads();
 }
 
 // slot -> global atom index
-__device__ __forceinline__ int slot_atom(const StageHdr &h, int s) {
+__device__ __forceinline__ int slot_atom(const BinDesc &h, int s) {
   int r = 0;
 #pragma unroll
   for (int k = 1; k < MAXR; k++) r += (s >= h.pre[k]) ? 1 : 0;
   return h.rs[r] + (s - h.pre[r]);
+}
+
+// Stage the bin's neighborhood records into LDS.  Each thread issues the loads of K slots
+// before its first LDS store, so a whole neighborhood (~1000 atoms) is one burst of
+// independent loads rather than 18 dependent range loops.
+template <bool VEL, bool EN, bool TY>
+__device__ __forceinline__ void stage_atoms(const BinDesc &h, const double4 *__restrict__ xf,
+                                            const double4 *__restrict__ vr,
+                                            const double *__restrict__ en,
+                                            const int *__restrict__ ty, double4 *sx, double4 *sv,
+                                            double *se, int *sty) {
+  const int S = h.pre[MAXR];
+  constexpr int K = 4;
+  for (int s0 = threadIdx.x; s0 < S; s0 += BT * K) {
+    int g[K];
+    double4 a[K], v[K];
+    double e[K];
+    int t[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) g[k] = slot_atom(h, min(s0 + k * BT, S - 1));
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      a[k] = xf[g[k]];
+      if (VEL) v[k] = vr[g[k]];
+      if (EN) e[k] = en[g[k]];
+      if (TY) t[k] = ty[g[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const int s = s0 + k * BT;
+      if (s < S) {
+        sx[s] = a[k];
+        if (VEL) sv[s] = v[k];
+        if (EN) se[s] = e[k];
+        if (TY) sty[s] = t[k];
+      }
+    }
+  }
 }
 
 // per-bin lower bounds of sorted keys: beg[b] = first p with key[p] >= b (b in [0,nbins])
@@ -128,53 +188,31 @@ static __global__ void k_lower_bound(int nbins, int n, int base, const unsigned 
   beg[b] = base + lo;
 }
 
-// ---- list build: count pass (per-atom counts, per-bin totals, per-bin staged size) -------
+// ---- list build: count pass (row counts, row offsets, per-bin E/L) and fill pass --------
 template <bool FILL>
 __global__ void __launch_bounds__(BT)
-k_bin_neigh(BinCtx c, const double4 *__restrict__ xf, const int *__restrict__ ty,
-            const Coefs *__restrict__ cf, int *__restrict__ cnt, int *__restrict__ binE,
-            int *__restrict__ binS, const long long *__restrict__ boff,
+k_bin_neigh(int nbins, int *__restrict__ desc, const double4 *__restrict__ xf,
+            const int *__restrict__ ty, const Coefs *__restrict__ cf, int *__restrict__ cnt,
+            int *__restrict__ roff, int *__restrict__ binE, const long long *__restrict__ boff,
             unsigned short *__restrict__ nbr16) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  StageHdr &h = *reinterpret_cast<StageHdr *>(smem);
-  int *s_rowoff = reinterpret_cast<int *>(smem + kHdrBytes);
-  double *s_cns = reinterpret_cast<double *>(smem + kFixedBytes);
+  BinDesc &h = *reinterpret_cast<BinDesc *>(smem);
+  int *s_cnt = reinterpret_cast<int *>(smem + kHdrBytes);
+  double *s_cns = reinterpret_cast<double *>(smem + kFixedNeigh);
   const int b = xcd_block();
-  if (b >= c.nbins) return;
-  if (c.obeg[b + 1] == c.obeg[b]) {  // no owned atoms: nothing to list
-    if (!FILL && threadIdx.x == 0) {
-      binE[b] = 0;
-      binS[b] = 0;
-    }
-    return;
-  }
+  if (b >= nbins) return;
   const int nt1 = cf->ntypes + 1;
   for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
-  stage_header(c, b, h);
-  const int S = h.pre[MAXR];
-  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedBytes + kNeighCoefBytes);
-  int *sty = reinterpret_cast<int *>(sx + S);
-  for (int r = 0; r < MAXR; r++) {
-    const int n = h.pre[r + 1] - h.pre[r];
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-      sx[h.pre[r] + t] = xf[h.rs[r] + t];
-      sty[h.pre[r] + t] = ty[h.rs[r] + t];
-    }
-  }
+  load_desc(desc, b, h);
   const int R = h.nrows;
-  if (!FILL && threadIdx.x == 0) h.E = 0;
-  if (FILL) {
-    if (threadIdx.x == 0) {
-      int acc = 0;
-      for (int r = 0; r < R; r++) {
-        s_rowoff[r] = acc;
-        acc += cnt[h.row0 + r];
-      }
-      s_rowoff[R] = acc;
-      h.E = acc;
-      h.L = (acc + BT - 1) / BT;
-    }
+  if (R == 0) {  // no owned atoms: nothing to list
+    if (!FILL && threadIdx.x == 0) binE[b] = 0;
+    return;
   }
+  const int S = h.pre[MAXR];
+  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedNeigh + kNeighCoefBytes);
+  int *sty = reinterpret_cast<int *>(sx + S);
+  stage_atoms<false, false, true>(h, xf, nullptr, nullptr, ty, sx, nullptr, nullptr, sty);
   __syncthreads();
   constexpr int G = 8;
   const int lane = threadIdx.x & (G - 1);
@@ -186,7 +224,7 @@ k_bin_neigh(BinCtx c, const double4 *__restrict__ xf, const int *__restrict__ ty
     const double4 xi = sx[si];
     const double *crow = s_cns + sty[si] * nt1;
     int n = 0;
-    int e = FILL ? s_rowoff[r] : 0;
+    int e = FILL ? roff[h.row0 + r] : 0;
     for (int base = 0; base < S; base += G) {
       const int s = base + lane;
       bool hit = false;
@@ -209,17 +247,33 @@ k_bin_neigh(BinCtx c, const double4 *__restrict__ xf, const int *__restrict__ ty
     }
     if (!FILL) {
       n = group_sum_i<G>(n);
-      if (lane == 0) {
-        cnt[h.row0 + r] = n;
-        atomicAdd(&h.E, n);
-      }
+      if (lane == 0) s_cnt[r] = n;
     }
   }
   if (!FILL) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-      binE[b] = h.E;
-      binS[b] = S;
+    if (threadIdx.x < 64) {  // one wave: exclusive scan of the row counts -> roff, E, L
+      int carry = 0;
+      for (int base = 0; base < R; base += 64) {
+        const int r = base + threadIdx.x;
+        const int c0 = r < R ? s_cnt[r] : 0;
+        int v = c0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int u = __shfl_up(v, d, 64);
+          if ((int)threadIdx.x >= d) v += u;
+        }
+        if (r < R) {
+          cnt[h.row0 + r] = c0;
+          roff[h.row0 + r] = carry + v - c0;
+        }
+        carry += __shfl(v, 63, 64);
+      }
+      if (threadIdx.x == 0) {
+        binE[b] = carry;
+        desc[(size_t)b * kDescInts + offsetof(BinDesc, E) / 4] = carry;
+        desc[(size_t)b * kDescInts + offsetof(BinDesc, L) / 4] = (carry + BT - 1) / BT;
+      }
     }
   }
 }
@@ -233,18 +287,16 @@ static __global__ void k_bin_listlen(int nbins, const int *__restrict__ binE,
 }
 
 // ---- staged pair passes ------------------------------------------------------------------
-// Common prologue: stage header, rows' list offsets, and the thread's contiguous run
-// [e0, e1) with its starting row.
+// A thread's contiguous run [e0, e1) of its bin's entries and the row holding e0.
 struct Run {
   int e0, e1, r;
 };
 
-__device__ __forceinline__ Run thread_run(const StageHdr &h, const int *s_rowoff) {
+__device__ __forceinline__ Run thread_run(const BinDesc &h, const int *s_rowoff) {
   Run q;
   q.e0 = threadIdx.x * h.L;
   q.e1 = min(q.e0 + h.L, h.E);
-  // row containing e0: last r with rowoff[r] <= e0
-  int lo = 0, hi = h.nrows - 1;
+  int lo = 0, hi = h.nrows - 1;  // last r with rowoff[r] <= e0
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (s_rowoff[mid] <= q.e0) lo = mid;
@@ -254,60 +306,37 @@ __device__ __forceinline__ Run thread_run(const StageHdr &h, const int *s_rowoff
   return q;
 }
 
-__device__ __forceinline__ void load_rowoffs(const StageHdr &h, const int *__restrict__ cnt,
+// the rows' list offsets (precomputed at rebuild) plus E at [nrows]
+__device__ __forceinline__ void load_rowoffs(const BinDesc &h, const int *__restrict__ roff,
                                              int *s_rowoff) {
-  // inclusive scan of the bin's row counts (rows <= MAXROWS) by one wave
-  if (threadIdx.x < 64) {
-    int carry = 0;
-    for (int base = 0; base < h.nrows; base += 64) {
-      const int r = base + threadIdx.x;
-      int v = r < h.nrows ? cnt[h.row0 + r] : 0;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int u = __shfl_up(v, d, 64);
-        if ((int)threadIdx.x >= d) v += u;
-      }
-      if (r < h.nrows) s_rowoff[r + 1] = carry + v;
-      carry += __shfl(v, 63, 64);
-    }
-    if (threadIdx.x == 0) s_rowoff[0] = 0;
-  }
+  for (int r = threadIdx.x; r < h.nrows; r += blockDim.x) s_rowoff[r] = roff[h.row0 + r];
+  if (threadIdx.x == 0) s_rowoff[h.nrows] = h.E;
 }
 
 template <int DIM, bool NT1>
 __global__ void __launch_bounds__(BT)
-k_bin_rhosum(BinCtx c, double4 *__restrict__ xf, const int *__restrict__ ty,
-             double4 *__restrict__ vr, const int *__restrict__ cnt,
+k_bin_rhosum(int nbins, const int *__restrict__ desc, double4 *__restrict__ xf,
+             const int *__restrict__ ty, double4 *__restrict__ vr, const int *__restrict__ roff,
              const long long *__restrict__ boff, const unsigned short *__restrict__ nbr16,
              const Coefs *__restrict__ cf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  StageHdr &h = *reinterpret_cast<StageHdr *>(smem);
+  BinDesc &h = *reinterpret_cast<BinDesc *>(smem);
   int *s_rowoff = reinterpret_cast<int *>(smem + kHdrBytes);
-  double *s_acc = reinterpret_cast<double *>(smem + kHdrBytes + kRowoffBytes);
-  RhoPair *s_c = reinterpret_cast<RhoPair *>(smem + kFixedBytes);
+  double *s_acc = reinterpret_cast<double *>(smem + kFixedNeigh);
+  RhoPair *s_c = reinterpret_cast<RhoPair *>(smem + kFixedRho);
   const int b = xcd_block();
-  if (b >= c.nbins || c.obeg[b + 1] == c.obeg[b]) return;
+  if (b >= nbins) return;
   const int nt1 = cf->ntypes + 1;
   if (!NT1)
     for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_c[t] = cf->rho[t];
-  stage_header(c, b, h);
+  load_desc(desc, b, h);
+  if (h.nrows == 0) return;
   const int S = h.pre[MAXR];
-  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedBytes + (NT1 ? 0 : kRhoCoefBytes));
+  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedRho + (NT1 ? 0 : kRhoCoefBytes));
   int *sty = reinterpret_cast<int *>(sx + S);
-  for (int r = 0; r < MAXR; r++) {
-    const int n = h.pre[r + 1] - h.pre[r];
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-      sx[h.pre[r] + t] = xf[h.rs[r] + t];
-      if (!NT1) sty[h.pre[r] + t] = ty[h.rs[r] + t];
-    }
-  }
-  load_rowoffs(h, cnt, s_rowoff);
+  load_rowoffs(h, roff, s_rowoff);
   for (int r = threadIdx.x; r < h.nrows; r += blockDim.x) s_acc[r] = 0.0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    h.E = s_rowoff[h.nrows];
-    h.L = (h.E + BT - 1) / BT;
-  }
+  stage_atoms<false, false, !NT1>(h, xf, nullptr, nullptr, ty, sx, nullptr, nullptr, sty);
   __syncthreads();
   const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
   Run q = thread_run(h, s_rowoff);
@@ -373,53 +402,40 @@ k_bin_rhosum(BinCtx c, double4 *__restrict__ xf, const int *__restrict__ ty,
 
 template <int DIM, int VISC, int MODE, bool NT1>
 __global__ void __launch_bounds__(BT)
-k_bin_force(BinCtx c, const double4 *__restrict__ xf, const double4 *__restrict__ vr,
-            const int *__restrict__ ty, const double *__restrict__ en,
-            const int *__restrict__ cnt, const long long *__restrict__ boff,
-            const unsigned short *__restrict__ nbr16, const Coefs *__restrict__ cf,
-            double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-            double gz) {
+k_bin_force(int nbins, const int *__restrict__ desc, const double4 *__restrict__ xf,
+            const double4 *__restrict__ vr, const int *__restrict__ ty,
+            const double *__restrict__ en, const int *__restrict__ roff,
+            const long long *__restrict__ boff, const unsigned short *__restrict__ nbr16,
+            const Coefs *__restrict__ cf, double4 *__restrict__ fo, double *__restrict__ de,
+            double gx, double gy, double gz) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  StageHdr &h = *reinterpret_cast<StageHdr *>(smem);
+  BinDesc &h = *reinterpret_cast<BinDesc *>(smem);
   int *s_rowoff = reinterpret_cast<int *>(smem + kHdrBytes);
-  double(*s_acc)[MAXROWS] = reinterpret_cast<double(*)[MAXROWS]>(smem + kHdrBytes + kRowoffBytes);
-  TaitPair *s_t = reinterpret_cast<TaitPair *>(smem + kFixedBytes);
-  HeatPair *s_h = reinterpret_cast<HeatPair *>(smem + kFixedBytes + align16((int)sizeof(TaitPair) * NT2));
+  double(*s_acc)[MAXROWS] = reinterpret_cast<double(*)[MAXROWS]>(smem + kFixedNeigh);
+  TaitPair *s_t = reinterpret_cast<TaitPair *>(smem + kFixedForce);
+  HeatPair *s_h = reinterpret_cast<HeatPair *>(smem + kFixedForce + align16((int)sizeof(TaitPair) * NT2));
   const int b = xcd_block();
-  if (b >= c.nbins || c.obeg[b + 1] == c.obeg[b]) return;
+  if (b >= nbins) return;
   const int nt1 = cf->ntypes + 1;
   if (!NT1)
     for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) {
       if (TAIT) s_t[t] = cf->tait[t];
       if (HEAT) s_h[t] = cf->heat[t];
     }
-  stage_header(c, b, h);
+  load_desc(desc, b, h);
+  if (h.nrows == 0) return;
   const int S = h.pre[MAXR];
-  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedBytes + (NT1 ? 0 : kForceCoefBytes));
+  double4 *sx = reinterpret_cast<double4 *>(smem + kFixedForce + (NT1 ? 0 : kForceCoefBytes));
   double4 *sv = sx + S;
   double *se = reinterpret_cast<double *>(sv + S);
   int *sty = reinterpret_cast<int *>(se + (HEAT ? S : 0));
-  for (int r = 0; r < MAXR; r++) {
-    const int n = h.pre[r + 1] - h.pre[r];
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-      const int g = h.rs[r] + t, s = h.pre[r] + t;
-      sx[s] = xf[g];
-      sv[s] = vr[g];
-      if (HEAT) se[s] = en[g];
-      if (!NT1) sty[s] = ty[g];
-    }
-  }
-  load_rowoffs(h, cnt, s_rowoff);
+  load_rowoffs(h, roff, s_rowoff);
   for (int r = threadIdx.x; r < h.nrows; r += blockDim.x) {
     s_acc[0][r] = s_acc[1][r] = s_acc[2][r] = s_acc[3][r] = s_acc[4][r] = 0.0;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    h.E = s_rowoff[h.nrows];
-    h.L = (h.E + BT - 1) / BT;
-  }
+  stage_atoms<true, HEAT, !NT1>(h, xf, vr, en, ty, sx, sv, se, sty);
   __syncthreads();
   TaitPair t1{};
   HeatPair h1{};
@@ -539,29 +555,6 @@ k_bin_force(BinCtx c, const double4 *__restrict__ xf, const double4 *__restrict_
     }
     de[i] = s_acc[4][r];
   }
-}
-
-// global index of neighbor entry for the (device) neighbor-count API: row counts are cnt[]
-
-}  // namespace sph
-
-namespace sph {
-
-// staged size S and owned row count of every bin; device maxima into mx[0], mx[1]
-static __global__ void k_bin_sizes(BinCtx c, int *__restrict__ binS, int *__restrict__ mx) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= c.nbins) return;
-  const int rows = c.obeg[b + 1] - c.obeg[b];
-  int S = 0;
-  if (rows > 0)
-    for (int r = 0; r < MAXR; r++) {
-      int st, cn;
-      bin_range(c, b, r, st, cn);
-      S += cn;
-    }
-  binS[b] = S;
-  atomicMax(&mx[0], S);
-  atomicMax(&mx[1], rows);
 }
 
 // reorder the ghost segment by bin: scratch <- ghosts in sorted order

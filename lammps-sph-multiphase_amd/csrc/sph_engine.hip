@@ -79,7 +79,7 @@ struct sph_engine {
   int stage_max = 0, rows_max = 0;
   size_t lds_neigh = 0, lds_rho = 0, lds_force = 0;
   DBuf<unsigned> okey, gkey;
-  DBuf<int> obeg, gbeg, binE, binS, mx, ccnt;
+  DBuf<int> obeg, gbeg, binE, desc, roff, mx, ccnt;
   DBuf<long long> blen, boff;
   DBuf<unsigned short> nbr16;
   DBuf<int> gowner2, gimg2;
@@ -234,7 +234,8 @@ struct sph_engine {
     obeg.reserve(nbins + 1);
     gbeg.reserve(nbins + 1);
     binE.reserve(nbins + 1);
-    binS.reserve(nbins + 1);
+    desc.reserve((size_t)nbins * kDescInts);
+    roff.reserve(n + 1);
     blen.reserve(nbins + 1);
     boff.reserve(nbins + 1);
     mx.reserve(2);
@@ -244,22 +245,24 @@ struct sph_engine {
     hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, ng, n, gkey.p, gbeg.p);
     SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 2 * sizeof(int), s));
     const BinCtx c = bin_ctx();
-    hipLaunchKernelGGL(k_bin_sizes, dim3(blocks(nbins)), dim3(BLK), 0, s, c, binS.p, mx.p);
+    hipLaunchKernelGGL(k_bin_desc, dim3(blocks(nbins)), dim3(BLK), 0, s, c, desc.p, mx.p);
     int hm[2];
     SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     SPH_HIP_TRY(hipStreamSynchronize(s));
     stage_max = hm[0];
     rows_max = hm[1];
     const bool nt = nt1(), heat = (force_mode & M_HEAT) != 0;
-    lds_neigh = kFixedBytes + kNeighCoefBytes + (size_t)stage_max * neigh_atom_bytes();
-    lds_rho = kFixedBytes + (nt ? 0 : kRhoCoefBytes) + (size_t)stage_max * rho_atom_bytes(nt);
-    lds_force = kFixedBytes + (nt ? 0 : kForceCoefBytes) + (size_t)stage_max * force_atom_bytes(heat, nt);
+    lds_neigh = kFixedNeigh + kNeighCoefBytes + (size_t)stage_max * neigh_atom_bytes();
+    lds_rho = kFixedRho + (nt ? 0 : kRhoCoefBytes) + (size_t)stage_max * rho_atom_bytes(nt);
+    lds_force = kFixedForce + (nt ? 0 : kForceCoefBytes) + (size_t)stage_max * force_atom_bytes(heat, nt);
     const size_t lds_cap = 160 * 1024;
     if (rows_max > MAXROWS || stage_max >= 65535 || lds_neigh > lds_cap || lds_rho > lds_cap ||
         lds_force > lds_cap)
       return false;
-    hipLaunchKernelGGL((k_bin_neigh<false>), dim3(nbins), dim3(BT), lds_neigh, s, c, xf.p, ty.p,
-                       dc, cnt.p, binE.p, binS.p, (const long long *)nullptr,
+    for (const void *k : {(const void *)k_bin_neigh<false>, (const void *)k_bin_neigh<true>})
+      SPH_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_neigh));
+    hipLaunchKernelGGL((k_bin_neigh<false>), dim3(nbins), dim3(BT), lds_neigh, s, nbins, desc.p, xf.p,
+                       ty.p, dc, cnt.p, roff.p, binE.p, (const long long *)nullptr,
                        (unsigned short *)nullptr);
     hipLaunchKernelGGL(k_bin_listlen, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, binE.p, blen.p);
     size_t tb = 0;
@@ -270,8 +273,8 @@ struct sph_engine {
     SPH_HIP_TRY(hipStreamSynchronize(s));
     const long long tot = *h_total;
     nbr16.reserve(tot > 0 ? (size_t)tot : 1);
-    hipLaunchKernelGGL((k_bin_neigh<true>), dim3(nbins), dim3(BT), lds_neigh, s, c, xf.p, ty.p,
-                       dc, cnt.p, binE.p, binS.p, boff.p, nbr16.p);
+    hipLaunchKernelGGL((k_bin_neigh<true>), dim3(nbins), dim3(BT), lds_neigh, s, nbins, desc.p, xf.p,
+                       ty.p, dc, cnt.p, roff.p, binE.p, boff.p, nbr16.p);
     // entries proper (without padding) = sum of row counts
     size_t tb2 = 0;
     SPH_HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tb2, binE.p, mx.p, nbins, s));
@@ -405,8 +408,8 @@ struct sph_engine {
   void bin_rhosum_t() {
     auto k = k_bin_rhosum<DIM, NT1>;
     SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rho));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_rho, s, bin_ctx(), xf.p, ty.p, vr.p, cnt.p,
-                       boff.p, nbr16.p, dc);
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_rho, s, nbins, desc.p, xf.p, ty.p, vr.p,
+                       roff.p, boff.p, nbr16.p, dc);
   }
   void launch_bin_rhosum() {
     if (cfg.dim == 3) {
@@ -419,8 +422,8 @@ struct sph_engine {
   void bin_force_t() {
     auto k = k_bin_force<DIM, VISC, MODE, NT1>;
     SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_force, s, bin_ctx(), xf.p, vr.p, ty.p,
-                       en.p, cnt.p, boff.p, nbr16.p, dc, fo.p, de.p, cfg.gravity[0],
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_force, s, nbins, desc.p, xf.p, vr.p, ty.p,
+                       en.p, roff.p, boff.p, nbr16.p, dc, fo.p, de.p, cfg.gravity[0],
                        cfg.gravity[1], cfg.gravity[2]);
   }
   template <int DIM, bool NT1>
@@ -731,7 +734,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->h_scalar) (void)hipHostFree(e->h_scalar);
   if (e->h_total) (void)hipHostFree(e->h_total);
-  for (auto *b : {&e->obeg, &e->gbeg, &e->binE, &e->binS, &e->mx, &e->ccnt, &e->gowner2, &e->gimg2})
+  for (auto *b : {&e->obeg, &e->gbeg, &e->binE, &e->desc, &e->roff, &e->mx, &e->ccnt, &e->gowner2, &e->gimg2})
     b->release();
   e->okey.release();
   e->gkey.release();

@@ -29,7 +29,9 @@ SPH="atom_vec_meso.cpp atom_vec_meso_multiphase.cpp pair_sph_rhosum.cpp
      pair_sph_heatconduction_phasechange.cpp pair_sph_colorgradient.cpp
      sph_kernel_quintic.cpp sph_energy_equation.cpp"
 
-CXXFLAGS="-O2 -fPIC -w -std=gnu++98 -DLAMMPS_SMALLBIG -I$REF -I$REF/USER-SPH -I$REF/STUBS"
+# the reference's own serial build: g++ -O3 at the compiler's default C++ dialect (src/MAKE/
+# Makefile.serial:9-10); the dialect matters -- under C++98 pow(double,int) is __builtin_powi
+CXXFLAGS="-O3 -fPIC -w -DLAMMPS_SMALLBIG -I$REF -I$REF/USER-SPH -I$REF/STUBS"
 objs=()
 compile() {  # src obj
   if [ ! -f "$2" ] || [ "$1" -nt "$2" ]; then g++ $CXXFLAGS -c "$1" -o "$2"; fi

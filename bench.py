@@ -61,24 +61,73 @@ def c2_config(sph, n):
 
 
 def cpu_baseline(n_cpu, steps=2):
-    """Oracle C restatement (single core) on the same workload at n_cpu^3 particles:
-    `steps` non-rebuild steps + one neighbor rebuild amortised over 10 steps."""
+    """CPU baseline on the same C2 workload at n_cpu^3 particles, one core.
+
+    kind "reference": the reference's own USER-SPH compute code (oracle/_ref/libsph_ref.so,
+    compiled from /root/reference/src by oracle/build_ref.sh -- PairSPHRhoSum::compute,
+    PairSPHTaitwater::compute, Neighbor::full_bin, half_from_full_newton): rhosum on the
+    full list + taitwater on the half list, `steps` times, plus one list build amortised over
+    neigh_every = 10.  Falls back to the oracle's C restatement (kind "port")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
     s = po.cubic_lattice(n_cpu)
-    run = po.RefRun(s, po.c2_physics())
-    run.setup()
+    ph = po.c2_physics()
+    R = po.ref() if po.ref_available() else None
+    if R is None:
+        run = po.RefRun(s, ph)
+        run.setup()
+        t0 = time.perf_counter()
+        run.run(steps)                       # steps 1..steps: forward comm, no rebuild
+        t_steps = (time.perf_counter() - t0) / steps
+        t0 = time.perf_counter()
+        run._build()
+        t_build = time.perf_counter() - t0
+        per_step = t_steps + t_build / 10.0
+        return {"value": s.n / per_step, "unit": "particle-steps/s", "cores": 1, "kind": "port",
+                "sample": f"oracle/sph_oracle.c (scalar C restatement) on {s.n} particles "
+                          f"(same C2 physics): {steps} steps timed ({t_steps:.3f} s/step) + one "
+                          f"neighbor rebuild ({t_build:.2f} s) amortised over neigh_every=10"}
+    cns, cmax = po.cutneighsq(1, ph.cutmax(1), ph.skin)
+    g = po.borders(s, cmax)
+    args = (3, 1, g.nlocal, g.nghost, np.ascontiguousarray(g.x), g.type, s.boxlo, s.boxhi,
+            s.boxlo, s.boxhi, cmax, np.ascontiguousarray(cns))
     t0 = time.perf_counter()
-    run.run(steps)                       # steps 1..steps: forward comm, no rebuild
-    t_steps = (time.perf_counter() - t0) / steps
-    t0 = time.perf_counter()
-    run._build()
-    t_build = time.perf_counter() - t0
-    per_step = t_steps + t_build / 10.0
-    return {"value": s.n / per_step, "unit": "particle-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/sph_oracle.c (scalar C restatement) on {s.n} particles "
-                      f"(same C2 physics): {steps} steps timed ({t_steps:.3f} s/step) + one "
-                      f"neighbor rebuild ({t_build:.2f} s) amortised over neigh_every=10"}
+    foff = np.zeros(g.nlocal + 1, dtype=np.int64)
+    tot = R.ref_neigh_full(*args, foff, None, 0)
+    fnb = np.zeros(tot, dtype=np.int32)
+    R.ref_neigh_full(*args, foff, fnb.ctypes.data, tot)
+    hoff = np.zeros(g.nlocal + 1, dtype=np.int64)
+    htot = R.ref_neigh_half_from_full(g.nlocal, g.nghost, g.x, foff, fnb, hoff, None)
+    hnb = np.zeros(htot, dtype=np.int32)
+    R.ref_neigh_half_from_full(g.nlocal, g.nghost, g.x, foff, fnb, hoff, hnb.ctypes.data)
+    t_build = (time.perf_counter() - t0) / 2.0   # two passes of full_bin (count + fill)
+    rho = g.gather(s.rho)
+    vest = g.gather(s.v)
+    f = np.zeros((g.nall, 3))
+    drho = np.zeros(g.nall)
+    de = np.zeros(g.nall)
+    cut = np.ascontiguousarray(ph.tait_cut)
+    visc = np.ascontiguousarray(ph.visc)
+    t_rho = t_tait = 0.0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        R.ref_rhosum(3, 1, g.nlocal, g.nghost, g.x, g.type, s.mass, cut, foff, fnb, rho)
+        t1 = time.perf_counter()
+        R.ref_taitwater(3, 1, g.nlocal, g.nghost, 1, g.x, vest, rho, g.type, s.mass, ph.rho0,
+                        ph.c0, visc, cut, hoff, hnb, f, drho, de)
+        t2 = time.perf_counter()
+        t_rho += (t1 - t0) / steps
+        t_tait += (t2 - t1) / steps
+    per_step = t_rho + t_tait + t_build / 10.0
+    return {"value": s.n / per_step, "unit": "particle-steps/s", "cores": 1,
+            "kind": "reference",
+            "sample": f"reference USER-SPH compute code (oracle/_ref, built from the reference "
+                      f"sources, g++ -O3) on {s.n} particles, same C2 inputs: "
+                      f"PairSPHRhoSum::compute {t_rho:.3f} s + PairSPHTaitwater::compute "
+                      f"{t_tait:.3f} s per step (mean of {steps}) + Neighbor::full_bin + "
+                      f"half_from_full_newton {t_build:.2f} s amortised over neigh_every=10; "
+                      f"comm/integrate (<1%) not included",
+            "pair_only_particle_steps_per_s": s.n / (t_rho + t_tait)}
 
 
 def main():
@@ -89,6 +138,8 @@ def main():
     ap.add_argument("--n", type=int, default=100, help="lattice edge (n^3 particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
+    ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
+                    help="pair-kernel path: 0 = LDS-staged bins, 1 = CSR rows")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +156,9 @@ def main():
     dev = local % ndev
 
     x, v, t, rho, e, cv = make_system(args.n, 12345 + rank)
-    eng = sph.Engine(c2_config(sph, args.n), device=dev)
+    cfg = c2_config(sph, args.n)
+    cfg.kernel_path = args.path
+    eng = sph.Engine(cfg, device=dev)
     eng.set_atoms(x, v, t, rho, e, cv)
     eng.setup()
     eng.run(args.warmup)
@@ -161,8 +214,10 @@ def main():
                                "periodic, skin 0.3, rebuild every 10",
                    "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "parallelism": f"{world} independent 1M boxes (one per GPU)"},
-        "roofline": {"bound": "hbm", "kernel": "k_force<TAIT> (sph/taitwater pass)",
+                   "parallelism": f"{world} independent 1M boxes (one per GPU)",
+                   "kernel_path": "lds-staged bins" if st["staged"] else "csr rows"},
+        "roofline": {"bound": "hbm", "kernel": ("k_bin_force" if st["staged"] else "k_force")
+                     + "<TAIT> (sph/taitwater pass)",
                      "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,
                      "bytes_per_particle": bytes_tait, "ms_per_launch": ms_tait},

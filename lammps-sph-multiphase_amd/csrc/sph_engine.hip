@@ -158,7 +158,10 @@ struct sph_engine {
     bkey2.reserve(n);
     bidx.reserve(n);
     bidx2.reserve(n);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p, bidx.p);
+    // Morton order unless the staged path needs linear bins (and bins fit 10 bits/axis)
+    const bool mort = !want_staged() && bn.nb[0] <= 1024 && bn.nb[1] <= 1024 && bn.nb[2] <= 1024;
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p,
+                       bidx.p, mort ? 1 : 0);
     size_t tb = 0;
     SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
     tmp_reserve(tb);
@@ -191,7 +194,7 @@ struct sph_engine {
     bkey2.reserve(ng);
     bidx.reserve(ng);
     bidx2.reserve(ng);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p, bkey.p, bidx.p);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p, bkey.p, bidx.p, 0);
     int endbit = 1;
     while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
     size_t tb = 0;
@@ -365,7 +368,7 @@ struct sph_engine {
     bidx2.reserve(nall);
     bstart.reserve(nbins);
     bend.reserve(nbins);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, bn, xf.p, bkey.p, bidx.p);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, bn, xf.p, bkey.p, bidx.p, 0);
     int endbit = 1;
     while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
     size_t tb = 0;

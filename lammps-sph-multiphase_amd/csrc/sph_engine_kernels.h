@@ -204,15 +204,31 @@ __device__ __forceinline__ int bin_coord(double x, double lo, double inv, int nb
   return c < 0 ? 0 : (c >= nb ? nb - 1 : c);
 }
 
+// spread the low 10 bits of v to every third bit (Morton interleave)
+__device__ __forceinline__ unsigned spread3(unsigned v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000ffu;
+  v = (v | (v << 8)) & 0x0300f00fu;
+  v = (v | (v << 4)) & 0x030c30c3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// Sort keys: linear bin index (x fastest; the staged path needs each x-row of bins
+// contiguous), or the bins' Morton code (morton != 0; the CSR path's row order: a run
+// of consecutive rows then covers a compact block of space, so the neighbor records a
+// wave of rows gathers stay within one XCD's L2).
 static __global__ void k_bin_keys(int n, int first, Bins bn, const double4 *__restrict__ xf,
-                                  unsigned *__restrict__ key, int *__restrict__ idx) {
+                                  unsigned *__restrict__ key, int *__restrict__ idx,
+                                  int morton = 0) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const double4 x = xf[first + k];
   const int cx = bin_coord(x.x, bn.lo[0], bn.inv[0], bn.nb[0]);
   const int cy = bin_coord(x.y, bn.lo[1], bn.inv[1], bn.nb[1]);
   const int cz = bin_coord(x.z, bn.lo[2], bn.inv[2], bn.nb[2]);
-  key[k] = (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
+  key[k] = morton ? (spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2))
+                  : (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
   idx[k] = first + k;
 }
 

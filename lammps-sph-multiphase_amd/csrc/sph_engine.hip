@@ -18,9 +18,35 @@
 #include "sph_dispatch.h"
 #include "sph_bin_kernels.h"
 #include "sph_engine_kernels.h"
+#include "sph_row_kernels.h"
 #include "sph_util.h"
 
 using namespace sph;
+
+namespace sph {
+static int env_int(const char *name, int dflt) {
+  const char *s = getenv(name);
+  return s ? atoi(s) : dflt;
+}
+// SPH_ROWTILE: tile shape index of SPH_ROW_TILES (tuning; default 3 = 16 lanes x 2 pairs,
+// the fastest measured on C2 1M: tools/sweep_rowtile.sh)
+int row_tile() {
+  static int t = env_int("SPH_ROWTILE", 3);
+  return t;
+}
+}  // namespace sph
+// SPH_ROWK=0 routes the engine through the generic pair-layer kernels (comparison only)
+// list builder (default 2, fastest end to end on C2 1M: tools/sweep_neigh.sh):
+// 3 = binned copy over full-size bins (27-bin stencil, rows in lockstep),
+// 2 = binned copy over half-size bins with per-row trimming, 1 = bidx-indirect (original)
+static int neigh_q() {
+  static int v = env_int("SPH_NEIGH", 2);
+  return v == 1 ? 0 : v;
+}
+static bool row_kernels() {
+  static bool on = env_int("SPH_ROWK", 1) != 0;
+  return on;
+}
 
 namespace {
 
@@ -68,6 +94,10 @@ struct sph_engine {
   // bins
   Bins bn{};
   int nbins = 0;
+  QBins qb{};
+  int nqbins = 0;
+  DBuf<int> qbeg, tb;
+  DBuf<double4> xb;
   DBuf<unsigned> bkey, bkey2;
   DBuf<int> bidx, bidx2, bstart, bend;
   // neighbor list
@@ -358,6 +388,86 @@ struct sph_engine {
       }
     }
     nbins = bn.nb[0] * bn.nb[1] * bn.nb[2];
+    // half-size bins of the CSR list builder (k_neigh2, reach 2)
+    for (int k = 0; k < 3; k++) {
+      const double ext = bn.nb[k] > 0 && bn.inv[k] > 0.0 ? bn.nb[k] / bn.inv[k] : 0.0;
+      int nb = 1;
+      if (k < cfg.dim) {
+        nb = (int)(ext / (neigh_q() == 2 ? 0.5 * cutneighmax : cutneighmax));
+        if (nb < 1) nb = 1;
+        if (nb > 8192) nb = 8192;
+      }
+      qb.lo[k] = bn.lo[k];
+      qb.nb[k] = nb;
+      qb.inv[k] = (k < cfg.dim) ? nb / ext : 0.0;
+      qb.size[k] = (k < cfg.dim) ? ext / nb : 1.0;
+    }
+    qb.cutmaxsq = cutneighmax * cutneighmax;
+    nqbins = qb.nb[0] * qb.nb[1] * qb.nb[2];
+  }
+
+  // CSR full list over half-size bins and a bin-ordered copy of all atoms
+  void build_list_q() {
+    const int n = nlocal, nall = nlocal + nghost;
+    Bins b;
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = qb.lo[k];
+      b.inv[k] = qb.inv[k];
+      b.nb[k] = qb.nb[k];
+    }
+    bkey.reserve(nall);
+    bkey2.reserve(nall);
+    bidx.reserve(nall);
+    bidx2.reserve(nall);
+    qbeg.reserve(nqbins + 1);
+    xb.reserve(nall);
+    tb.reserve(nall);
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, b, xf.p,
+                       bkey.p, bidx.p, 0);
+    int endbit = 1;
+    while ((1u << endbit) < (unsigned)nqbins && endbit < 32) endbit++;
+    size_t tbytes = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
+    tmp_reserve(tbytes);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tbytes, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
+    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nqbins + 1)), dim3(BLK), 0, s, nqbins, nall,
+                       0, bkey2.p, qbeg.p);
+    hipLaunchKernelGGL(k_bin_copy, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bidx2.p, xf.p,
+                       ty.p, xb.p, tb.p);
+    ccnt.reserve(n + 1);
+    off.reserve(n + 1);
+    constexpr int G = 8, U = 2;
+    dim3 grid(grid_for_rows(n, G)), block(BLK);
+    auto launch = [&](bool fill) {
+      if (n == 0) return;
+      const bool t = nt1(), q2 = neigh_q() == 2;
+#define SPH_NQ(F, T, R, TR)                                                                  \
+  hipLaunchKernelGGL((k_neigh2<G, U, F, T, R, TR>), grid, block, 0, s, n, qb, cfg.dim, xf.p, \
+                     ty.p, xb.p, tb.p, qbeg.p, dc, F ? (int *)nullptr : ccnt.p,                \
+                     F ? off.p : (const int *)nullptr, F ? nbr.p : (int *)nullptr)
+      if (fill) {
+        if (q2) { if (t) SPH_NQ(true, true, 2, true); else SPH_NQ(true, false, 2, true); }
+        else { if (t) SPH_NQ(true, true, 1, false); else SPH_NQ(true, false, 1, false); }
+      } else {
+        if (q2) { if (t) SPH_NQ(false, true, 2, true); else SPH_NQ(false, false, 2, true); }
+        else { if (t) SPH_NQ(false, true, 1, false); else SPH_NQ(false, false, 1, false); }
+      }
+#undef SPH_NQ
+    };
+    launch(false);
+    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
+    size_t tb2 = 0;
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, off.p, off.p, n + 1, s));
+    tmp_reserve(tb2);
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb2, off.p, off.p, n + 1, s));
+    const int tot = read_scalar(off.p + n);
+    SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
+    nbr.reserve(tot > 0 ? tot : 1);
+    launch(true);
+    if (!staged) {
+      nbr_total = tot;
+      nbr_builds++;
+    }
   }
 
   void build_bins() {
@@ -464,8 +574,12 @@ struct sph_engine {
       staged = build_staged();
     }
     if (!staged || need_csr) {
-      build_bins();
-      build_list();
+      if (neigh_q()) {
+        build_list_q();
+      } else {
+        build_bins();
+        build_list();
+      }
     }
   }
 
@@ -481,6 +595,24 @@ struct sph_engine {
                        gowner.p, gimg.p, xf.p, vr.p, en.p);
   }
 
+  RowArgs row_args() {
+    RowArgs a;
+    a.n = nlocal;
+    a.off = off.p;
+    a.nbr = nbr.p;
+    a.xf = xf.p;
+    a.vr = vr.p;
+    a.ty = ty.p;
+    a.en = en.p;
+    a.cf = dc;
+    a.fo = fo.p;
+    a.de = de.p;
+    a.gx = cfg.gravity[0];
+    a.gy = cfg.gravity[1];
+    a.gz = cfg.gravity[2];
+    return a;
+  }
+
   void pair_compute(bool do_rhosum, bool setup = false) {
     const int nall = nlocal + nghost;
     if (do_rhosum) {
@@ -489,8 +621,12 @@ struct sph_engine {
         if (staged) {
           launch_bin_rhosum();
         } else {
-          RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
-          launch_rhosum(cfg.dim, true, nt1(), s, ra);
+          if (row_kernels()) {
+            row_rhosum(nt1(), s, row_args());
+          } else {
+            RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
+            launch_rhosum(cfg.dim, true, nt1(), s, ra);
+          }
         }
       }
       if (nghost) {
@@ -506,6 +642,9 @@ struct sph_engine {
     } else if (force_mode && staged) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       launch_bin_force();
+    } else if (force_mode && row_kernels()) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      row_force(nt1(), cfg.tait_visc, force_mode, s, row_args());
     } else if (force_mode) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       ForceArgs a{};
@@ -741,6 +880,9 @@ int sph_engine_destroy(sph_engine *e) {
     b->release();
   e->okey.release();
   e->gkey.release();
+  e->qbeg.release();
+  e->tb.release();
+  e->xb.release();
   e->blen.release();
   e->boff.release();
   e->nbr16.release();

@@ -334,6 +334,114 @@ k_neigh(int nlocal, Bins bn, int dim, const double4 *__restrict__ xf,
   }
 }
 
+// ---- CSR full-list build over a binned copy ----------------------------------------
+// Bins here are >= cutneighmax / 2 (reach S = 2 bins).  Every atom, owned or ghost, is
+// copied in bin order into xb (x, y, z, atom index as a double) so that a stencil row is
+// one contiguous, coalesced range; per (dy, dz) row of bins the x-range is trimmed to the
+// bins that can hold a point within cutneighmax of x_i, and rows whose y/z slab distance
+// already exceeds it are skipped.  The trimming is conservative (slab distances shrunk
+// by a margin) -- membership itself is decided only by rsq <= cutneighsq[it][jt] in
+// fp64, exactly as Neighbor::full_bin (neigh_full.cpp:241-344).
+struct QBins {
+  double lo[3], inv[3], size[3];
+  int nb[3];
+  double cutmaxsq;
+};
+
+static __global__ void k_bin_copy(int n, const int *__restrict__ perm,
+                                  const double4 *__restrict__ xf, const int *__restrict__ ty,
+                                  double4 *__restrict__ xb, int *__restrict__ tb) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int j = perm[p];
+  const double4 x = xf[j];
+  xb[p] = make_double4(x.x, x.y, x.z, (double)j);
+  tb[p] = ty[j];
+}
+
+// distance from coordinate v to bin b's slab along one axis (0 inside), shrunk by a margin
+__device__ __forceinline__ double slab_gap(double v, int b, int c, double lo, double size) {
+  if (b == c) return 0.0;
+  const double edge = (b < c) ? lo + (b + 1) * size : lo + b * size;
+  const double g = (b < c) ? v - edge : edge - v;
+  return fmax(g - 1e-6 * size, 0.0);
+}
+
+template <int G, int U, bool FILL, bool NT1, int R, bool TRIM>
+__global__ void __launch_bounds__(256)
+k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
+         const int *__restrict__ ty, const double4 *__restrict__ xb,
+         const int *__restrict__ tb, const int *__restrict__ beg,
+         const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
+         int *__restrict__ nbr) {
+  __shared__ double s_cns[NT2];
+  const int nt1 = cf->ntypes + 1;
+  if (!NT1) {
+    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
+    __syncthreads();
+  }
+  const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (i >= nlocal) return;
+  const double4 xi = xf[i];
+  const double *crow = s_cns + (NT1 ? 0 : ty[i] * nt1);
+  const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
+  const int cx = bin_coord(xi.x, q.lo[0], q.inv[0], q.nb[0]);
+  const int cy = bin_coord(xi.y, q.lo[1], q.inv[1], q.nb[1]);
+  const int cz = bin_coord(xi.z, q.lo[2], q.inv[2], q.nb[2]);
+  const int zr = (dim == 3) ? R : 0;
+  const double di = (double)i;
+  int n = 0;
+  int pos = FILL ? off[i] : 0;
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+  for (int bz = max(cz - zr, 0); bz <= min(cz + zr, q.nb[2] - 1); bz++) {
+    const double gz = (TRIM && dim == 3) ? slab_gap(xi.z, bz, cz, q.lo[2], q.size[2]) : 0.0;
+    for (int by = max(cy - R, 0); by <= min(cy + R, q.nb[1] - 1); by++) {
+      int bx0 = max(cx - R, 0), bx1 = min(cx + R, q.nb[0] - 1);
+      if (TRIM) {
+        const double gy = slab_gap(xi.y, by, cy, q.lo[1], q.size[1]);
+        const double d2 = gy * gy + gz * gz;
+        if (d2 > q.cutmaxsq) continue;
+        const double ext = sqrt(q.cutmaxsq - d2) * (1.0 + 1e-9) + 1e-9 * q.size[0];
+        bx0 = bin_coord(xi.x - ext, q.lo[0], q.inv[0], q.nb[0]);
+        bx1 = bin_coord(xi.x + ext, q.lo[0], q.inv[0], q.nb[0]);
+      }
+      const int brow = (bz * q.nb[1] + by) * q.nb[0];
+      const int s = beg[brow + bx0], e = beg[brow + bx1 + 1];
+      for (int base = s; base < e; base += G * U) {  // group-uniform trip count
+        const int b0 = base + lane;
+        double4 xj[U];
+        int tj[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int p = min(b0 + u * G, e - 1);
+          xj[u] = xb[p];
+          tj[u] = NT1 ? 1 : tb[p];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+          const double rsq = dx * dx + dy * dy + dz * dz;
+          const bool hit = (b0 + u * G < e) && (xj[u].w != di) &&
+                           rsq <= (NT1 ? cns1 : crow[tj[u]]);
+          if (FILL) {
+            const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
+            if (hit) nbr[pos + __popcll(m & ((1ull << lane) - 1ull))] = (int)xj[u].w;
+            pos += __popcll(m);
+          } else {
+            n += hit ? 1 : 0;
+          }
+        }
+      }
+    }
+  }
+  if (!FILL) {
+    n = group_sum_i<G>(n);
+    if (lane == 0) cnt[i] = n;
+  }
+}
+
 static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__restrict__ off) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) off[i] = cnt[i];

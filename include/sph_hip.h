@@ -111,6 +111,43 @@ int sph_hip_taitwater(sph_hip_ctx *ctx, double *f, double *drho, double *de,
 int sph_hip_heatconduction(sph_hip_ctx *ctx, double *de);
 
 /* ======================================================================================
+ * 1b. Multiphase styles (atom_style meso/multiphase: per-atom rmass; quintic kernel).
+ *     Tables are (nt+1)^2 row-major; like coeff()+init_one() the upper triangle i <= j is
+ *     read and mirrored.  Stage atoms with sph_hip_atoms (x, vest, rho, e, type) and then
+ *     sph_hip_atoms_multiphase (rmass, cv: nlocal + nghost each; cv may be NULL).
+ * ==================================================================================== */
+int sph_hip_atoms_multiphase(sph_hip_ctx *ctx, const double *rmass, const double *cv);
+
+/* PairSPHRhoSumMultiphase (pair_sph_rhosum_multiphase.cpp:112-167, coeff :194-216):
+   cut = h per pair; rho[0..nlocal) <- rmass_i (W(0)/h_ii^d + sum_j W(r/h)/h^d).  Full list. */
+int sph_hip_rhosum_multiphase_coeff(sph_hip_ctx *ctx, const double *cut);
+int sph_hip_rhosum_multiphase(sph_hip_ctx *ctx, double *rho);
+
+/* PairSPHTaitwaterMultiphase (pair_sph_taitwater_multiphase.cpp:95-183, coeff :225-262):
+   per type rho0, soundspeed, gamma, rbackground (B = c^2 rho0 / gamma); per pair viscosity
+   and cut.  f (nall*3) is ACCUMULATED; HALF lists scatter onto j (newton_pair) exactly as
+   the reference, including its p_j = p(rho_j; gamma[itype]) asymmetry. */
+int sph_hip_taitwater_multiphase_coeff(sph_hip_ctx *ctx, const double *rho0,
+                                       const double *soundspeed, const double *gamma,
+                                       const double *rbackground, const double *viscosity,
+                                       const double *cut);
+int sph_hip_taitwater_multiphase(sph_hip_ctx *ctx, double *f);
+
+/* PairSPHHeatConductionPhaseChange (pair_sph_heatconduction_phasechange.cpp:81-138, coeff
+   :177-225): alpha, cut per pair; fixflag (int, the type whose temperature is clamped, 0 =
+   none) and tc per pair, either may be NULL (4-argument coeff form).  de (nall) is
+   ACCUMULATED. */
+int sph_hip_heatconduction_phasechange_coeff(sph_hip_ctx *ctx, const double *alpha,
+                                             const int *fixflag, const double *tc,
+                                             const double *cut);
+int sph_hip_heatconduction_phasechange(sph_hip_ctx *ctx, double *de);
+
+/* PairSPHColorGradient (pair_sph_colorgradient.cpp:118-187): alpha, cut per pair;
+   cg[0..nlocal)*3 is OVERWRITTEN (the reference zeroes it first).  Full list. */
+int sph_hip_colorgradient_coeff(sph_hip_ctx *ctx, const double *alpha, const double *cut);
+int sph_hip_colorgradient(sph_hip_ctx *ctx, double *cg);
+
+/* ======================================================================================
  * 2. Device-resident engine
  * ==================================================================================== */
 #define SPH_MAXTYPES 8

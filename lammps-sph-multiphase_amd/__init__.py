@@ -93,6 +93,15 @@ EXPORTS = {
     "sph_hip_rhosum": (_i, [_vp, _dp]),
     "sph_hip_taitwater": (_i, [_vp, _dp, _dp, _dp, _vp]),
     "sph_hip_heatconduction": (_i, [_vp, _dp]),
+    "sph_hip_atoms_multiphase": (_i, [_vp, _dp, _vp]),
+    "sph_hip_rhosum_multiphase_coeff": (_i, [_vp, _dp]),
+    "sph_hip_rhosum_multiphase": (_i, [_vp, _dp]),
+    "sph_hip_taitwater_multiphase_coeff": (_i, [_vp, _dp, _dp, _dp, _dp, _dp, _dp]),
+    "sph_hip_taitwater_multiphase": (_i, [_vp, _dp]),
+    "sph_hip_heatconduction_phasechange_coeff": (_i, [_vp, _dp, _vp, _vp, _dp]),
+    "sph_hip_heatconduction_phasechange": (_i, [_vp, _dp]),
+    "sph_hip_colorgradient_coeff": (_i, [_vp, _dp, _dp]),
+    "sph_hip_colorgradient": (_i, [_vp, _dp]),
     "sph_engine_create": (_i, [_i, C.POINTER(EngineConfig), C.POINTER(_vp)]),
     "sph_engine_destroy": (_i, [_vp]),
     "sph_engine_comm_uid": (_i, [_vp]),
@@ -212,6 +221,45 @@ class PairContext:
 
     def heatconduction(self, de):
         _chk(self.L.sph_hip_heatconduction(self.h, de))
+
+    # -- multiphase styles (section 1b) --------------------------------------------------
+    def atoms_multiphase(self, rmass, cv=None):
+        rmass = np.ascontiguousarray(rmass, dtype=np.float64)
+        cv = None if cv is None else np.ascontiguousarray(cv, dtype=np.float64)
+        _chk(self.L.sph_hip_atoms_multiphase(self.h, rmass, _ptr(cv)))
+        self._keep_mp = (rmass, cv)
+
+    def rhosum_multiphase_coeff(self, cut):
+        _chk(self.L.sph_hip_rhosum_multiphase_coeff(self.h, self._t(cut)))
+
+    def rhosum_multiphase(self, rho):
+        _chk(self.L.sph_hip_rhosum_multiphase(self.h, rho))
+        return rho
+
+    def taitwater_multiphase_coeff(self, rho0, c0, gamma, rbackground, visc, cut):
+        _chk(self.L.sph_hip_taitwater_multiphase_coeff(
+            self.h, self._t(rho0), self._t(c0), self._t(gamma), self._t(rbackground),
+            self._t(visc), self._t(cut)))
+
+    def taitwater_multiphase(self, f):
+        _chk(self.L.sph_hip_taitwater_multiphase(self.h, f))
+
+    def heatconduction_phasechange_coeff(self, alpha, cut, fixflag=None, tc=None):
+        ff = None if fixflag is None else np.ascontiguousarray(fixflag, dtype=np.int32).ravel()
+        tcv = None if tc is None else self._t(tc)
+        self._keep_hpc = (ff, tcv)
+        _chk(self.L.sph_hip_heatconduction_phasechange_coeff(self.h, self._t(alpha), _ptr(ff),
+                                                            _ptr(tcv), self._t(cut)))
+
+    def heatconduction_phasechange(self, de):
+        _chk(self.L.sph_hip_heatconduction_phasechange(self.h, de))
+
+    def colorgradient_coeff(self, alpha, cut):
+        _chk(self.L.sph_hip_colorgradient_coeff(self.h, self._t(alpha), self._t(cut)))
+
+    def colorgradient(self, cg):
+        _chk(self.L.sph_hip_colorgradient(self.h, cg))
+        return cg
 
 
 # ------------------------------------------------------------------------------------------

@@ -1,0 +1,260 @@
+// sph_mp_kernels.h -- gfx950 kernels of the multiphase USER-SPH styles (atom_style
+// meso/multiphase: per-atom rmass; quintic spline kernel):
+//   sph/rhosum/multiphase          pair_sph_rhosum_multiphase.cpp:112-167      (full list)
+//   sph/taitwater/multiphase       pair_sph_taitwater_multiphase.cpp:95-183    (half list)
+//   sph/heatconduction/phasechange pair_sph_heatconduction_phasechange.cpp:81-138 (half)
+//   sph/colorgradient              pair_sph_colorgradient.cpp:118-187          (full list)
+// Same walk as sph_kernels.h: G lanes per list row, register accumulation, xor-shuffle
+// group reduction; half lists scatter the Newton-3 share onto j with fp64 atomics, as the
+// reference does.  The two half-list styles are NOT pair-symmetric in the reference
+// (p_j takes gamma[itype], pair_sph_taitwater_multiphase.cpp:148; the fixed-temperature
+// clamp depends on which atom is i, pair_sph_heatconduction_phasechange.cpp:124-129), so
+// they follow the caller's half list exactly instead of being rewritten as gathers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sph_kernels.h"
+
+namespace sph {
+
+struct MpCoefs {
+  int ntypes, dim;
+  // rhosum/multiphase: h = cut[it][jt]
+  double rcut[NT2], rcutsq[NT2];
+  // taitwater/multiphase: per type rho0, B = c^2 rho0 / gamma, gamma, rbackground
+  double rho0[MAXT + 1], B[MAXT + 1], gamma[MAXT + 1], rbg[MAXT + 1];
+  double tvisc[NT2], tcut[NT2], tcutsq[NT2];
+  // heatconduction/phasechange
+  double halpha[NT2], hcut[NT2], hcutsq[NT2], htc[NT2];
+  int hfix[NT2];
+  // colorgradient
+  double calpha[NT2], ccut[NT2], ccutsq[NT2];
+};
+
+// Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r, pow() of the reference kept)
+__device__ __forceinline__ double quintic_w(int dim, double r) {
+  const double norm = (dim == 3) ? 0.0716197243913529 : 0.04195297663091802;
+  const double s = 3.0 * r;
+  if (s < 1.0) return norm * (pow(3 - s, 5) - 6 * pow(2 - s, 5) + 15 * pow(1 - s, 5));
+  if (s < 2.0) return norm * (pow(3 - s, 5) - 6 * pow(2 - s, 5));
+  if (s < 3.0) return norm * pow(3 - s, 5);
+  return 0.0;
+}
+__device__ __forceinline__ double quintic_dw(int dim, double r) {
+  const double norm = 3.0 * ((dim == 3) ? 0.0716197243913529 : 0.04195297663091802);
+  const double s = 3.0 * r;
+  double wfd;
+  if (s < 1) {
+    wfd = -50 * pow(s, 4) + 120 * pow(s, 3) - 120 * s;
+  } else if (s < 2) {
+    wfd = 25 * pow(s, 4) - 180 * pow(s, 3) + 450 * pow(s, 2) - 420 * s + 75;
+  } else if (s < 3.0) {
+    wfd = -5 * pow(s, 4) + 60 * pow(s, 3) - 270 * pow(s, 2) + 540 * s - 405;
+  } else {
+    wfd = 0.0;
+  }
+  return norm * wfd;
+}
+
+struct MpArgs {
+  int inum, nlocal, newton, dim, half;
+  const int *ilist, *off, *nbr;
+  const double4 *xf;  // x, y, z, (unused)
+  const double4 *vr;  // vest, rho
+  const int *ty;
+  const double *rm, *en, *cv;
+  const MpCoefs *mc;
+  double *rho;    // rhosum out (nall)
+  double4 *fo;    // taitwater out (nall, x y z used)
+  double *de;     // heat out (nall)
+  double4 *cg;    // colorgradient out (nall)
+};
+
+template <int G>
+__global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int nt1 = c->ntypes + 1;
+  const int i = a.ilist[row];
+  const double4 xi = a.xf[i];
+  const int it = a.ty[i];
+  const int dim = a.dim;
+  double acc = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int j = a.nbr[k];
+    const double4 xj = a.xf[j];
+    const int jt = a.ty[j];
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (rsq < c->rcutsq[it * nt1 + jt]) {
+      const double ih = 1.0 / c->rcut[it * nt1 + jt];
+      const double r = sqrt(rsq) * ih;
+      acc += (dim == 3) ? quintic_w(3, r) * ih * ih * ih : quintic_w(2, r) * ih * ih;
+    }
+  }
+  acc = group_sum<G>(acc);
+  if (lane == 0) {
+    const double h = c->rcut[it * nt1 + it];
+    const double self = (dim == 3) ? quintic_w(3, 0.0) / (h * h * h) : quintic_w(2, 0.0) / (h * h);
+    a.rho[i] = (self + acc) * a.rm[i];
+  }
+}
+
+// p = B (pow(rho/rho0, gamma) - rbackground), pair_sph_taitwater_multiphase.cpp:289-292
+__device__ __forceinline__ double mp_pressure(double B, double rho0, double gamma, double rbg,
+                                              double rho) {
+  return B * (pow(rho / rho0, gamma) - rbg);
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) k_mp_tait(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int nt1 = c->ntypes + 1;
+  const int i = a.ilist[row];
+  const double4 xi = a.xf[i], vi = a.vr[i];
+  const int it = a.ty[i];
+  const double rhoi = vi.w;
+  const double pi = mp_pressure(c->B[it], c->rho0[it], c->gamma[it], c->rbg[it], rhoi);
+  const double Vi = a.rm[i] / rhoi;
+  const double Vi2 = Vi * Vi;
+  double fx = 0.0, fy = 0.0, fz = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int j = a.nbr[k];
+    const double4 xj = a.xf[j], vj = a.vr[j];
+    const int jt = a.ty[j];
+    const int p = it * nt1 + jt;
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (!(rsq < c->tcutsq[p])) continue;
+    const double ih = 1.0 / c->tcut[p];
+    const double r = sqrt(rsq);
+    double wfd;
+    if (a.dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih / r;
+    else wfd = quintic_dw(2, r * ih) * ih * ih * ih / r;
+    const double rhoj = vj.w;
+    const double Vj = a.rm[j] / rhoj;
+    const double Vj2 = Vj * Vj;
+    // reference quirk kept: p_j with gamma[itype] (pair_sph_taitwater_multiphase.cpp:148)
+    const double pj = mp_pressure(c->B[jt], c->rho0[jt], c->gamma[it], c->rbg[jt], rhoj);
+    const double pij = (rhoj * pi + rhoi * pj) / (rhoi + rhoj);
+    const double velx = vi.x - vj.x, vely = vi.y - vj.y, velz = vi.z - vj.z;
+    const double fvisc = (Vi2 + Vj2) * c->tvisc[p] * wfd;
+    const double fpair = -(Vi2 + Vj2) * pij * wfd;
+    const double tx = dx * fpair + velx * fvisc;
+    const double ty_ = dy * fpair + vely * fvisc;
+    const double tz = dz * fpair + velz * fvisc;
+    fx += tx;
+    fy += ty_;
+    fz += tz;
+    if (a.half && (a.newton || j < a.nlocal)) {
+      atomicAdd(&a.fo[j].x, -tx);
+      atomicAdd(&a.fo[j].y, -ty_);
+      atomicAdd(&a.fo[j].z, -tz);
+    }
+  }
+  fx = group_sum<G>(fx);
+  fy = group_sum<G>(fy);
+  fz = group_sum<G>(fz);
+  if (lane == 0) {
+    if (a.half) {
+      atomicAdd(&a.fo[i].x, fx);
+      atomicAdd(&a.fo[i].y, fy);
+      atomicAdd(&a.fo[i].z, fz);
+    } else {
+      a.fo[i].x += fx;
+      a.fo[i].y += fy;
+      a.fo[i].z += fz;
+    }
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) k_mp_heat(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int nt1 = c->ntypes + 1;
+  const int i = a.ilist[row];
+  const double4 xi = a.xf[i];
+  const int it = a.ty[i];
+  const double rhoi = a.vr[i].w;
+  const double mi = a.rm[i];
+  const double Ti0 = a.en[i] / a.cv[i];   // sph_energy2t, sph_energy_equation.cpp:16-18
+  double dE = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int j = a.nbr[k];
+    const double4 xj = a.xf[j];
+    const int jt = a.ty[j];
+    const int p = it * nt1 + jt;
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (!(rsq < c->hcutsq[p])) continue;
+    const double ih = 1.0 / c->hcut[p];
+    double wfd;
+    if (a.dim == 3) {
+      wfd = quintic_dw(3, sqrt(rsq) * ih);
+      wfd = wfd * ih * ih * ih * ih / sqrt(rsq);
+    } else {
+      wfd = quintic_dw(2, sqrt(rsq) * ih);
+      wfd = wfd * ih * ih * ih / sqrt(rsq);
+    }
+    double Ti = Ti0;
+    double Tj = a.en[j] / a.cv[j];
+    const int ff = c->hfix[p];
+    if (ff == it && Ti < Tj) Ti = c->htc[p];
+    if (ff == jt && Tj < Ti) Tj = c->htc[p];
+    const double deltaE = 2.0 * c->halpha[p] * (Ti - Tj) * wfd / (rhoi * a.vr[j].w);
+    dE += deltaE * a.rm[j];
+    if (a.half && (a.newton || j < a.nlocal)) atomicAdd(&a.de[j], -deltaE * mi);
+  }
+  dE = group_sum<G>(dE);
+  if (lane == 0) {
+    if (a.half) atomicAdd(&a.de[i], dE);
+    else a.de[i] += dE;
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int nt1 = c->ntypes + 1;
+  const int i = a.ilist[row];
+  const double4 xi = a.xf[i];
+  const int it = a.ty[i];
+  const double sigmai = a.vr[i].w / a.rm[i];
+  double gx = 0.0, gy = 0.0, gz = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int j = a.nbr[k];
+    const double4 xj = a.xf[j];
+    const int jt = a.ty[j];
+    const int p = it * nt1 + jt;
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (!(rsq < c->ccutsq[p])) continue;
+    const double r = sqrt(rsq);
+    const double ih = 1.0 / c->ccut[p];
+    double wfd;
+    if (a.dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih;
+    else wfd = quintic_dw(2, r * ih) * ih * ih * ih;
+    const double sigmaj = a.vr[j].w / a.rm[j];
+    const double dphi = -wfd * c->calpha[p] / (sigmaj * sigmaj) * sigmai;
+    gx += dphi * (dx / r);
+    gy += dphi * (dy / r);
+    if (a.dim == 3) gz += dphi * (dz / r);
+  }
+  gx = group_sum<G>(gx);
+  gy = group_sum<G>(gy);
+  gz = group_sum<G>(gz);
+  if (lane == 0) a.cg[i] = make_double4(gx, gy, gz, 0.0);
+}
+
+}  // namespace sph

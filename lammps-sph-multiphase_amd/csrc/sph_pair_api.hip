@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "sph_coef.h"
+#include "sph_ctx.h"
 #include "sph_dispatch.h"
 #include "sph_util.h"
 
@@ -48,30 +49,6 @@ void require_device(int device) {
 }  // namespace sph
 
 using namespace sph;
-
-struct sph_hip_ctx {
-  int device = 0, dim = 3, ntypes = 1, newton = 1;
-  hipStream_t stream = nullptr;
-  Coefs hc{};
-  Coefs *dc = nullptr;
-  bool have_rho = false, have_tait = false, have_heat = false;
-  int tait_visc = SPH_VISC_MONAGHAN;
-  int nlocal = 0, nghost = 0;
-  int list_kind = -1, inum = 0;
-  DBuf<double4> xf, vr, fo;
-  DBuf<double> en, de, rho_out, virial;
-  DBuf<int> ty, ilist, off, nbr;
-  std::vector<double4> h4;
-  std::vector<double> h1;
-  std::vector<int> hoff, hnbr, hilist;
-  bool coef_dirty = true;
-
-  void upload_coefs() {
-    if (!coef_dirty) return;
-    SPH_HIP_TRY(hipMemcpyAsync(dc, &hc, sizeof(Coefs), hipMemcpyHostToDevice, stream));
-    coef_dirty = false;
-  }
-};
 
 extern "C" {
 
@@ -118,6 +95,10 @@ int sph_hip_destroy(sph_hip_ctx *c) {
   c->ilist.release();
   c->off.release();
   c->nbr.release();
+  c->rm.release();
+  c->cv.release();
+  c->cg.release();
+  if (c->dm) (void)hipFree(c->dm);
   if (c->dc) (void)hipFree(c->dc);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -171,6 +152,7 @@ int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const
   const size_t nall = (size_t)nlocal + nghost;
   c->nlocal = nlocal;
   c->nghost = nghost;
+  c->have_mp_atoms = false;  // rmass/cv must be restaged for the new atom set
   if (nall == 0) return SPH_HIP_OK;
   for (size_t i = 0; i < nall; i++)
     SPH_REQUIRE(type[i] >= 1 && type[i] <= c->ntypes, SPH_HIP_EINVAL,

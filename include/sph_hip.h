@@ -148,6 +148,37 @@ int sph_hip_colorgradient_coeff(sph_hip_ctx *ctx, const double *alpha, const dou
 int sph_hip_colorgradient(sph_hip_ctx *ctx, double *cg);
 
 /* ======================================================================================
+ * 1c. fix phase_change (FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-352)
+ * ==================================================================================== */
+typedef struct {
+  double Tc, Tt, Hwv, dr, to_mass, cutoff;   /* required args (fix_phase_change.cpp:58-67) */
+  int from_type, to_type;
+  int energy_chance;                          /* 1: "ENERGY rate" form (:70-73) */
+  double change_chance, rate;                 /* prob, or rate of the ENERGY form */
+  double dt;                                  /* update->dt */
+  int maxattempt;                             /* option "attempt" (default 10) */
+  double sublo[3], subhi[3], boxhi[3];        /* domain->sublo/subhi/boxhi */
+  int top[3];                                 /* comm->myloc[d] == comm->procgrid[d]-1 */
+} sph_phasechange_params;
+
+/* One pre_exchange on this rank.  Uses the staged atoms (sph_hip_atoms: x, vest, rho, e,
+   type; sph_hip_atoms_multiphase: rmass, cv) and the fix's FULL list (sph_hip_list /
+   sph_hip_list_csr with SPH_LIST_FULL).  v and cg (atom->v, atom->colorgradient) are nall*3.
+   The Park-Miller stream (*seed, RanPark) is consumed in the reference's order, so the
+   same seed gives the same insertions.  e[0..nlocal) is updated for atoms that changed
+   phase; dmass[0..nall) receives the mass taken from from_type atoms (reverse-communicate
+   the ghost part, then call sph_hip_phasechange_finish).  Up to cap new atoms are written
+   as 13-double records {x[3], v[3], vest[3], e, rmass, rho, cv}, their parent atom index in
+   parent[]; *nins = number inserted (may exceed cap: then call again with more room, the
+   seed must be restored by the caller).  The caller creates them (avec->create_atom,
+   type to_type) and updates natoms/tags as the reference does (:336-351). */
+int sph_hip_phasechange(sph_hip_ctx *ctx, const sph_phasechange_params *p, int *seed,
+                        const double *v, const double *cg, double *e, double *dmass, int cap,
+                        int *nins, double *new_atoms, int *parent);
+/* rmass[i] -= dmass[i]; e[i] *= mold / rmass[i] for i < nlocal (:327-334).  Host only. */
+int sph_hip_phasechange_finish(int nlocal, const double *dmass, double *rmass, double *e);
+
+/* ======================================================================================
  * 2. Device-resident engine
  * ==================================================================================== */
 #define SPH_MAXTYPES 8

@@ -102,6 +102,9 @@ EXPORTS = {
     "sph_hip_heatconduction_phasechange": (_i, [_vp, _dp]),
     "sph_hip_colorgradient_coeff": (_i, [_vp, _dp, _dp]),
     "sph_hip_colorgradient": (_i, [_vp, _dp]),
+    "sph_hip_phasechange": (_i, [_vp, _vp, C.POINTER(_i), _dp, _dp, _dp, _dp, _i,
+                                 C.POINTER(_i), _vp, _vp]),
+    "sph_hip_phasechange_finish": (_i, [_i, _dp, _dp, _dp]),
     "sph_engine_create": (_i, [_i, C.POINTER(EngineConfig), C.POINTER(_vp)]),
     "sph_engine_destroy": (_i, [_vp]),
     "sph_engine_comm_uid": (_i, [_vp]),
@@ -145,6 +148,16 @@ def device_count() -> int:
 
 def _ptr(a):
     return None if a is None else a.ctypes.data
+
+
+class PhaseChangeParams(C.Structure):
+    """sph_phasechange_params (include/sph_hip.h section 1c)."""
+    _fields_ = [("Tc", C.c_double), ("Tt", C.c_double), ("Hwv", C.c_double),
+                ("dr", C.c_double), ("to_mass", C.c_double), ("cutoff", C.c_double),
+                ("from_type", C.c_int), ("to_type", C.c_int), ("energy_chance", C.c_int),
+                ("change_chance", C.c_double), ("rate", C.c_double), ("dt", C.c_double),
+                ("maxattempt", C.c_int), ("sublo", C.c_double * 3),
+                ("subhi", C.c_double * 3), ("boxhi", C.c_double * 3), ("top", C.c_int * 3)]
 
 
 # ------------------------------------------------------------------------------------------
@@ -256,6 +269,23 @@ class PairContext:
 
     def colorgradient_coeff(self, alpha, cut):
         _chk(self.L.sph_hip_colorgradient_coeff(self.h, self._t(alpha), self._t(cut)))
+
+    def phasechange(self, params, seed, v, cg, e, cap=None):
+        """One FixPhaseChange::pre_exchange.  Returns (seed, nins, new_atoms (nins, 13),
+        parent, dmass); e is updated in place."""
+        nall = self.nlocal + self.nghost
+        cap = nall if cap is None else cap
+        sd = _i(int(seed))
+        nins = _i(0)
+        dmass = np.zeros(nall)
+        rec = np.zeros((max(cap, 1), 13))
+        par = np.zeros(max(cap, 1), dtype=np.int32)
+        _chk(self.L.sph_hip_phasechange(self.h, C.byref(params), C.byref(sd),
+                                        np.ascontiguousarray(v, dtype=np.float64),
+                                        np.ascontiguousarray(cg, dtype=np.float64), e, dmass,
+                                        cap, C.byref(nins), rec.ctypes.data, par.ctypes.data))
+        n = nins.value
+        return sd.value, n, rec[:min(n, cap)].copy(), par[:min(n, cap)].copy(), dmass
 
     def colorgradient(self, cg):
         _chk(self.L.sph_hip_colorgradient(self.h, cg))

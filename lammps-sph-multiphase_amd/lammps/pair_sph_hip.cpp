@@ -1,0 +1,198 @@
+/* ----------------------------------------------------------------------------------------
+   LAMMPS-side binding of the MI355X USER-SPH engine: compute() of the sph/<style>/hip pair styles.
+   Each compute() stages the rank's atoms and the style's NeighList into the device
+   context and calls the style's C-ABI entry point (include/sph_hip.h); the loops it
+   replaces are cited per class.  Everything else (settings, coeff, init_one, comm) is the
+   reference style's own code, inherited.
+------------------------------------------------------------------------------------------ */
+#include "pair_sph_hip.h"
+
+#include <cstdio>
+#include <vector>
+
+#include "atom.h"
+#include "comm.h"
+#include "domain.h"
+#include "error.h"
+#include "force.h"
+#include "memory.h"
+#include "neigh_list.h"
+#include "sph_hip.h"
+#include "update.h"
+
+using namespace LAMMPS_NS;
+
+namespace {
+sph_hip_ctx *g_ctx = NULL;
+}
+
+sph_hip_ctx *LAMMPS_NS::sph_hip_rank_ctx(LAMMPS *lmp) {
+  if (!g_ctx) {
+    const int ndev = sph_hip_device_count();
+    if (ndev < 1) lmp->error->one(FLERR, "sph/<style>/hip styles need a HIP device");
+    sph_hip_check(lmp,
+                  sph_hip_create(lmp->comm->me % ndev, lmp->domain->dimension,
+                                 lmp->atom->ntypes, lmp->force->newton_pair, &g_ctx),
+                  "sph_hip_create");
+  }
+  return g_ctx;
+}
+
+void LAMMPS_NS::sph_hip_check(LAMMPS *lmp, int rc, const char *where) {
+  if (rc == SPH_HIP_OK) return;
+  char msg[1200];
+  snprintf(msg, sizeof(msg), "%s failed (%d): %s", where, rc, sph_hip_last_error());
+  lmp->error->one(FLERR, msg);
+}
+
+void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, int kind,
+                              bool multiphase) {
+  Atom *atom = lmp->atom;
+  const int nlocal = atom->nlocal, nghost = atom->nghost;
+  const int nall = nlocal + nghost;
+  // x and vest are memory->create 2-D arrays: contiguous nmax*3 backing (memory.h:124-137)
+  sph_hip_check(lmp,
+                sph_hip_atoms(ctx, nlocal, nghost, nall ? &atom->x[0][0] : NULL,
+                              (nall && atom->vest) ? &atom->vest[0][0] : NULL, atom->rho,
+                              atom->e, atom->type),
+                "sph_hip_atoms");
+  if (multiphase)
+    sph_hip_check(lmp, sph_hip_atoms_multiphase(ctx, atom->rmass, atom->cv),
+                  "sph_hip_atoms_multiphase");
+  sph_hip_check(lmp,
+                sph_hip_list(ctx, kind, list->inum, list->ilist, list->numneigh,
+                             list->firstneigh),
+                "sph_hip_list");
+}
+
+namespace {
+
+// (nt+1)^2 row-major view of a memory->create 2-D table (contiguous backing)
+const double *tab(double **t) { return &t[0][0]; }
+
+double *virial_target(LAMMPS *lmp, Pair *p) {
+  if (p->vflag_atom) lmp->error->all(FLERR, "sph/<style>/hip styles do not tally per-atom virials");
+  return (p->evflag && p->vflag_global) ? p->virial : NULL;
+}
+
+}  // namespace
+
+/* pair_sph_rhosum.cpp:66-204 */
+void PairSPHRhoSumHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  if (nstep != 0 && (update->ntimestep % nstep) == 0) {
+    sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+    sph_hip_check(lmp, sph_hip_rhosum_coeff(ctx, tab(cut), atom->mass), "sph_hip_rhosum_coeff");
+    sph_hip_stage(lmp, ctx, list, SPH_LIST_FULL, false);
+    sph_hip_check(lmp, sph_hip_rhosum(ctx, atom->rho), "sph_hip_rhosum");
+  }
+  comm->forward_comm_pair(this);
+}
+
+/* pair_sph_taitwater.cpp:53-200 */
+void PairSPHTaitwaterHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp,
+                sph_hip_taitwater_coeff(ctx, SPH_VISC_MONAGHAN, rho0, soundspeed, B,
+                                        tab(viscosity), tab(cut), atom->mass),
+                "sph_hip_taitwater_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, false);
+  if (atom->nlocal + atom->nghost)
+    sph_hip_check(lmp,
+                  sph_hip_taitwater(ctx, &atom->f[0][0], atom->drho, atom->de,
+                                    virial_target(lmp, this)),
+                  "sph_hip_taitwater");
+  if (vflag_fdotr) virial_fdotr_compute();
+}
+
+/* pair_sph_taitwater_morris.cpp:52-200 */
+void PairSPHTaitwaterMorrisHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp,
+                sph_hip_taitwater_coeff(ctx, SPH_VISC_MORRIS, rho0, soundspeed, B,
+                                        tab(viscosity), tab(cut), atom->mass),
+                "sph_hip_taitwater_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, false);
+  if (atom->nlocal + atom->nghost)
+    sph_hip_check(lmp,
+                  sph_hip_taitwater(ctx, &atom->f[0][0], atom->drho, atom->de,
+                                    virial_target(lmp, this)),
+                  "sph_hip_taitwater");
+  if (vflag_fdotr) virial_fdotr_compute();
+}
+
+/* pair_sph_heatconduction.cpp:47-134 */
+void PairSPHHeatConductionHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp, sph_hip_heatconduction_coeff(ctx, tab(alpha), tab(cut), atom->mass),
+                "sph_hip_heatconduction_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, false);
+  sph_hip_check(lmp, sph_hip_heatconduction(ctx, atom->de), "sph_hip_heatconduction");
+}
+
+/* pair_sph_rhosum_multiphase.cpp:68-174 */
+void PairSPHRhoSumMultiphaseHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  if (nstep != 0 && (update->ntimestep % nstep) == 0) {
+    sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+    sph_hip_check(lmp, sph_hip_rhosum_multiphase_coeff(ctx, tab(cut)),
+                  "sph_hip_rhosum_multiphase_coeff");
+    sph_hip_stage(lmp, ctx, list, SPH_LIST_FULL, true);
+    sph_hip_check(lmp, sph_hip_rhosum_multiphase(ctx, atom->rho), "sph_hip_rhosum_multiphase");
+  }
+  comm->forward_comm_pair(this);
+}
+
+/* pair_sph_taitwater_multiphase.cpp:55-186 */
+void PairSPHTaitwaterMultiphaseHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp,
+                sph_hip_taitwater_multiphase_coeff(ctx, rho0, soundspeed, gamma, rbackground,
+                                                   tab(viscosity), tab(cut)),
+                "sph_hip_taitwater_multiphase_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, true);
+  if (atom->nlocal + atom->nghost)
+    sph_hip_check(lmp, sph_hip_taitwater_multiphase(ctx, &atom->f[0][0]),
+                  "sph_hip_taitwater_multiphase");
+  if (vflag_fdotr) virial_fdotr_compute();
+}
+
+/* pair_sph_heatconduction_phasechange.cpp:52-141 */
+void PairSPHHeatConductionPhaseChangeHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp,
+                sph_hip_heatconduction_phasechange_coeff(ctx, tab(alpha), &fixflag[0][0],
+                                                         tab(tc), tab(cut)),
+                "sph_hip_heatconduction_phasechange_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, true);
+  sph_hip_check(lmp, sph_hip_heatconduction_phasechange(ctx, atom->de),
+                "sph_hip_heatconduction_phasechange");
+}
+
+/* pair_sph_colorgradient.cpp:70-191 */
+void PairSPHColorGradientHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  if (nstep != 0 && (update->ntimestep % nstep) == 0) {
+    sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+    sph_hip_check(lmp, sph_hip_colorgradient_coeff(ctx, tab(alpha), tab(cut)),
+                  "sph_hip_colorgradient_coeff");
+    sph_hip_stage(lmp, ctx, list, SPH_LIST_FULL, true);
+    if (atom->nlocal)
+      sph_hip_check(lmp, sph_hip_colorgradient(ctx, &atom->colorgradient[0][0]),
+                    "sph_hip_colorgradient");
+  }
+  comm->forward_comm_pair(this);
+}

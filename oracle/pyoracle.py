@@ -37,6 +37,32 @@ class OrcDomain(C.Structure):
                 ("periodic", C.c_int * 3)]
 
 
+class PcParams(C.Structure):
+    """orc_pc_params (sph_oracle.h): fix phase_change arguments."""
+    _fields_ = [("dim", C.c_int), ("Tc", C.c_double), ("Tt", C.c_double), ("Hwv", C.c_double),
+                ("dr", C.c_double), ("to_mass", C.c_double), ("cutoff", C.c_double),
+                ("from_type", C.c_int), ("to_type", C.c_int), ("energy_chance", C.c_int),
+                ("change_chance", C.c_double), ("rate", C.c_double), ("dt", C.c_double),
+                ("maxattempt", C.c_int), ("sublo", C.c_double * 3),
+                ("subhi", C.c_double * 3), ("boxhi", C.c_double * 3), ("top", C.c_int * 3)]
+
+
+def phasechange(p: "PcParams", seed, nlocal, x, v, vest, cg, e, rmass, rho, cv, type_, off,
+                neigh, cap=None):
+    """FixPhaseChange::pre_exchange (oracle).  e is updated in place.  Returns
+    (seed, nins, new_atoms (nins, 13), parent, dmass)."""
+    nall = x.shape[0]
+    cap = nall if cap is None else cap
+    sd = C.c_int(int(seed))
+    dmass = np.zeros(nall)
+    rec = np.zeros((max(cap, 1), 13))
+    par = np.zeros(max(cap, 1), dtype=np.int32)
+    n = lib().orc_phasechange(C.byref(p), C.byref(sd), nlocal, nall, x, v, vest, cg, e, rmass,
+                              rho, cv, type_, off, _nz(neigh), dmass, cap, rec.ctypes.data,
+                              par.ctypes.data)
+    return sd.value, n, rec[:min(n, cap)].copy(), par[:min(n, cap)].copy(), dmass
+
+
 def build_oracle() -> str:
     src = os.path.join(HERE, "sph_oracle.c")
     if (not os.path.exists(ORACLE_SO)) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
@@ -84,6 +110,13 @@ def lib():
                                                      _dp, _dp, _lp, _ip, _dp]
         L.orc_colorgradient.argtypes = [_i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp, _lp,
                                         _ip, _dp]
+        L.orc_park_uniform.argtypes = [C.POINTER(_i)]
+        L.orc_park_uniform.restype = _d
+        L.orc_phasechange.argtypes = [C.POINTER(PcParams), C.POINTER(_i), _i, _i, _dp, _dp,
+                                      _dp, _dp, _dp, _dp, _dp, _dp, _ip, _lp, _ip, _dp, _i,
+                                      C.c_void_p, C.c_void_p]
+        L.orc_phasechange.restype = _i
+        L.orc_phasechange_finish.argtypes = [_i, _dp, _dp, _dp]
         L.orc_meso_setup.argtypes = [_i, _dp, _dp]
         L.orc_meso_initial.argtypes = [_i, _d, _d, _ip, _dp, C.c_void_p, _dp, _dp, _dp, _dp,
                                        _dp, _dp, _dp, _dp]

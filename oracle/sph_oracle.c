@@ -769,3 +769,201 @@ void orc_meso_final(int nlocal, double dtf, const int *type, const double *mass,
     rho[i] += dtf * drho[i];
   }
 }
+
+/* ------------------------------------------------------------------------------------
+   FixPhaseChange, src/USER-SPH/fix_phase_change.cpp
+   ------------------------------------------------------------------------------------ */
+/* RanPark::uniform, src/random_park.cpp:42-49 */
+double orc_park_uniform(int *seed) {
+  const int IA = 16807, IM = 2147483647, IQ = 127773, IR = 2836;
+  const double AM = 1.0 / IM;
+  int k = *seed / IQ;
+  *seed = IA * (*seed - k * IQ) - IR * k;
+  if (*seed < 0) *seed += IM;
+  return AM * *seed;
+}
+
+/* isfromphasearound, fix_phase_change.cpp:538-563 */
+static int pc_around(const orc_pc_params *p, int i, const double *x, const int *type,
+                     const long *off, const int *neigh) {
+  const double cutoff2 = p->cutoff * p->cutoff;
+  for (long jj = off[i]; jj < off[i + 1]; jj++) {
+    const int j = neigh[jj];
+    if (type[j] == p->from_type) {
+      const double delx = x[3 * i] - x[3 * j];
+      const double dely = x[3 * i + 1] - x[3 * j + 1];
+      const double delz = x[3 * i + 2] - x[3 * j + 2];
+      const double rsq = delx * delx + dely * dely + delz * delz;
+      if (rsq <= cutoff2) return 1;
+    }
+  }
+  return 0;
+}
+
+/* insert_one_atom's ownership test, fix_phase_change.cpp:425-456 (orthogonal box) */
+static int pc_mine(const orc_pc_params *p, const double *c) {
+  if (c[0] >= p->sublo[0] && c[0] < p->subhi[0] && c[1] >= p->sublo[1] &&
+      c[1] < p->subhi[1] && c[2] >= p->sublo[2] && c[2] < p->subhi[2])
+    return 1;
+  if (p->dim == 3 && c[2] >= p->boxhi[2] && p->top[2] && c[0] >= p->sublo[0] &&
+      c[0] < p->subhi[0] && c[1] >= p->sublo[1] && c[1] < p->subhi[1])
+    return 1;
+  if (p->dim == 2 && c[1] >= p->boxhi[1] && p->top[1] && c[0] >= p->sublo[0] &&
+      c[0] < p->subhi[0])
+    return 1;
+  return 0;
+}
+
+/* create_newpos_simple / create_newpos, fix_phase_change.cpp:466-520 */
+static void pc_newpos_simple(int *seed, const double *xone, double delta, double *coord) {
+  coord[0] = xone[0] + (orc_park_uniform(seed) - 0.5) * delta;
+  coord[1] = xone[1] + (orc_park_uniform(seed) - 0.5) * delta;
+  coord[2] = xone[2] + (orc_park_uniform(seed) - 0.5) * delta;
+}
+
+static void pc_newpos(int dim, int *seed, const double *xone, const double *cg, double delta,
+                      double *coord) {
+  const double CG_SMALL = 1.0e-20;
+  double eij[3];
+  if (dim == 3) {
+    double b1[3] = {-cg[1], cg[0], 0};
+    const double b1abs = sqrt(b1[0] * b1[0] + b1[1] * b1[1] + b1[2] * b1[2]);
+    if (b1abs > CG_SMALL) {
+      b1[0] = b1[0] / b1abs;
+      b1[1] = b1[1] / b1abs;
+      b1[2] = b1[2] / b1abs;
+    }
+    double b2[3];
+    b2[0] = -cg[0] * cg[1] * cg[2] / (pow(cg[1], 2) + pow(cg[0], 2));
+    b2[1] = -cg[2] * pow(cg[1], 2) / (pow(cg[1], 2) + pow(cg[0], 2));
+    b2[2] = cg[1];
+    const double b2abs = sqrt(b2[0] * b2[0] + b2[1] * b2[1] + b2[2] * b2[2]);
+    if (b1abs > CG_SMALL) { /* the reference tests b1abs here (:494) */
+      b2[0] = b2[0] / b2abs;
+      b2[1] = b2[1] / b2abs;
+      b2[2] = b2[2] / b2abs;
+    }
+    const double atmp = orc_park_uniform(seed) - 0.5;
+    const double btmp = orc_park_uniform(seed) - 0.5;
+    eij[0] = atmp * b1[0] + btmp * b2[0];
+    eij[1] = atmp * b1[1] + btmp * b2[1];
+    eij[2] = atmp * b1[2] + btmp * b2[2];
+  } else {
+    double atmp = orc_park_uniform(seed);
+    if (atmp > 0.5) atmp = 1;
+    else atmp = -1;
+    eij[0] = -atmp * cg[1];
+    eij[1] = atmp * cg[0];
+    eij[2] = 0.0;
+  }
+  const double eijabs = sqrt(eij[0] * eij[0] + eij[1] * eij[1] + eij[2] * eij[2]);
+  coord[0] = xone[0] + eij[0] * delta / eijabs;
+  coord[1] = xone[1] + eij[1] * delta / eijabs;
+  coord[2] = xone[2] + eij[2] * delta / eijabs;
+}
+
+/* FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-321 (up to reverse comm) */
+int orc_phasechange(const orc_pc_params *p, int *seed, int nlocal, int nall, const double *x,
+                    const double *v, const double *vest, const double *cg, double *e,
+                    const double *rmass, const double *rho, const double *cv,
+                    const int *type, const long *off, const int *neigh, double *dmass,
+                    int cap, double *new_atoms, int *parent) {
+  int nins = 0;
+  for (int i = 0; i < nall; i++) dmass[i] = 0.0;
+  for (int i = 0; i < nlocal; i++) {
+    const double Ti = e[i] / cv[i];
+    int isphasechange;
+    if ((Ti < p->Tc) || (type[i] != p->to_type)) {
+      isphasechange = 0;
+    } else if (p->energy_chance) {
+      const double threshold = (e[i] - p->Tc * cv[i]) / p->Hwv * p->dt * p->rate;
+      isphasechange = (orc_park_uniform(seed) < threshold) && pc_around(p, i, x, type, off, neigh);
+    } else {
+      isphasechange = (orc_park_uniform(seed) < p->change_chance) && (Ti > p->Tt) &&
+                      pc_around(p, i, x, type, off, neigh);
+    }
+    if (!isphasechange) continue;
+    double coord[3];
+    int ok = 0, natempt = 0;
+    double delta = p->dr;
+    do {
+      pc_newpos(p->dim, seed, x + 3 * i, cg + 3 * i, delta, coord);
+      ok = pc_mine(p, coord);
+      delta = 0.75 * delta;
+      natempt++;
+    } while (!ok && natempt < p->maxattempt);
+    if (!ok) {
+      delta = p->dr;
+      natempt = 0;
+      do {
+        pc_newpos_simple(seed, x + 3 * i, delta, coord);
+        ok = pc_mine(p, coord);
+        delta = 0.75 * delta;
+        natempt++;
+      } while (!ok && natempt < p->maxattempt);
+    }
+    if (!ok) continue;
+    /* weights over from_type neighbours heavier than half a new particle (:236-256) */
+    double wtotal = 0.0;
+    for (long jj = off[i]; jj < off[i + 1]; jj++) {
+      const int j = neigh[jj];
+      if (type[j] == p->from_type && rmass[j] > 0.5 * p->to_mass) {
+        const double delx = x[3 * i] - x[3 * j];
+        const double dely = x[3 * i + 1] - x[3 * j + 1];
+        const double delz = x[3 * i + 2] - x[3 * j + 2];
+        const double rsq = delx * delx + dely * dely + delz * delz;
+        wtotal += (p->dim == 3) ? orc_kernel_quintic3d(sqrt(rsq) * p->cutoff)
+                                : orc_kernel_quintic2d(sqrt(rsq) * p->cutoff);
+      }
+    }
+    double dmom[3] = {0, 0, 0}, dmomest[3] = {0, 0, 0};
+    for (long jj = off[i]; jj < off[i + 1]; jj++) {
+      const int j = neigh[jj];
+      if (type[j] == p->from_type && rmass[j] > 0.5 * p->to_mass) {
+        const double delx = x[3 * i] - x[3 * j];
+        const double dely = x[3 * i + 1] - x[3 * j + 1];
+        const double delz = x[3 * i + 2] - x[3 * j + 2];
+        const double rsq = delx * delx + dely * dely + delz * delz;
+        const double wfd = (p->dim == 3) ? orc_kernel_quintic3d(sqrt(rsq) * p->cutoff)
+                                         : orc_kernel_quintic2d(sqrt(rsq) * p->cutoff);
+        const double dmass_aux = p->to_mass * wfd / wtotal;
+        dmass[j] += dmass_aux;
+        dmom[0] += v[3 * j] * dmass_aux;
+        dmom[1] += v[3 * j + 1] * dmass_aux;
+        dmom[2] += v[3 * j + 2] * dmass_aux;
+        dmomest[0] += vest[3 * j] * dmass_aux;
+        dmomest[1] += vest[3 * j + 1] * dmass_aux;
+        dmomest[2] += vest[3 * j + 2] * dmass_aux;
+      }
+    }
+    const double energy_aux = 0.5 * (e[i] - p->Hwv);
+    if (nins < cap) {
+      double *r = new_atoms + 13 * (size_t)nins;
+      r[0] = coord[0];
+      r[1] = coord[1];
+      r[2] = coord[2];
+      r[3] = dmom[0] / p->to_mass;
+      r[4] = dmom[1] / p->to_mass;
+      r[5] = dmom[2] / p->to_mass;
+      r[6] = dmomest[0] / p->to_mass;
+      r[7] = dmomest[1] / p->to_mass;
+      r[8] = dmomest[2] / p->to_mass;
+      r[9] = energy_aux;
+      r[10] = p->to_mass;
+      r[11] = rho[i];
+      r[12] = cv[i];
+      parent[nins] = i;
+    }
+    e[i] = energy_aux;
+    nins++;
+  }
+  return nins;
+}
+
+void orc_phasechange_finish(int nlocal, const double *dmass, double *rmass, double *e) {
+  for (int i = 0; i < nlocal; i++) {
+    const double mold = rmass[i];
+    rmass[i] -= dmass[i];
+    e[i] = e[i] * mold / rmass[i];
+  }
+}

@@ -148,6 +148,35 @@ void orc_meso_final(int nlocal, double dtf, const int *type, const double *mass,
                     const double *rmass, double *v, const double *f, double *rho,
                     const double *drho, double *e, const double *de);
 
+/* ---- fix phase_change (FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-352) ---- */
+typedef struct {
+  int dim;
+  double Tc, Tt, Hwv, dr, to_mass, cutoff;   /* required args, fix_phase_change.cpp:58-67 */
+  int from_type, to_type;
+  int energy_chance;                          /* "ENERGY rate" form (:70-73) */
+  double change_chance, rate, dt;             /* dt = update->dt */
+  int maxattempt;                             /* option "attempt", default 10 (:364) */
+  double sublo[3], subhi[3], boxhi[3];
+  int top[3];                                 /* comm->myloc[d] == procgrid[d]-1 */
+} orc_pc_params;
+
+/* RanPark::uniform, src/random_park.cpp:42-49 (seed updated in place) */
+double orc_park_uniform(int *seed);
+
+/* One pre_exchange call on one rank.  Arrays hold nall = nlocal + nghost atoms (x, v,
+   vest, cg: 3 per atom); the list is the fix's FULL list (rows 0..nlocal).  e is updated
+   in place for the atoms that change phase; dmass[0..nall) receives the mass taken from
+   from_type atoms (ghost entries still to be reverse-communicated).  New atoms (at most
+   cap) are written as records of 13 doubles {x[3], v[3], vest[3], e, rmass, rho, cv} with
+   the index of the parent atom in parent[].  Returns the number inserted. */
+int orc_phasechange(const orc_pc_params *p, int *seed, int nlocal, int nall, const double *x,
+                    const double *v, const double *vest, const double *cg, double *e,
+                    const double *rmass, const double *rho, const double *cv,
+                    const int *type, const long *off, const int *neigh, double *dmass,
+                    int cap, double *new_atoms, int *parent);
+/* after reverse comm of dmass: rmass -= dmass, e renormalised (fix_phase_change.cpp:327-334) */
+void orc_phasechange_finish(int nlocal, const double *dmass, double *rmass, double *e);
+
 #ifdef __cplusplus
 }
 #endif

@@ -216,7 +216,7 @@ def main():
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
                    "parallelism": f"{world} independent 1M boxes (one per GPU)",
                    "kernel_path": "lds-staged bins" if st["staged"] else "csr rows"},
-        "roofline": {"bound": "hbm", "kernel": ("k_bin_force" if st["staged"] else "k_force")
+        "roofline": {"bound": "hbm", "kernel": ("k_bin_force" if st["staged"] else "k_row_force")
                      + "<TAIT> (sph/taitwater pass)",
                      "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,
@@ -231,6 +231,17 @@ def main():
                     "integrate_ms_per_step": st["ms_integrate"] / args.steps,
                     "comm_ms_per_step": st["ms_comm"] / args.steps},
     }
+    # HBM traffic per launch of the roofline kernel from PMC counters (tools/pmc_traffic.sh
+    # on this same command; FETCH_SIZE x2 + WRITE_SIZE), if a summary for it is committed
+    tj = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if os.path.exists(tj):
+        kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]
+        for k, v in json.load(open(tj)).items():
+            if k.split("<")[0].split("::")[-1] == kname and v.get("traffic_bytes"):
+                out["roofline"]["traffic"] = v["traffic_bytes"] / 1e9
+                out["roofline"]["traffic_unit"] = "GB per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE)"
+                out["roofline"]["algorithmic_GB_per_launch"] = bytes_tait * nloc / 1e9
+                break
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n)
     if rank == 0:

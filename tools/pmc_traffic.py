@@ -1,0 +1,44 @@
+"""Per-launch HBM traffic of each kernel family from two rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE; both in KB).  gfx950 correction (MI355X_MICROARCH.md, HBM):
+FETCH_SIZE reports half the bytes of wide reads, so traffic = 2*FETCH + WRITE."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def family(name):
+    for k in ("k_row_force", "k_row_rhosum", "k_bin_force", "k_bin_rhosum", "k_force",
+              "k_rhosum", "k_neigh2", "k_neigh"):
+        if k in name:
+            return name.split("(")[0]
+    return None
+
+
+def load(path, counter):
+    agg = collections.defaultdict(list)
+    for f in glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = family(r["Kernel_Name"])
+            if k:
+                agg[k].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main(root):
+    fetch, nf = load(f"{root}/fetch", "FETCH_SIZE")
+    write, nw = load(f"{root}/write", "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k)
+        w = write.get(k)
+        out[k] = {"fetch_bytes": f, "write_bytes": w, "launches": [nf.get(k, 0), nw.get(k, 0)],
+                  "traffic_bytes": (2.0 * f + w) if (f is not None and w is not None) else None}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -210,7 +210,9 @@ typedef struct {
   double heat_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
   /* body force per unit mass (fix gravity style), added in post_force: f += m*g */
   double gravity[3];
-  /* brick decomposition (procgrid[0]*procgrid[1]*procgrid[2] ranks; 1 1 1 = serial) */
+  /* brick decomposition (procgrid[0]*procgrid[1]*procgrid[2] bricks, uniform split; 1 1 1 or
+     0 0 0 = one brick).  Bricks are numbered x fastest; each must be wider than the ghost
+     cutoff (CommBrick maxneed = 1). */
   int procgrid[3];
   int rank;                    /* my rank in the brick, x fastest */
   /* spatially sort owned particles at every rebuild (atom->sort analogue) */
@@ -237,10 +239,21 @@ typedef struct sph_engine sph_engine;
 int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out);
 int sph_engine_destroy(sph_engine *e);
 
-/* RCCL communicator for procgrid runs: uid = ncclUniqueId bytes (128) produced by
-   sph_engine_comm_uid on rank 0 and distributed by the caller (MPI_Bcast / torch). */
+/* Brick decomposition (cfg.procgrid, cfg.rank; CommBrick's swaps, comm_brick.cpp).  Every
+   brick needs a communicator before sph_engine_setup:
+   * RCCL, one process per GPU: uid = ncclUniqueId bytes (128) produced by
+     sph_engine_comm_uid on rank 0 and distributed by the caller (MPI_Bcast / torch);
+   * a local world: several bricks in one process (one host thread per brick, any devices),
+     halo exchange by device copies -- for tests and bricks that share a GPU.
+   Owned atoms migrate between bricks at rebuilds; sph_engine_get_atoms then returns them in
+   local order with their tags (sph_engine_set_tags sets global tags; default = index). */
 int sph_engine_comm_uid(void *uid128);
 int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank);
+typedef struct sph_local_world sph_local_world;
+int sph_local_world_create(int nranks, sph_local_world **out);
+int sph_local_world_destroy(sph_local_world *w);
+int sph_engine_comm_local(sph_engine *e, sph_local_world *w, int rank);
+int sph_engine_set_tags(sph_engine *e, const int *tags);
 
 /* Owned particles of this rank (tag order is the caller's order; results are returned in
    the same order).  v is the velocity; vest is set from v at setup (FixMeso::setup_pre_force). */

@@ -109,6 +109,10 @@ EXPORTS = {
     "sph_engine_destroy": (_i, [_vp]),
     "sph_engine_comm_uid": (_i, [_vp]),
     "sph_engine_comm_init": (_i, [_vp, _vp, _i, _i]),
+    "sph_local_world_create": (_i, [_i, C.POINTER(_vp)]),
+    "sph_local_world_destroy": (_i, [_vp]),
+    "sph_engine_comm_local": (_i, [_vp, _vp, _i]),
+    "sph_engine_set_tags": (_i, [_vp, _ip]),
     "sph_engine_set_atoms": (_i, [_vp, _i, _dp, _dp, _ip, _dp, _vp, _vp]),
     "sph_engine_setup": (_i, [_vp]),
     "sph_engine_run": (_i, [_vp, _i]),
@@ -341,6 +345,28 @@ def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every
     return c
 
 
+def comm_uid() -> bytes:
+    """ncclUniqueId (128 bytes) for sph_engine_comm_init; make it on rank 0, broadcast."""
+    buf = C.create_string_buffer(128)
+    _chk(load().sph_engine_comm_uid(buf))
+    return buf.raw
+
+
+class LocalWorld:
+    """Several bricks in one process (sph_local_world): one host thread per brick."""
+
+    def __init__(self, nranks: int):
+        self.L = load()
+        h = _vp()
+        _chk(self.L.sph_local_world_create(nranks, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.L.sph_local_world_destroy(self.h)
+            self.h = None
+
+
 class Engine:
     def __init__(self, cfg: EngineConfig, device: int = 0):
         self.L = load()
@@ -389,14 +415,28 @@ class Engine:
         return self.L.sph_engine_nlocal(self.h)
 
     def get_atoms(self):
+        """Owned atoms: set_atoms order for a single brick, else local order; "tag" always."""
         n = self.nlocal
         out = {k: np.zeros((n, 3)) for k in ("x", "v", "f")}
         out.update({k: np.zeros(n) for k in ("rho", "e", "drho", "de")})
+        out["tag"] = np.zeros(n, dtype=np.int32)
         _chk(self.L.sph_engine_get_atoms(self.h, out["x"].ctypes.data, out["v"].ctypes.data,
                                          out["rho"].ctypes.data, out["e"].ctypes.data,
                                          out["f"].ctypes.data, out["drho"].ctypes.data,
-                                         out["de"].ctypes.data, None))
+                                         out["de"].ctypes.data, out["tag"].ctypes.data))
         return out
+
+    def set_tags(self, tags):
+        tags = np.ascontiguousarray(tags, dtype=np.int32)
+        _chk(self.L.sph_engine_set_tags(self.h, tags))
+
+    def comm_local(self, world: "LocalWorld", rank: int):
+        _chk(self.L.sph_engine_comm_local(self.h, world.h, rank))
+        self._world = world
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = C.create_string_buffer(bytes(uid), 128)
+        _chk(self.L.sph_engine_comm_init(self.h, buf, nranks, rank))
 
     def neighbor_counts(self):
         c = np.zeros(self.nlocal, dtype=np.int32)

@@ -1,0 +1,355 @@
+// sph_comm.h -- brick decomposition transport and the halo/migration pack kernels.
+//
+// The engine splits the box into procgrid bricks exactly like CommBrick
+// (comm_brick.cpp:150-400 setup, :573-680 exchange, :690-880 borders, :400-560 forward and
+// reverse comm): per dimension two swaps, the first sending atoms within cutghost of the
+// lower face to the lower neighbour (shifted by +prd across the periodic boundary), the
+// second the upper face to the upper neighbour; later dimensions forward earlier ghosts
+// (edges and corners).  A swap whose neighbour is this brick itself (procgrid[d] == 1) is
+// a device copy; a remote one goes through a Transport:
+//   * RcclTransport  -- one process per GPU, ncclSend/ncclRecv pairs on the engine's
+//                       stream (RCCL over xGMI); the production multi-GPU path;
+//   * LocalTransport -- several bricks in one process (threads, one engine each, any GPU),
+//                       device-to-device copies between their buffers; used to test the
+//                       decomposition on a single GPU and for bricks sharing a device.
+// Only the counts of a swap need the host (buffer sizing at borders/exchange time); the
+// per-step forward comm is stream-ordered.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+#include "sph_engine_kernels.h"
+#include "sph_util.h"
+
+namespace sph {
+
+struct Transport {
+  virtual ~Transport() {}
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  // exchange one int with two peers (send to dest, receive from src); host-synchronous
+  virtual int exchange_count(int nsend, int dest, int src, hipStream_t s) = 0;
+  // exchange device buffers (stream-ordered on s)
+  virtual void exchange(const void *sbuf, size_t sbytes, int dest, void *rbuf, size_t rbytes,
+                        int src, hipStream_t s) = 0;
+  virtual void barrier(hipStream_t s) = 0;
+};
+
+#define SPH_NCCL_TRY(call)                                                             \
+  do {                                                                                 \
+    ncclResult_t r_ = (call);                                                          \
+    SPH_REQUIRE(r_ == ncclSuccess, SPH_HIP_ECOMM, "%s: %s", #call, ncclGetErrorString(r_)); \
+  } while (0)
+
+class RcclTransport : public Transport {
+ public:
+  RcclTransport(const ncclUniqueId &id, int nranks, int rank) : n_(nranks), me_(rank) {
+    SPH_NCCL_TRY(ncclCommInitRank(&comm_, nranks, id, rank));
+    SPH_HIP_TRY(hipMalloc(&dcnt_, 2 * sizeof(int)));
+  }
+  ~RcclTransport() override {
+    if (dcnt_) (void)hipFree(dcnt_);
+    if (comm_) (void)ncclCommDestroy(comm_);
+  }
+  int rank() const override { return me_; }
+  int size() const override { return n_; }
+  int exchange_count(int nsend, int dest, int src, hipStream_t s) override {
+    int h[2] = {nsend, 0};
+    SPH_HIP_TRY(hipMemcpyAsync(dcnt_, h, sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_NCCL_TRY(ncclGroupStart());
+    SPH_NCCL_TRY(ncclSend(dcnt_, 1, ncclInt32, dest, comm_, s));
+    SPH_NCCL_TRY(ncclRecv(dcnt_ + 1, 1, ncclInt32, src, comm_, s));
+    SPH_NCCL_TRY(ncclGroupEnd());
+    SPH_HIP_TRY(hipMemcpyAsync(&h[1], dcnt_ + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    return h[1];
+  }
+  void exchange(const void *sbuf, size_t sbytes, int dest, void *rbuf, size_t rbytes, int src,
+                hipStream_t s) override {
+    SPH_NCCL_TRY(ncclGroupStart());
+    if (sbytes) SPH_NCCL_TRY(ncclSend(sbuf, sbytes, ncclUint8, dest, comm_, s));
+    if (rbytes) SPH_NCCL_TRY(ncclRecv(rbuf, rbytes, ncclUint8, src, comm_, s));
+    SPH_NCCL_TRY(ncclGroupEnd());
+  }
+  void barrier(hipStream_t s) override {
+    SPH_NCCL_TRY(ncclAllReduce(dcnt_, dcnt_, 1, ncclInt32, ncclSum, comm_, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+  }
+
+ private:
+  int n_, me_;
+  ncclComm_t comm_ = nullptr;
+  int *dcnt_ = nullptr;
+};
+
+// Bricks of one process: every brick runs in its own host thread; a swap posts its send
+// buffer, meets the others at a barrier, copies its peer's buffer, meets them again.
+struct LocalWorld {
+  explicit LocalWorld(int n) : n(n), post(n) {}
+  struct Post {
+    const void *buf = nullptr;
+    size_t bytes = 0;
+    int dest = -1, count = 0;
+  };
+  int n;
+  std::vector<Post> post;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long generation = 0;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const long g = generation;
+    if (++arrived == n) {
+      arrived = 0;
+      generation++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != g; });
+    }
+  }
+};
+
+class LocalTransport : public Transport {
+ public:
+  LocalTransport(LocalWorld *w, int rank) : w_(w), me_(rank) {}
+  int rank() const override { return me_; }
+  int size() const override { return w_->n; }
+  int exchange_count(int nsend, int dest, int src, hipStream_t s) override {
+    w_->post[me_].count = nsend;
+    w_->post[me_].dest = dest;
+    w_->barrier();
+    SPH_REQUIRE(w_->post[src].dest == me_, SPH_HIP_ECOMM, "local swap mismatch (%d -> %d)", src,
+                me_);
+    const int nrecv = w_->post[src].count;
+    w_->barrier();
+    return nrecv;
+  }
+  void exchange(const void *sbuf, size_t sbytes, int dest, void *rbuf, size_t rbytes, int src,
+                hipStream_t s) override {
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // my send buffer is packed
+    w_->post[me_].buf = sbuf;
+    w_->post[me_].bytes = sbytes;
+    w_->post[me_].dest = dest;
+    w_->barrier();
+    SPH_REQUIRE(w_->post[src].dest == me_ && w_->post[src].bytes == rbytes, SPH_HIP_ECOMM,
+                "local swap mismatch (%d -> %d: %zu vs %zu bytes)", src, me_,
+                w_->post[src].bytes, rbytes);
+    if (rbytes)
+      SPH_HIP_TRY(hipMemcpyAsync(rbuf, w_->post[src].buf, rbytes, hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    w_->barrier();  // the sender may reuse its buffer now
+  }
+  void barrier(hipStream_t s) override {
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    w_->barrier();
+  }
+
+ private:
+  LocalWorld *w_;
+  int me_;
+};
+
+// ---- pack / unpack kernels -------------------------------------------------------------
+// border record (AtomVecMeso::pack_border/unpack_border, atom_vec_meso.cpp:422-600):
+// x (shifted), vest + rho, e, type
+struct BorderRec {
+  double4 x, v;
+  double e;
+  int type, pad;
+};
+
+__device__ __forceinline__ double4 shift_x(double4 x, int dim, double shift) {
+  if (dim == 0) x.x += shift;
+  else if (dim == 1) x.y += shift;
+  else x.z += shift;
+  return x;
+}
+
+static __global__ void k_pack_border(int n, const int *__restrict__ list, int dim, double shift,
+                                     const double4 *__restrict__ xf,
+                                     const double4 *__restrict__ vr,
+                                     const double *__restrict__ en, const int *__restrict__ ty,
+                                     BorderRec *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];
+  BorderRec r;
+  r.x = shift_x(xf[i], dim, shift);
+  r.v = vr[i];
+  r.e = en[i];
+  r.type = ty[i];
+  r.pad = 0;
+  out[k] = r;
+}
+
+static __global__ void k_unpack_border(int n, int first, const BorderRec *__restrict__ in,
+                                       double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                       double *__restrict__ en, int *__restrict__ ty) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const BorderRec r = in[k];
+  xf[first + k] = r.x;
+  vr[first + k] = r.v;
+  en[first + k] = r.e;
+  ty[first + k] = r.type;
+}
+
+// forward comm (AtomVecMeso::pack_comm_vel, atom_vec_meso.cpp:246-360): x (shifted),
+// vest + rho, e as 9 doubles per atom
+static __global__ void k_pack_forward(int n, const int *__restrict__ list, int dim,
+                                      double shift, const double4 *__restrict__ xf,
+                                      const double4 *__restrict__ vr,
+                                      const double *__restrict__ en, double *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];
+  const double4 x = shift_x(xf[i], dim, shift);
+  const double4 v = vr[i];
+  double *o = out + 9 * (size_t)k;
+  o[0] = x.x;
+  o[1] = x.y;
+  o[2] = x.z;
+  o[3] = v.x;
+  o[4] = v.y;
+  o[5] = v.z;
+  o[6] = v.w;
+  o[7] = en[i];
+  o[8] = x.w;
+}
+
+static __global__ void k_unpack_forward(int n, int first, const double *__restrict__ in,
+                                        double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                        double *__restrict__ en) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double *o = in + 9 * (size_t)k;
+  xf[first + k] = make_double4(o[0], o[1], o[2], o[8]);
+  vr[first + k] = make_double4(o[3], o[4], o[5], o[6]);
+  en[first + k] = o[7];
+}
+
+// forward_comm_pair of sph/rhosum (pair_sph_rhosum.cpp:290-313): rho, plus the EOS term
+// P/rho^2 the force pass reads from the same record
+static __global__ void k_pack_rho(int n, const int *__restrict__ list,
+                                  const double4 *__restrict__ xf,
+                                  const double4 *__restrict__ vr, double2 *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];
+  out[k] = make_double2(vr[i].w, xf[i].w);
+}
+
+static __global__ void k_unpack_rho(int n, int first, const double2 *__restrict__ in,
+                                    double4 *__restrict__ xf, double4 *__restrict__ vr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double2 r = in[k];
+  vr[first + k].w = r.x;
+  xf[first + k].w = r.y;
+}
+
+// reverse comm (AtomVecMeso::pack_reverse/unpack_reverse, atom_vec_meso.cpp:387-418):
+// f, drho, de of the swap's ghosts back onto the sender's atoms
+static __global__ void k_pack_reverse(int n, int first, const double4 *__restrict__ fo,
+                                      const double *__restrict__ de, double *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double4 f = fo[first + k];
+  double *o = out + 5 * (size_t)k;
+  o[0] = f.x;
+  o[1] = f.y;
+  o[2] = f.z;
+  o[3] = f.w;
+  o[4] = de[first + k];
+}
+
+static __global__ void k_unpack_reverse(int n, const int *__restrict__ list,
+                                        const double *__restrict__ in,
+                                        double4 *__restrict__ fo, double *__restrict__ de) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];  // distinct within one swap
+  const double *o = in + 5 * (size_t)k;
+  double4 f = fo[i];
+  f.x += o[0];
+  f.y += o[1];
+  f.z += o[2];
+  f.w += o[3];
+  fo[i] = f;
+  de[i] += o[4];
+}
+
+// migration record (AtomVecMeso::pack_exchange, atom_vec_meso.cpp:620-700)
+struct MigRec {
+  double4 x, v, vel;
+  double e;
+  int type, tag;
+};
+
+static __global__ void k_flag_leave(int n, int dim, double lo, double hi,
+                                    const double4 *__restrict__ xf,
+                                    unsigned char *__restrict__ leave,
+                                    unsigned char *__restrict__ stay) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double4 x = xf[i];
+  const double c = dim == 0 ? x.x : (dim == 1 ? x.y : x.z);
+  const bool out = c < lo || c >= hi;  // comm_brick.cpp:601-615
+  leave[i] = out ? 1 : 0;
+  stay[i] = out ? 0 : 1;
+}
+
+static __global__ void k_pack_mig(int n, const int *__restrict__ list,
+                                  const double4 *__restrict__ xf,
+                                  const double4 *__restrict__ vr,
+                                  const double4 *__restrict__ vel,
+                                  const double *__restrict__ en, const int *__restrict__ ty,
+                                  const int *__restrict__ tag, MigRec *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];
+  MigRec r;
+  r.x = xf[i];
+  r.v = vr[i];
+  r.vel = vel[i];
+  r.e = en[i];
+  r.type = ty[i];
+  r.tag = tag[i];
+  out[k] = r;
+}
+
+// keep the received atoms that fall in this brick along dim (comm_brick.cpp:650-672)
+static __global__ void k_flag_mine(int n, int dim, double lo, double hi,
+                                   const MigRec *__restrict__ in,
+                                   unsigned char *__restrict__ flag) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const double4 x = in[k].x;
+  const double c = dim == 0 ? x.x : (dim == 1 ? x.y : x.z);
+  flag[k] = (c >= lo && c < hi) ? 1 : 0;
+}
+
+// gather the listed records (staying atoms or accepted arrivals) into slots first..
+static __global__ void k_gather_mig(int n, const int *__restrict__ list,
+                                    const MigRec *__restrict__ in, int first,
+                                    double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                    double4 *__restrict__ vel, double *__restrict__ en,
+                                    int *__restrict__ ty, int *__restrict__ tag) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const MigRec r = in[list ? list[k] : k];
+  const int d = first + k;
+  xf[d] = r.x;
+  vr[d] = r.v;
+  vel[d] = r.vel;
+  en[d] = r.e;
+  ty[d] = r.type;
+  tag[d] = r.tag;
+}
+
+}  // namespace sph

@@ -11,10 +11,12 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <vector>
 
 #include "sph_coef.h"
+#include "sph_comm.h"
 #include "sph_dispatch.h"
 #include "sph_bin_kernels.h"
 #include "sph_engine_kernels.h"
@@ -70,8 +72,24 @@ struct sph_engine {
   int force_mode = 0;  // M_TAIT | M_HEAT
 
   int nlocal = 0, nghost = 0;
+  // brick decomposition (CommBrick): this brick's grid location, face neighbours, swaps
+  int pg[3] = {1, 1, 1}, myloc[3] = {0, 0, 0}, procneigh[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  int me = 0, nprocs = 1;
+  Transport *tr = nullptr;
+  struct Swap {
+    int dim = 0, dir = 0, sendproc = 0, recvproc = 0, nsend = 0, nrecv = 0, firstrecv = 0;
+    double lo = 0.0, hi = 0.0, shift = 0.0;
+    bool remote = false;
+    DBuf<int> list;
+  };
+  Swap swaps[6];
+  int nswap = 0;
+  DBuf<unsigned char> cbs, cbr, flag2;
+  DBuf<int> sel2;
+  bool multi() const { return pg[0] * pg[1] * pg[2] > 1; }
   int64_t step = 0;
   bool setup_done = false;
+  bool global_tags = false;
   int last_build = 0;
 
   // atoms (owned first, then ghosts): layout of sph_kernels.h
@@ -214,7 +232,7 @@ struct sph_engine {
     SPH_HIP_TRY(hipMemcpyAsync(okey.p, bkey2.p, n * sizeof(unsigned), hipMemcpyDeviceToDevice, s));
   }
 
-  bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2; }
+  bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2 && !multi(); }
 
   // order the ghost segment by bin too (the staged ranges need it contiguous)
   void sort_ghosts() {
@@ -326,7 +344,194 @@ struct sph_engine {
   }
 
   // CommBrick::setup slabs (comm_brick.cpp:330-380) + borders (:696-864) on one process
+
+  // ordered indices i in [0, n) with flag[i] != 0 -> out (returns the count; host sync)
+  int select_flagged(const unsigned char *flag, int n, DBuf<int> &out) {
+    out.reserve(n > 0 ? n : 1);
+    nsel.reserve(1);
+    if (n == 0) return 0;
+    hipcub::CountingInputIterator<int> it(0);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flag, out.p, nsel.p, n, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flag, out.p, nsel.p, n, s));
+    return read_scalar(nsel.p);
+  }
+
+  // move the packed send buffer (cbs, sbytes) of swap-like traffic to cbr (rbytes)
+  void swap_move(bool remote, size_t sbytes, int dest, size_t rbytes, int src) {
+    if (remote) {
+      tr->exchange(cbs.p, sbytes, dest, cbr.p, rbytes, src, s);
+    } else if (rbytes) {
+      SPH_HIP_TRY(hipMemcpyAsync(cbr.p, cbs.p, rbytes, hipMemcpyDeviceToDevice, s));
+    }
+  }
+
+  // CommBrick::borders over a procgrid (comm_brick.cpp:690-880, maxneed = 1)
+  void borders_multi() {
+    nghost = 0;
+    int nall = nlocal;
+    nswap = 0;
+    for (int d = 0; d < cfg.dim; d++) {
+      const int nlast = nall;  // both swaps of a dimension scan owned + earlier ghosts
+      for (int dir = 0; dir < 2; dir++) {
+        Swap &sw = swaps[nswap++];
+        sw.dim = d;
+        sw.dir = dir;
+        sw.sendproc = procneigh[d][dir];
+        sw.recvproc = procneigh[d][1 - dir];
+        sw.remote = pg[d] > 1;
+        bool sendflag = true;  // sendneed/recvneed across a non-periodic boundary (:226-274)
+        if (!box.periodic[d]) sendflag = dir == 0 ? myloc[d] > 0 : myloc[d] < pg[d] - 1;
+        sw.lo = dir == 0 ? -1.0e20 : subhi[d] - cutghost;
+        sw.hi = dir == 0 ? sublo[d] + cutghost : 1.0e20;
+        int pbc = 0;
+        if (dir == 0 && myloc[d] == 0) pbc = 1;
+        if (dir == 1 && myloc[d] == pg[d] - 1) pbc = -1;
+        sw.shift = pbc * box.prd[d];
+        int ns = 0;
+        if (sendflag && nlast > 0) {
+          flags.reserve(nlast);
+          hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d,
+                             sw.lo, sw.hi, xf.p, flags.p);
+          ns = select_flagged(flags.p, nlast, sw.list);
+        }
+        sw.nsend = ns;
+        const int nr = sw.remote ? tr->exchange_count(ns, sw.sendproc, sw.recvproc, s) : ns;
+        sw.nrecv = nr;
+        sw.firstrecv = nall;
+        cbs.reserve((size_t)(ns > 0 ? ns : 1) * sizeof(BorderRec));
+        cbr.reserve((size_t)(nr > 0 ? nr : 1) * sizeof(BorderRec));
+        if (ns)
+          hipLaunchKernelGGL(k_pack_border, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sw.list.p, d,
+                             sw.shift, xf.p, vr.p, en.p, ty.p, (BorderRec *)cbs.p);
+        swap_move(sw.remote, (size_t)ns * sizeof(BorderRec), sw.sendproc,
+                  (size_t)nr * sizeof(BorderRec), sw.recvproc);
+        if (nr) {
+          ensure_atoms((size_t)nall + nr, true);
+          hipLaunchKernelGGL(k_unpack_border, dim3(blocks(nr)), dim3(BLK), 0, s, nr, nall,
+                             (const BorderRec *)cbr.p, xf.p, vr.p, en.p, ty.p);
+        }
+        nall += nr;
+      }
+    }
+    nghost = nall - nlocal;
+  }
+
+  // Comm::forward_comm (x, vest, rho, e) swap by swap
+  void forward_multi() {
+    for (int k = 0; k < nswap; k++) {
+      Swap &sw = swaps[k];
+      cbs.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * 9 * sizeof(double), true, s);
+      cbr.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * 9 * sizeof(double), true, s);
+      if (sw.nsend)
+        hipLaunchKernelGGL(k_pack_forward, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                           sw.list.p, sw.dim, sw.shift, xf.p, vr.p, en.p, (double *)cbs.p);
+      swap_move(sw.remote, (size_t)sw.nsend * 9 * sizeof(double), sw.sendproc,
+                (size_t)sw.nrecv * 9 * sizeof(double), sw.recvproc);
+      if (sw.nrecv)
+        hipLaunchKernelGGL(k_unpack_forward, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
+                           sw.firstrecv, (const double *)cbr.p, xf.p, vr.p, en.p);
+    }
+  }
+
+  // comm->forward_comm_pair of sph/rhosum: rho (+ the EOS term) swap by swap
+  void forward_rho_multi() {
+    for (int k = 0; k < nswap; k++) {
+      Swap &sw = swaps[k];
+      cbs.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * sizeof(double2), true, s);
+      cbr.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * sizeof(double2), true, s);
+      if (sw.nsend)
+        hipLaunchKernelGGL(k_pack_rho, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                           sw.list.p, xf.p, vr.p, (double2 *)cbs.p);
+      swap_move(sw.remote, (size_t)sw.nsend * sizeof(double2), sw.sendproc,
+                (size_t)sw.nrecv * sizeof(double2), sw.recvproc);
+      if (sw.nrecv)
+        hipLaunchKernelGGL(k_unpack_rho, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
+                           sw.firstrecv, (const double2 *)cbr.p, xf.p, vr.p);
+    }
+  }
+
+  // Comm::reverse_comm (f, drho, de): swaps in reverse order, ghosts back to senders
+  void reverse_multi() {
+    for (int k = nswap - 1; k >= 0; k--) {
+      Swap &sw = swaps[k];
+      cbs.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * 5 * sizeof(double), true, s);
+      cbr.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * 5 * sizeof(double), true, s);
+      if (sw.nrecv)
+        hipLaunchKernelGGL(k_pack_reverse, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
+                           sw.firstrecv, fo.p, de.p, (double *)cbs.p);
+      swap_move(sw.remote, (size_t)sw.nrecv * 5 * sizeof(double), sw.recvproc,
+                (size_t)sw.nsend * 5 * sizeof(double), sw.sendproc);
+      if (sw.nsend)
+        hipLaunchKernelGGL(k_unpack_reverse, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                           sw.list.p, (const double *)cbr.p, fo.p, de.p);
+    }
+  }
+
+  // CommBrick::exchange (comm_brick.cpp:573-680): atoms that left the brick along each
+  // split dimension go to the face neighbours, which keep the ones inside their slab
+  void exchange_multi() {
+    for (int d = 0; d < cfg.dim; d++) {
+      if (pg[d] == 1) continue;
+      const int n = nlocal;
+      flags.reserve(n > 0 ? n : 1);
+      flag2.reserve(n > 0 ? n : 1);
+      if (n)
+        hipLaunchKernelGGL(k_flag_leave, dim3(blocks(n)), dim3(BLK), 0, s, n, d, sublo[d],
+                           subhi[d], xf.p, flags.p, flag2.p);
+      const int nl = select_flagged(flags.p, n, sel);
+      const int nst = select_flagged(flag2.p, n, sel2);
+      cbs.reserve((size_t)(nl > 0 ? nl : 1) * sizeof(MigRec));
+      if (nl)
+        hipLaunchKernelGGL(k_pack_mig, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, xf.p,
+                           vr.p, vel.p, en.p, ty.p, tag.p, (MigRec *)cbs.p);
+      if (nl) {  // compact the staying atoms to the front (order kept)
+        DBuf<unsigned char> keep;
+        keep.reserve((size_t)(nst > 0 ? nst : 1) * sizeof(MigRec));
+        if (nst) {
+          hipLaunchKernelGGL(k_pack_mig, dim3(blocks(nst)), dim3(BLK), 0, s, nst, sel2.p, xf.p,
+                             vr.p, vel.p, en.p, ty.p, tag.p, (MigRec *)keep.p);
+          hipLaunchKernelGGL(k_gather_mig, dim3(blocks(nst)), dim3(BLK), 0, s, nst,
+                             (const int *)nullptr, (const MigRec *)keep.p, 0, xf.p, vr.p,
+                             vel.p, en.p, ty.p, tag.p);
+        }
+        SPH_HIP_TRY(hipStreamSynchronize(s));
+        keep.release();
+      }
+      nlocal = nst;
+      // pg == 2: both neighbours are the same brick, one exchange; otherwise send the
+      // leavers to both and let each keep its own
+      const int nex = (pg[d] == 2) ? 1 : 2;
+      for (int x = 0; x < nex; x++) {
+        const int dest = procneigh[d][x], src = procneigh[d][1 - x];
+        const int nr = tr->exchange_count(nl, dest, src, s);
+        cbr.reserve((size_t)(nr > 0 ? nr : 1) * sizeof(MigRec));
+        tr->exchange(cbs.p, (size_t)nl * sizeof(MigRec), dest, cbr.p, (size_t)nr * sizeof(MigRec),
+                     src, s);
+        if (nr == 0) continue;
+        flags.reserve(nr);
+        hipLaunchKernelGGL(k_flag_mine, dim3(blocks(nr)), dim3(BLK), 0, s, nr, d, sublo[d],
+                           subhi[d], (const MigRec *)cbr.p, flags.p);
+        const int nm = select_flagged(flags.p, nr, sel2);
+        if (nm == 0) continue;
+        ensure_atoms((size_t)nlocal + nm, true);
+        vel.reserve((size_t)nlocal + nm, true, s);
+        tag.reserve((size_t)nlocal + nm, true, s);
+        hipLaunchKernelGGL(k_gather_mig, dim3(blocks(nm)), dim3(BLK), 0, s, nm, sel2.p,
+                           (const MigRec *)cbr.p, nlocal, xf.p, vr.p, vel.p, en.p, ty.p, tag.p);
+        nlocal += nm;
+      }
+    }
+    fo.reserve(nlocal > 0 ? nlocal : 1, true, s);
+    de.reserve(nlocal > 0 ? nlocal : 1, true, s);
+  }
+
   void borders() {
+    if (multi()) {
+      borders_multi();
+      return;
+    }
     nghost = 0;
     int nall = nlocal;
     const int ndim = cfg.dim;
@@ -565,6 +770,7 @@ struct sph_engine {
   // pbc + sort + borders + list(s); `need_csr` also builds the global-index CSR list
   void build_all(bool need_csr) {
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
+    if (multi()) exchange_multi();
     const bool st = want_staged();
     if (st || cfg.sort) sort_owned();
     borders();
@@ -589,6 +795,11 @@ struct sph_engine {
   }
 
   void forward() {
+    if (multi()) {
+      Scope t(this, T_COMM);
+      forward_multi();
+      return;
+    }
     if (nghost == 0) return;
     Scope t(this, T_COMM);
     hipLaunchKernelGGL(k_forward, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal, box,
@@ -629,7 +840,10 @@ struct sph_engine {
           }
         }
       }
-      if (nghost) {
+      if (multi()) {
+        Scope t(this, T_COMM);
+        forward_rho_multi();
+      } else if (nghost) {
         Scope t(this, T_COMM);
         hipLaunchKernelGGL(k_forward_rho, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost,
                            nlocal, gowner.p, xf.p, vr.p);
@@ -710,7 +924,9 @@ struct sph_engine {
     a.de = de.p;
     a.cf = dc;
     launch_force(cfg.dim, nt1(), s, cfg.tait_visc, force_mode | M_HALF, a);
-    if (nghost)
+    if (multi())
+      reverse_multi();
+    else if (nghost)
       hipLaunchKernelGGL(k_reverse, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, n, gowner.p,
                          fo.p, de.p);
     // post_force body force (fix gravity style), as the full-list kernel applies it
@@ -777,10 +993,13 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
   SPH_REQUIRE(cfg->dim == 2 || cfg->dim == 3, SPH_HIP_EINVAL, "dimension must be 2 or 3");
   SPH_REQUIRE(cfg->ntypes >= 1 && cfg->ntypes <= SPH_MAXTYPES, SPH_HIP_EINVAL,
               "ntypes %d outside [1,%d]", cfg->ntypes, SPH_MAXTYPES);
-  const int pg = cfg->procgrid[0] * cfg->procgrid[1] * cfg->procgrid[2];
-  SPH_REQUIRE(pg == 1 || pg == 0, SPH_HIP_EINVAL,
-              "procgrid %dx%dx%d: multi-rank bricks go through sph_engine_comm_init",
-              cfg->procgrid[0], cfg->procgrid[1], cfg->procgrid[2]);
+  const int pgn = cfg->procgrid[0] * cfg->procgrid[1] * cfg->procgrid[2];
+  SPH_REQUIRE(pgn == 0 || (cfg->procgrid[0] >= 1 && cfg->procgrid[1] >= 1 &&
+                           cfg->procgrid[2] >= 1 && cfg->rank >= 0 && cfg->rank < pgn),
+              SPH_HIP_EINVAL, "bad procgrid %dx%dx%d / rank %d", cfg->procgrid[0],
+              cfg->procgrid[1], cfg->procgrid[2], cfg->rank);
+  SPH_REQUIRE(pgn <= 1 || cfg->dim == 3 || cfg->procgrid[2] == 1, SPH_HIP_EINVAL,
+              "2-D runs cannot split z");
   require_device(device);
   sph_engine *e = new sph_engine;
   try {
@@ -824,17 +1043,40 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin);
     SPH_REQUIRE(e->cutneighmax > 0.0, SPH_HIP_EINVAL, "no pair style enabled / zero cutoff");
     e->cutghost = e->cutneighmax;  // CommBrick::setup: cutghost = cutneighmax (:166)
+    if (pgn > 1) {
+      for (int k = 0; k < 3; k++) e->pg[k] = cfg->procgrid[k];
+      e->nprocs = pgn;
+      e->me = cfg->rank;
+    }
+    // brick of this rank, x fastest (Domain::set_local_box with uniform xsplit, domain.cpp)
+    e->myloc[0] = e->me % e->pg[0];
+    e->myloc[1] = (e->me / e->pg[0]) % e->pg[1];
+    e->myloc[2] = e->me / (e->pg[0] * e->pg[1]);
     for (int k = 0; k < 3; k++) {
       e->box.lo[k] = cfg->boxlo[k];
       e->box.hi[k] = cfg->boxhi[k];
       e->box.prd[k] = cfg->boxhi[k] - cfg->boxlo[k];
       e->box.periodic[k] = (k < cfg->dim) ? cfg->periodic[k] : 0;
-      e->sublo[k] = cfg->boxlo[k];
-      e->subhi[k] = cfg->boxhi[k];
+      const double lo = (double)e->myloc[k] / e->pg[k], hi = (double)(e->myloc[k] + 1) / e->pg[k];
+      e->sublo[k] = cfg->boxlo[k] + e->box.prd[k] * lo;
+      e->subhi[k] = (e->myloc[k] + 1 == e->pg[k]) ? cfg->boxhi[k]
+                                                   : cfg->boxlo[k] + e->box.prd[k] * hi;
+      auto at = [&](int dx, int dy, int dz) {
+        const int l[3] = {(e->myloc[0] + dx + e->pg[0]) % e->pg[0],
+                          (e->myloc[1] + dy + e->pg[1]) % e->pg[1],
+                          (e->myloc[2] + dz + e->pg[2]) % e->pg[2]};
+        return (l[2] * e->pg[1] + l[1]) * e->pg[0] + l[0];
+      };
+      e->procneigh[k][0] = at(k == 0 ? -1 : 0, k == 1 ? -1 : 0, k == 2 ? -1 : 0);
+      e->procneigh[k][1] = at(k == 0 ? 1 : 0, k == 1 ? 1 : 0, k == 2 ? 1 : 0);
       if (e->box.periodic[k])
         SPH_REQUIRE(e->cutghost < e->box.prd[k], SPH_HIP_EINVAL,
                     "ghost cutoff %g >= box length %g in dim %d (multi-hop borders unsupported)",
                     e->cutghost, e->box.prd[k], k);
+      if (e->pg[k] > 1)  // CommBrick maxneed = 1: a brick must be wider than the ghost cut
+        SPH_REQUIRE(e->cutghost < e->subhi[k] - e->sublo[k], SPH_HIP_EINVAL,
+                    "ghost cutoff %g >= brick width %g in dim %d (multi-hop swaps unsupported)",
+                    e->cutghost, e->subhi[k] - e->sublo[k], k);
     }
     e->sc.dtv = cfg->dt;
     e->sc.dtf = 0.5 * cfg->dt * (cfg->ftm2v > 0 ? cfg->ftm2v : 1.0);  // fix_meso.cpp:63-66
@@ -883,6 +1125,12 @@ int sph_engine_destroy(sph_engine *e) {
   e->qbeg.release();
   e->tb.release();
   e->xb.release();
+  for (auto &sw : e->swaps) sw.list.release();
+  e->cbs.release();
+  e->cbr.release();
+  e->flag2.release();
+  e->sel2.release();
+  delete e->tr;
   e->blen.release();
   e->boff.release();
   e->nbr16.release();
@@ -939,6 +1187,9 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
 int sph_engine_setup(sph_engine *e) {
   SPH_API_BEGIN
   SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_setup: NULL engine");
+  SPH_REQUIRE(!e->multi() || e->tr, SPH_HIP_ECOMM,
+              "brick %d of %d: attach a communicator (sph_engine_comm_init / _comm_local) first",
+              e->me, e->nprocs);
   SPH_HIP_TRY(hipSetDevice(e->device));
   e->setup();
   SPH_HIP_TRY(hipGetLastError());
@@ -984,8 +1235,11 @@ int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, doubl
   SPH_HIP_TRY(hipMemcpyAsync(hde.data(), e->de.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  // one brick of a decomposition (or caller tags): local slot order, tag[] names the atom;
+  // otherwise the set_atoms order
+  const bool local_order = e->multi() || e->global_tags;
   for (int i = 0; i < n; i++) {
-    const int t = ht[i];
+    const int t = local_order ? i : ht[i];
     SPH_REQUIRE(t >= 0 && t < n, SPH_HIP_ERUNTIME, "corrupt tag %d", t);
     if (x) {
       x[3 * t] = hx[i].x;
@@ -1006,7 +1260,7 @@ int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, doubl
     }
     if (drho) drho[t] = hf[i].w;
     if (de) de[t] = hde[i];
-    if (tag) tag[i] = t;
+    if (tag) tag[t] = ht[i];
   }
   SPH_API_END
 }
@@ -1022,7 +1276,8 @@ int sph_engine_neighbor_counts(sph_engine *e, int *numneigh) {
                              hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
-  for (int i = 0; i < n; i++) numneigh[ht[i]] = hc[i];
+  const bool local_order = e->multi() || e->global_tags;
+  for (int i = 0; i < n; i++) numneigh[local_order ? i : ht[i]] = hc[i];
   SPH_API_END
 }
 
@@ -1075,18 +1330,60 @@ int sph_engine_sync(sph_engine *e) {
 
 int sph_engine_comm_uid(void *uid128) {
   SPH_API_BEGIN
-  SPH_REQUIRE(false, SPH_HIP_ECOMM, "RCCL brick decomposition not built in this library yet");
-  (void)uid128;
+  SPH_REQUIRE(uid128, SPH_HIP_EINVAL, "sph_engine_comm_uid: NULL buffer");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId id;
+  SPH_NCCL_TRY(ncclGetUniqueId(&id));
+  memcpy(uid128, &id, sizeof(id));
   SPH_API_END
+}
+
+static void attach(sph_engine *e, Transport *t) {
+  SPH_REQUIRE(t->size() == e->nprocs && t->rank() == e->me, SPH_HIP_EINVAL,
+              "communicator rank %d/%d does not match the engine's brick %d/%d", t->rank(),
+              t->size(), e->me, e->nprocs);
+  delete e->tr;
+  e->tr = t;
 }
 
 int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank) {
   SPH_API_BEGIN
-  (void)e;
-  (void)uid128;
-  (void)nranks;
-  (void)rank;
-  SPH_REQUIRE(false, SPH_HIP_ECOMM, "RCCL brick decomposition not built in this library yet");
+  SPH_REQUIRE(e && uid128, SPH_HIP_EINVAL, "sph_engine_comm_init: NULL argument");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  ncclUniqueId id;
+  memcpy(&id, uid128, sizeof(id));
+  attach(e, new RcclTransport(id, nranks, rank));
+  SPH_API_END
+}
+
+int sph_local_world_create(int nranks, sph_local_world **out) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(out && nranks >= 1, SPH_HIP_EINVAL, "sph_local_world_create: bad argument");
+  *out = reinterpret_cast<sph_local_world *>(new LocalWorld(nranks));
+  SPH_API_END
+}
+
+int sph_local_world_destroy(sph_local_world *w) {
+  delete reinterpret_cast<LocalWorld *>(w);
+  return SPH_HIP_OK;
+}
+
+int sph_engine_comm_local(sph_engine *e, sph_local_world *w, int rank) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && w, SPH_HIP_EINVAL, "sph_engine_comm_local: NULL argument");
+  LocalWorld *lw = reinterpret_cast<LocalWorld *>(w);
+  SPH_REQUIRE(rank >= 0 && rank < lw->n, SPH_HIP_EINVAL, "rank %d outside [0,%d)", rank, lw->n);
+  attach(e, new LocalTransport(lw, rank));
+  SPH_API_END
+}
+
+int sph_engine_set_tags(sph_engine *e, const int *tags) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && (tags || e->nlocal == 0), SPH_HIP_EINVAL, "sph_engine_set_tags: bad argument");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  if (e->nlocal)
+    SPH_HIP_TRY(hipMemcpy(e->tag.p, tags, e->nlocal * sizeof(int), hipMemcpyHostToDevice));
+  e->global_tags = true;
   SPH_API_END
 }
 

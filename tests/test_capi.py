@@ -17,7 +17,7 @@ LIB = os.path.join(ROOT, "lammps-sph-multiphase_amd", "libsph_hip.so")
 def declared_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(sph_(?:hip|engine)_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(sph_(?:hip|engine|local_world)_\w+)\s*\(", txt)))
 
 
 @pytest.fixture(scope="module")

@@ -1,0 +1,170 @@
+"""GPU parity of the brick decomposition (CommBrick swaps: borders, forward comm, forward
+rho, setup reverse comm, exchange/migration at rebuilds) against the single-process oracle
+driver.  Several bricks run in one process, one host thread per brick, each its own engine
+on the one GPU, exchanging halos through a local world (device copies) -- the same engine
+code path the RCCL transport drives across GPUs; only the copy primitive differs.
+
+Per tag: neighbor counts bit-exact, rho/f/drho/de/x/v/e within 1e-10 normwise.
+
+The systems start at rest.  The reference's step-0 force call sees ghost `vest` as it was
+at borders() time (borders run before FixMeso::setup_pre_force): with a decomposition the
+ghosts of a neighbouring brick are stale, with one process only the periodic images are --
+so the reference's own setup forces depend on the processor grid unless v = 0 at setup.
+From rest every decomposition must agree with the single-process oracle."""
+import threading
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from conftest import rel_err
+from scenarios import c2_system, c3_system
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def brick_index(x, lo, hi, pg):
+    idx = np.zeros(x.shape[0], dtype=np.int64)
+    mult = 1
+    for d in range(3):
+        prd = hi[d] - lo[d]
+        c = np.zeros(x.shape[0], dtype=np.int64)
+        for k in range(1, pg[d]):
+            c += (x[:, d] >= lo[d] + prd * (k / pg[d])).astype(np.int64)
+        idx += c * mult
+        mult *= pg[d]
+    return idx
+
+
+def at_rest(s):
+    s.v[:] = 0.0
+    return s
+
+
+def run_bricks(sph_amd, s, ph, pg, nsteps, every=None):
+    nt = s.ntypes
+    P = int(np.prod(pg))
+    kw = {}
+    if ph.rhosum_nstep > 0:
+        kw["rhosum"] = dict(nstep=ph.rhosum_nstep, cut=ph.rhosum_cut)
+    if ph.tait:
+        kw["tait"] = dict(rho0=ph.rho0, c0=ph.c0, visc=ph.visc, cut=ph.tait_cut, morris=ph.morris)
+    if ph.heat:
+        kw["heat"] = dict(alpha=ph.alpha, cut=ph.heat_cut)
+    world = sph_amd.LocalWorld(P)
+    owner = brick_index(s.x, s.boxlo, s.boxhi, pg)
+    engines = []
+    for r in range(P):
+        cfg = sph_amd.make_config(s.dim, nt, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
+                                  neigh_every=every or ph.every, kernel_path=1,
+                                  procgrid=pg, rank=r, **kw)
+        eng = sph_amd.Engine(cfg)
+        sel = np.nonzero(owner == r)[0]
+        eng.set_atoms(s.x[sel], s.v[sel], s.type[sel], s.rho[sel], s.e[sel], s.cv[sel])
+        eng.set_tags(sel)
+        eng.comm_local(world, r)
+        engines.append(eng)
+    errors = []
+
+    def work(eng):
+        try:
+            eng.setup()
+            eng.run(nsteps)
+        except Exception as ex:  # surfaced below
+            errors.append(ex)
+
+    th = [threading.Thread(target=work, args=(e,)) for e in engines]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in th), "brick threads hung"
+    assert not errors, errors
+    n = s.n
+    out = {k: np.zeros((n, 3)) for k in ("x", "v", "f")}
+    out.update({k: np.zeros(n) for k in ("rho", "e", "drho", "de")})
+    counts = np.zeros(n, dtype=np.int32)
+    seen = np.zeros(n, dtype=np.int64)
+    nloc = []
+    for eng in engines:
+        got = eng.get_atoms()
+        tags = got["tag"]
+        seen[tags] += 1
+        for k in out:
+            out[k][tags] = got[k]
+        counts[tags] = eng.neighbor_counts()
+        nloc.append(eng.nlocal)
+    assert (seen == 1).all(), "every atom owned by exactly one brick"
+    for e in engines:
+        e.close()
+    world.close()
+    return out, counts, nloc
+
+
+def compare(out, ref, tol=TOL):
+    s = ref.s
+    assert rel_err(out["rho"], s.rho) < tol
+    assert rel_err(out["f"], ref.f) < tol
+    assert rel_err(out["drho"], ref.drho) < tol
+    assert rel_err(out["de"], ref.de) < tol
+    assert rel_err(out["x"], s.x) < tol
+    assert rel_err(out["v"], s.v) < tol
+
+
+@pytest.mark.parametrize("pg", [(2, 1, 1), (1, 2, 2), (2, 2, 2)])
+def test_bricks_c2_setup_and_run(gpu, sph_amd, pg):
+    s = at_rest(c2_system(12))
+    ph = po.c2_physics()
+    ph.every = 4
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(9)                       # rebuilds (and migrations) at steps 4 and 8
+    out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9)
+    assert sum(nloc) == s.n
+    assert np.array_equal(counts, ref.numneigh_full())
+    compare(out, ref)
+
+
+def test_bricks_c3_morris_heat(gpu, sph_amd):
+    s = at_rest(c3_system(12))
+    ph = po.c3_physics()
+    ph.every = 3
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(7)
+    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 7)
+    assert np.array_equal(counts, ref.numneigh_full())
+    compare(out, ref)
+    assert rel_err(out["e"], ref.s.e) < TOL
+
+
+def test_bricks_migration(gpu, sph_amd):
+    """Pressure-driven motion from rest with a larger step: atoms of the lattice plane that
+    sits on the brick face (x = 6) cross it between rebuilds and migrate."""
+    s = at_rest(c2_system(12))
+    ph = po.c2_physics()
+    ph.dt = 5e-3
+    ph.every = 5
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(40)
+    side0 = s.x[:, 0] < 6.0
+    moved = (ref.s.x[:, 0] < 6.0) != side0
+    out, counts, nloc = run_bricks(sph_amd, s, ph, (2, 1, 1), 40)
+    assert moved.any(), "no atom crossed the brick face: the test would not exercise migration"
+    assert sum(nloc) == s.n
+    assert np.array_equal(counts, ref.numneigh_full())
+    compare(out, ref)
+
+
+def test_bricks_2d(gpu, sph_amd):
+    s = at_rest(c2_system(30, dim=2))
+    ph = po.c2_physics(2.5)
+    ph.every = 4
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(9)
+    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 9)
+    assert np.array_equal(counts, ref.numneigh_full())
+    compare(out, ref)

@@ -8,8 +8,10 @@ visc 0.1, h 3), skin 0.3, neighbor rebuild every 10 steps, dt 1e-3, fix meso.  A
 is one full Verlet step of the device-resident engine (integrate, forward comm or
 rebuild, rhosum, forward rho, taitwater, integrate) with everything already in HBM.
 
-N > 1 ranks (torch.distributed.run) each advance their own 1M-particle box on their own
-GPU (weak scaling; see DESIGN.md "Multi-GPU" for the status of the brick decomposition).
+N > 1 ranks (torch.distributed.run, one per GPU) run ONE box decomposed into N bricks
+(CommBrick-style spatial decomposition, halo exchange and migration over RCCL/xGMI): each
+brick holds a 100^3 share, the global box is 100*procgrid per side (weak scaling; N = 8 is
+BASELINE config C4, 200^3 = 8M particles on 2x2x2 GPUs).
 Rank 0 prints ONE JSON line.  `roofline` covers the dominant kernel (the taitwater force
 pass), timed live with HIP events recorded on the engine's stream; `cpu_baseline` is the
 oracle's C restatement timed on this host on a bounded sample (rank 0, N = 1 only).
@@ -38,26 +40,62 @@ def load_pkg():
 
 def make_system(n, seed):
     """Same construction as oracle/pyoracle.cubic_lattice."""
+    x, v, t, rho, e, cv, _ = brick_lattice(n, (1, 1, 1), 0, seed)
+    return x, v, t, rho, e, cv
+
+
+def procgrid_for(nranks):
+    """Brick grid for nranks: least total face area, x >= y >= z (2 -> 2x1x1, 8 -> 2x2x2)."""
+    best = None
+    for px in range(1, nranks + 1):
+        if nranks % px:
+            continue
+        for py in range(1, nranks // px + 1):
+            if (nranks // px) % py:
+                continue
+            pz = nranks // (px * py)
+            if not (px >= py >= pz):
+                continue
+            area = px * py + py * pz + px * pz
+            if best is None or area < best[0]:
+                best = (area, (px, py, pz))
+    return best[1]
+
+
+def brick_lattice(n, pg, rank, seed=12345):
+    """Rank `rank`'s n^3 share of the global (n*pg)-per-side jittered sc lattice, with the
+    global tags of its sites.  pg = (1,1,1), rank 0 is exactly the single-box C2 system."""
+    loc = (rank % pg[0], (rank // pg[0]) % pg[1], rank // (pg[0] * pg[1]))
     g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij"), -1)
     g = g.reshape(-1, 3)
-    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]
+    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]   # create_atoms order: z, y, x
+    g = g + np.array(loc) * n
     x = g.astype(np.float64)
-    x += np.random.default_rng(seed).uniform(-0.1, 0.1, size=x.shape)
-    v = np.random.default_rng(4928459).normal(0.0, 0.01, size=x.shape)
+    x += np.random.default_rng(seed + rank).uniform(-0.1, 0.1, size=x.shape)
+    v = np.random.default_rng(4928459 + rank).normal(0.0, 0.01, size=x.shape)
     N = x.shape[0]
-    return x, v, np.ones(N, np.int32), np.ones(N), np.zeros(N), np.ones(N)
+    NX, NY = n * pg[0], n * pg[1]
+    tags = ((g[:, 2] * NY + g[:, 1]) * NX + g[:, 0]).astype(np.int32)
+    return x, v, np.ones(N, np.int32), np.ones(N), np.zeros(N), np.ones(N), tags
 
 
-def c2_config(sph, n):
+def share_uid(dist, rank, make_uid):
+    """RCCL unique id from rank 0 to every rank (torch.distributed object broadcast)."""
+    obj = [make_uid() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def c2_config(sph, n, pg=(1, 1, 1), rank=0):
     h = 3.0
     cut = np.zeros((2, 2))
     cut[1, 1] = h
     visc = np.zeros((2, 2))
     visc[1, 1] = 0.1
-    return sph.make_config(3, 1, [0.0, 0.0, 0.0], [float(n)] * 3, [1, 1, 1], [0.0, 1.0], 0.3,
-                           1e-3, neigh_every=10, rhosum=dict(nstep=1, cut=cut),
+    return sph.make_config(3, 1, [0.0, 0.0, 0.0], [float(n * p) for p in pg], [1, 1, 1],
+                           [0.0, 1.0], 0.3, 1e-3, neigh_every=10, rhosum=dict(nstep=1, cut=cut),
                            tait=dict(rho0=np.array([0.0, 1.0]), c0=np.array([0.0, 10.0]),
-                                     visc=visc, cut=cut))
+                                     visc=visc, cut=cut), procgrid=pg, rank=rank)
 
 
 def cpu_baseline(n_cpu, steps=2):
@@ -135,7 +173,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=100, help="lattice edge (n^3 particles per GPU)")
+    ap.add_argument("--edge", type=int, default=100, help="lattice edge (edge^3 particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
@@ -155,11 +193,15 @@ def main():
     assert ndev > 0, "bench.py needs a HIP device"
     dev = local % ndev
 
-    x, v, t, rho, e, cv = make_system(args.n, 12345 + rank)
-    cfg = c2_config(sph, args.n)
-    cfg.kernel_path = args.path
+    pg = procgrid_for(world)
+    x, v, t, rho, e, cv, tags = brick_lattice(args.edge, pg, rank)
+    cfg = c2_config(sph, args.edge, pg, rank)
+    cfg.kernel_path = args.path if world == 1 else 1
     eng = sph.Engine(cfg, device=dev)
     eng.set_atoms(x, v, t, rho, e, cv)
+    if world > 1:
+        eng.set_tags(tags)
+        eng.comm_init(share_uid(dist, rank, sph.comm_uid), world, rank)
     eng.setup()
     eng.run(args.warmup)
     eng.sync()
@@ -185,7 +227,7 @@ def main():
     st = eng.stats()
 
     nloc = st["nlocal"]
-    total_ps = nloc * world * args.steps / elapsed
+    total_ps = args.edge ** 3 * world * args.steps / elapsed
     n_full = st["nbr_full"] / max(nloc, 1)
     n_half = n_full / 2.0
     # algorithmic bytes per particle per pass (half-list CSR, int32, fp64)
@@ -210,11 +252,16 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (jittered sc lattice, gaussian velocities, seeded)",
-        "config": {"workload": f"C2: {nloc} particles/GPU cubic lattice, sph/rhosum + sph/taitwater, "
-                               "periodic, skin 0.3, rebuild every 10",
+        "config": {"workload": (f"C2: {args.edge ** 3} particles/GPU cubic lattice, sph/rhosum + "
+                                "sph/taitwater, periodic, skin 0.3, rebuild every 10")
+                               + ("" if world == 1 else
+                                  f"; one {args.edge * pg[0]}x{args.edge * pg[1]}x{args.edge * pg[2]} box "
+                                  f"in {pg[0]}x{pg[1]}x{pg[2]} bricks (C4 at 8 GPUs)"),
                    "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "parallelism": f"{world} independent 1M boxes (one per GPU)",
+                   "parallelism": ("single GPU" if world == 1 else
+                                   f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo "
+                                   "exchange + migration, one rank per GPU"),
                    "kernel_path": "lds-staged bins" if st["staged"] else "csr rows"},
         "roofline": {"bound": "hbm", "kernel": ("k_bin_force" if st["staged"] else "k_row_force")
                      + "<TAIT> (sph/taitwater pass)",

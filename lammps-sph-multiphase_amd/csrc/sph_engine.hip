@@ -1339,9 +1339,13 @@ int sph_engine_comm_uid(void *uid128) {
 }
 
 static void attach(sph_engine *e, Transport *t) {
-  SPH_REQUIRE(t->size() == e->nprocs && t->rank() == e->me, SPH_HIP_EINVAL,
-              "communicator rank %d/%d does not match the engine's brick %d/%d", t->rank(),
-              t->size(), e->me, e->nprocs);
+  const int sz = t->size(), rk = t->rank();
+  if (sz != e->nprocs || rk != e->me) {
+    delete t;
+    SPH_REQUIRE(false, SPH_HIP_EINVAL,
+                "communicator rank %d/%d does not match the engine's brick %d/%d", rk, sz,
+                e->me, e->nprocs);
+  }
   delete e->tr;
   e->tr = t;
 }

@@ -168,3 +168,23 @@ def test_bricks_2d(gpu, sph_amd):
     out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 9)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
+
+
+def test_rccl_communicator_single_rank(gpu, sph_amd):
+    """sph_engine_comm_uid / comm_init on a one-rank communicator (the RCCL transport's
+    setup and teardown; multi-GPU runs use the same calls with one rank per GPU)."""
+    s = at_rest(c2_system(8))
+    ph = po.c2_physics()
+    cfg = sph_amd.make_config(3, 1, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
+                              rhosum=dict(nstep=1, cut=ph.rhosum_cut),
+                              tait=dict(rho0=ph.rho0, c0=ph.c0, visc=ph.visc, cut=ph.tait_cut),
+                              kernel_path=1)
+    eng = sph_amd.Engine(cfg)
+    eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)
+    uid = sph_amd.comm_uid()
+    assert len(uid) == 128
+    eng.comm_init(uid, 1, 0)
+    eng.setup()
+    eng.run(3)
+    assert np.isfinite(eng.get_atoms()["f"]).all()
+    eng.close()

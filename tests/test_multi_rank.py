@@ -1,0 +1,73 @@
+"""The N > 1 host path of bench.py on CPU (torch.distributed gloo, world size 2): brick grid,
+each rank's share of the global lattice, the RCCL unique-id broadcast from rank 0, and the
+max-over-ranks timing reduction.  The device side of the decomposition is covered by
+tests/test_gpu_bricks.py (several bricks in one process on the GPU)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def worker(rank, world, port, q):
+    import torch
+
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pg = bench.procgrid_for(world)
+        n = 4
+        x, v, t, rho, e, cv, tags = bench.brick_lattice(n, pg, rank)
+        uid = bench.share_uid(dist, rank, lambda: bytes(range(128)))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (tags.tolist(), x.tolist()))
+        tt = torch.tensor([0.1 * (rank + 1)], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        q.put((rank, pg, uid, gathered, float(tt.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_bricks_gloo():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    for rank, pg, uid, gathered, tmax in res:
+        assert pg == (2, 1, 1)
+        assert uid == bytes(range(128))              # rank 0's id reached every rank
+        assert tmax == pytest.approx(0.2)            # max over ranks
+    gathered = res[0][3]
+    tags = np.concatenate([np.array(g[0]) for g in gathered])
+    xs = np.concatenate([np.array(g[1]) for g in gathered])
+    n, NX = 4, 8
+    assert np.array_equal(np.sort(tags), np.arange(n * n * NX))  # a partition of the box
+    # every site lies in its rank's brick (up to the +-0.1 jitter the first exchange fixes)
+    for r, g in enumerate(gathered):
+        xr = np.array(g[1])
+        assert (xr[:, 0] >= r * n - 0.1).all() and (xr[:, 0] < (r + 1) * n + 0.1).all()
+    # the sites are exactly those of the global lattice, tag = (z*NY + y)*NX + x
+    site = np.rint(xs).astype(int)
+    assert np.array_equal((site[:, 2] * n + site[:, 1]) * NX + site[:, 0], tags)

@@ -262,8 +262,10 @@ def main():
                    "parallelism": ("single GPU" if world == 1 else
                                    f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo "
                                    "exchange + migration, one rank per GPU"),
-                   "kernel_path": "lds-staged bins" if st["staged"] else "csr rows"},
-        "roofline": {"bound": "hbm", "kernel": ("k_bin_force" if st["staged"] else "k_row_force")
+                   "kernel_path": {1: "lds-staged bins", 2: "lds tiles"}.get(st["staged"],
+                                                                             "csr rows")},
+        "roofline": {"bound": "hbm",
+                     "kernel": {1: "k_bin_force", 2: "k_tile_force"}.get(st["staged"], "k_row2_force")
                      + "<TAIT> (sph/taitwater pass)",
                      "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,

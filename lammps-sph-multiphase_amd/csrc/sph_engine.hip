@@ -21,6 +21,8 @@
 #include "sph_bin_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_row_kernels.h"
+#include "sph_row2_kernels.h"
+#include "sph_tile_kernels.h"
 #include "sph_util.h"
 
 using namespace sph;
@@ -36,8 +38,16 @@ int row_tile() {
   static int t = env_int("SPH_ROWTILE", 3);
   return t;
 }
+// SPH_ROW2TILE: shape index of SPH_ROW2_TILES (default 3 = 8 lanes x 4 pairs, the fastest
+// with lane-pair gathers on C2 1M: profiles/r01/sweep_row2.log)
+int row2_tile() {
+  static int t = env_int("SPH_ROW2TILE", 3);
+  return t;
+}
 }  // namespace sph
-// SPH_ROWK=0 routes the engine through the generic pair-layer kernels (comparison only)
+// SPH_ROWK: 2 = second-generation row kernels (buffer loads, index prefetch, one-step
+// Newton rcp/sqrt; default), 1 = first-generation row kernels, 0 = the generic
+// pair-layer kernels (comparison only)
 // list builder (default 2, fastest end to end on C2 1M: tools/sweep_neigh.sh):
 // 3 = binned copy over full-size bins (27-bin stencil, rows in lockstep),
 // 2 = binned copy over half-size bins with per-row trimming, 1 = bidx-indirect (original)
@@ -45,9 +55,26 @@ static int neigh_q() {
   static int v = env_int("SPH_NEIGH", 2);
   return v == 1 ? 0 : v;
 }
-static bool row_kernels() {
-  static bool on = env_int("SPH_ROWK", 1) != 0;
-  return on;
+static int row_gen() {
+  static int g = env_int("SPH_ROWK", 2);
+  return g;
+}
+static bool row_kernels() { return row_gen() != 0; }
+// SPH_LP (default 1): lane-pair gathers in the row2 kernels; SPH_IV (default 0): 16-B
+// index vectors (4 consecutive entries per lane -- fewer index loads, but adjacent lanes
+// then gather records 4 entries apart and share fewer cache lines: slower on C2 1M,
+// profiles/r01/sweep_row2.log); SPH_EXP: study variants (kernel_sweep)
+static bool row2_lp() {
+  static bool v = env_int("SPH_LP", 1) != 0;
+  return v;
+}
+static bool row2_iv() {
+  static bool v = env_int("SPH_IV", 0) != 0;
+  return v;
+}
+static int row2_exp() {
+  static int v = env_int("SPH_EXP", 0);
+  return v;
 }
 
 namespace {
@@ -120,8 +147,14 @@ struct sph_engine {
   DBuf<int> bidx, bidx2, bstart, bend;
   // neighbor list
   DBuf<int> cnt, off, nbr;
-  int64_t nbr_total = 0;
+  int64_t nbr_total = 0;   // list entries (-1: strided list, counted on demand)
   int nbr_builds = 0, nbr_maxrow = 0;
+  bool strided = false;    // list in fixed-stride rows (row i at i*list_stride, ccnt[i])
+  int list_stride = 0;
+  // LDS-tiled path: bin-sorted ghost index list and its inverse
+  bool tiled = false;
+  DBuf<int> gidx, gpos;
+  DBuf<unsigned> nbr32;   // packed thread-major slot pairs
   // LDS-staged bin path
   bool staged = false;
   int stage_max = 0, rows_max = 0;
@@ -207,7 +240,8 @@ struct sph_engine {
     bidx.reserve(n);
     bidx2.reserve(n);
     // Morton order unless the staged path needs linear bins (and bins fit 10 bits/axis)
-    const bool mort = !want_staged() && bn.nb[0] <= 1024 && bn.nb[1] <= 1024 && bn.nb[2] <= 1024;
+    const bool mort = !want_staged() && !want_tiles() && bn.nb[0] <= 1024 && bn.nb[1] <= 1024 &&
+                      bn.nb[2] <= 1024;
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p,
                        bidx.p, mort ? 1 : 0);
     size_t tb = 0;
@@ -233,6 +267,7 @@ struct sph_engine {
   }
 
   bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2 && !multi(); }
+  bool want_tiles() const { return cfg.kernel_path == 2; }
 
   // order the ghost segment by bin too (the staged ranges need it contiguous)
   void sort_ghosts() {
@@ -611,8 +646,10 @@ struct sph_engine {
     nqbins = qb.nb[0] * qb.nb[1] * qb.nb[2];
   }
 
-  // CSR full list over half-size bins and a bin-ordered copy of all atoms
-  void build_list_q() {
+  // Full list over half-size bins and a bin-ordered copy of all atoms: CSR (count pass,
+  // scan, fill pass) or, when `csr` is false and an earlier build sized the rows, one
+  // fill pass into fixed-stride rows (ccnt = row counts; `strided` records which).
+  void build_list_q(bool csr) {
     const int n = nlocal, nall = nlocal + nghost;
     Bins b;
     for (int k = 0; k < 3; k++) {
@@ -643,13 +680,15 @@ struct sph_engine {
     off.reserve(n + 1);
     constexpr int G = 8, U = 2;
     dim3 grid(grid_for_rows(n, G)), block(BLK);
-    auto launch = [&](bool fill) {
+    auto launch = [&](bool fill, int stride) {
       if (n == 0) return;
       const bool t = nt1(), q2 = neigh_q() == 2;
+      int *const cnt_out = (!fill || stride > 0) ? ccnt.p : (int *)nullptr;
 #define SPH_NQ(F, T, R, TR)                                                                  \
   hipLaunchKernelGGL((k_neigh2<G, U, F, T, R, TR>), grid, block, 0, s, n, qb, cfg.dim, xf.p, \
-                     ty.p, xb.p, tb.p, qbeg.p, dc, F ? (int *)nullptr : ccnt.p,                \
-                     F ? off.p : (const int *)nullptr, F ? nbr.p : (int *)nullptr)
+                     ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
+                     (F && stride == 0) ? off.p : (const int *)nullptr,                        \
+                     F ? nbr.p : (int *)nullptr, stride, mx.p)
       if (fill) {
         if (q2) { if (t) SPH_NQ(true, true, 2, true); else SPH_NQ(true, false, 2, true); }
         else { if (t) SPH_NQ(true, true, 1, false); else SPH_NQ(true, false, 1, false); }
@@ -659,16 +698,43 @@ struct sph_engine {
       }
 #undef SPH_NQ
     };
-    launch(false);
+    mx.reserve(4);
+    // single pass into fixed-stride rows when a previous build sized them and nothing
+    // needs the CSR form (the setup half list, the tile/staged paths, row kernels gen < 2)
+    if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
+      nbr.reserve((size_t)n * list_stride);
+      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
+      launch(true, list_stride);
+      if (read_scalar(mx.p) == 0) {
+        strided = true;
+        nbr_total = -1;  // entries counted on demand (stats)
+        nbr_builds++;
+        return;
+      }
+    }
+    strided = false;
+    launch(false, 0);
     hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
     size_t tb2 = 0;
     SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, off.p, off.p, n + 1, s));
     tmp_reserve(tb2);
     SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb2, off.p, off.p, n + 1, s));
-    const int tot = read_scalar(off.p + n);
+    size_t tb3 = 0;
+    SPH_HIP_TRY(hipcub::DeviceReduce::Max(nullptr, tb3, ccnt.p, mx.p + 1, n, s));
+    tmp_reserve(tb3);
+    if (n > 0) SPH_HIP_TRY(hipcub::DeviceReduce::Max(tmp.p, tb3, ccnt.p, mx.p + 1, n, s));
+    else SPH_HIP_TRY(hipMemsetAsync(mx.p + 1, 0, sizeof(int), s));
+    int hm[2];
+    SPH_HIP_TRY(hipMemcpyAsync(&hm[0], off.p + n, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(&hm[1], mx.p + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    const int tot = hm[0];
     SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
     nbr.reserve(tot > 0 ? tot : 1);
-    launch(true);
+    launch(true, 0);
+    // stride of later single-pass builds: this build's longest row + 25% + 16, 16-aligned
+    list_stride = ((hm[1] + hm[1] / 4 + 16) + 15) & ~15;
+    nbr_maxrow = hm[1];
     if (!staged) {
       nbr_total = tot;
       nbr_builds++;
@@ -767,26 +833,129 @@ struct sph_engine {
     }
   }
 
+  // ---- LDS-tiled path (sph_tile_kernels.h) ---------------------------------------------
+  // Owned atoms are sorted by linear bin (sort_owned); ghosts stay where borders() put
+  // them and are reached through a bin-sorted index list (gidx, gbeg) and its inverse
+  // (gpos).  Bin descriptors (staged ranges) as for the staged path, then the CSR list is
+  // translated into thread-major 16-bit slot lists.  Returns false (CSR fallback) when a
+  // bin has too many rows or the LDS image does not fit.
+  bool build_tiles() {
+    const int n = nlocal, ng = nghost;
+    obeg.reserve(nbins + 1);
+    gbeg.reserve(nbins + 1);
+    desc.reserve((size_t)nbins * kDescInts);
+    mx.reserve(4);
+    gidx.reserve(ng > 0 ? ng : 1);
+    gpos.reserve(ng > 0 ? ng : 1);
+    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, n, 0,
+                       okey.p, obeg.p);
+    if (ng > 0) {
+      bkey.reserve(ng);
+      bkey2.reserve(ng);
+      bidx.reserve(ng);
+      hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p,
+                         bkey.p, bidx.p, 0);
+      int endbit = 1;
+      while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
+      size_t tb = 0;
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, gidx.p, ng, 0, endbit, s));
+      tmp_reserve(tb);
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, gidx.p, ng, 0, endbit, s));
+      hipLaunchKernelGGL(k_inverse_perm, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, gidx.p,
+                         gpos.p);
+    }
+    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, ng, 0,
+                       bkey2.p, gbeg.p);
+    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 4 * sizeof(int), s));
+    BinCtx c = bin_ctx();
+    hipLaunchKernelGGL(k_bin_desc, dim3(blocks(nbins)), dim3(BLK), 0, s, c, desc.p, mx.p);
+    blen.reserve(nbins + 1);
+    boff.reserve(nbins + 1);
+    hipLaunchKernelGGL(k_tile_plan, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, desc.p,
+                       off.p, blen.p, mx.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, blen.p, boff.p, nbins + 1, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, blen.p, boff.p, nbins + 1, s));
+    int hm[4];
+    SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(h_total, boff.p + nbins, sizeof(long long), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    stage_max = hm[0];
+    rows_max = hm[1];
+    if (hm[2] != 0 || hm[3] > TILE_LMAX || stage_max >= 65535 || rows_max < 1) return false;
+    const bool nt = nt1(), heat = (force_mode & M_HEAT) != 0;
+    lds_rho = tile_lds_bytes(false, false, nt, stage_max, rows_max);
+    lds_force = tile_lds_bytes(true, heat, nt, stage_max, rows_max);
+    if (lds_rho > 160 * 1024 || lds_force > 160 * 1024) return false;
+    const long long tot = *h_total;
+    nbr32.reserve(tot > 0 ? (size_t)tot : 1);
+    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_tile_translate, dim3(nbins), dim3(TB), 0, s, nbins, nlocal, desc.p,
+                       off.p, nbr.p, gpos.p, boff.p, nbr32.p, mx.p);
+    if (read_scalar(mx.p) != 0) return false;  // a neighbor outside the staged bins
+    return true;
+  }
+
+  template <bool NT1>
+  void tile_rhosum_t() {
+    auto k = k_tile_rhosum<NT1>;
+    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rho));
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(TB), lds_rho, s, nbins, rows_max, desc.p, gidx.p,
+                       xf.p, ty.p, vr.p, off.p, boff.p, nbr32.p, dc);
+  }
+  template <int VISC, int MODE, bool NT1>
+  void tile_force_t() {
+    auto k = k_tile_force<VISC, MODE, NT1>;
+    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
+    hipLaunchKernelGGL(k, dim3(nbins), dim3(TB), lds_force, s, nbins, rows_max, desc.p, gidx.p,
+                       xf.p, vr.p, ty.p, en.p, off.p, boff.p, nbr32.p, dc, fo.p, de.p,
+                       cfg.gravity[0], cfg.gravity[1], cfg.gravity[2]);
+  }
+  template <bool NT1>
+  void tile_force_n() {
+    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
+    switch (force_mode) {
+      case M_TAIT:
+        if (mor) tile_force_t<1, M_TAIT, NT1>(); else tile_force_t<0, M_TAIT, NT1>();
+        break;
+      case M_TAIT | M_HEAT:
+        if (mor) tile_force_t<1, M_TAIT | M_HEAT, NT1>();
+        else tile_force_t<0, M_TAIT | M_HEAT, NT1>();
+        break;
+      case M_HEAT: tile_force_t<0, M_HEAT, NT1>(); break;
+      default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", force_mode);
+    }
+  }
+  void launch_tile_rhosum() {
+    if (nt1()) tile_rhosum_t<true>(); else tile_rhosum_t<false>();
+  }
+  void launch_tile_force() {
+    if (nt1()) tile_force_n<true>(); else tile_force_n<false>();
+  }
+
   // pbc + sort + borders + list(s); `need_csr` also builds the global-index CSR list
   void build_all(bool need_csr) {
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
     if (multi()) exchange_multi();
     const bool st = want_staged();
-    if (st || cfg.sort) sort_owned();
+    if (st || cfg.sort || want_tiles()) sort_owned();
     borders();
     staged = false;
+    tiled = false;
     if (st) {
       sort_ghosts();
       staged = build_staged();
     }
     if (!staged || need_csr) {
       if (neigh_q()) {
-        build_list_q();
+        build_list_q(need_csr || st || want_tiles() || row_gen() != 2);
       } else {
         build_bins();
         build_list();
       }
     }
+    if (want_tiles() && nlocal > 0) tiled = build_tiles();
   }
 
   void rebuild() {
@@ -823,6 +992,39 @@ struct sph_engine {
     a.gz = cfg.gravity[2];
     return a;
   }
+  // extent of the list array the kernels may address
+  int64_t list_span() const { return strided ? (int64_t)nlocal * list_stride : nbr_total; }
+  // entries of the current list (sum of row counts for a strided list)
+  int64_t list_entries() {
+    if (!strided) return nbr_total;
+    if (nlocal == 0) return 0;
+    blen.reserve(1);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tb, ccnt.p, blen.p, nlocal, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(tmp.p, tb, ccnt.p, blen.p, nlocal, s));
+    long long v = 0;
+    SPH_HIP_TRY(hipMemcpyAsync(&v, blen.p, sizeof(long long), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    return v;
+  }
+  Row2Args row2_args() {
+    Row2Args b;
+    b.a = row_args();
+    b.nall = nlocal + nghost;
+    b.ntot = (int)list_span();
+    if (strided) {
+      b.stride = list_stride;
+      b.rcnt = ccnt.p;
+    }
+    b.lp = row2_lp();
+    b.iv = row2_iv();
+    b.exp = row2_exp();
+    return b;
+  }
+  bool use_row2() const {
+    return row_gen() == 2 && row2_fits((long)nlocal + nghost, (long)list_span());
+  }
 
   void pair_compute(bool do_rhosum, bool setup = false) {
     const int nall = nlocal + nghost;
@@ -831,8 +1033,12 @@ struct sph_engine {
         Scope t(this, T_RHO);
         if (staged) {
           launch_bin_rhosum();
+        } else if (tiled) {
+          launch_tile_rhosum();
         } else {
-          if (row_kernels()) {
+          if (use_row2()) {
+            row2_rhosum(nt1(), s, row2_args());
+          } else if (row_kernels()) {
             row_rhosum(nt1(), s, row_args());
           } else {
             RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
@@ -856,6 +1062,12 @@ struct sph_engine {
     } else if (force_mode && staged) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       launch_bin_force();
+    } else if (force_mode && tiled) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      launch_tile_force();
+    } else if (force_mode && use_row2()) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      row2_force(nt1(), cfg.tait_visc, force_mode, s, row2_args());
     } else if (force_mode && row_kernels()) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       row_force(nt1(), cfg.tait_visc, force_mode, s, row_args());
@@ -959,12 +1171,18 @@ struct sph_engine {
 
   // Verlet::run (verlet.cpp:222-308)
   void run(int nsteps) {
+    // the final_integrate of step k-1 runs fused with the initial_integrate of step k;
+    // the last step's final_integrate runs on its own after the loop
     for (int k = 0; k < nsteps; k++) {
       step++;
       {
         Scope t(this, T_INT);
-        hipLaunchKernelGGL(k_initial_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                           sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
+        if (k == 0)
+          hipLaunchKernelGGL(k_initial_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s,
+                             nlocal, sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
+        else
+          hipLaunchKernelGGL(k_final_initial, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
+                             sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
       }
       const int every = cfg.neigh_every > 0 ? cfg.neigh_every : 1;
       if ((step - last_build) % every == 0) {
@@ -974,12 +1192,12 @@ struct sph_engine {
         forward();
       }
       pair_compute(rhosum_due());
-      {
-        Scope t(this, T_INT);
-        hipLaunchKernelGGL(k_final_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                           sc, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
-      }
       if (timing && pending.size() > 4096) harvest();
+    }
+    if (nsteps > 0) {
+      Scope t(this, T_INT);
+      hipLaunchKernelGGL(k_final_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, sc,
+                         vr.p, en.p, ty.p, vel.p, fo.p, de.p);
     }
     SPH_HIP_TRY(hipGetLastError());
   }
@@ -1133,6 +1351,9 @@ int sph_engine_destroy(sph_engine *e) {
   delete e->tr;
   e->blen.release();
   e->boff.release();
+  e->gidx.release();
+  e->gpos.release();
+  e->nbr32.release();
   e->nbr16.release();
   if (e->dc) (void)hipFree(e->dc);
   if (e->s) (void)hipStreamDestroy(e->s);
@@ -1289,10 +1510,10 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->step = e->step;
   st->nlocal = e->nlocal;
   st->nghost = e->nghost;
-  st->nbr_full = e->nbr_total;
+  st->nbr_full = e->list_entries();
   st->nbr_builds = e->nbr_builds;
   st->nbr_maxrow = e->nbr_maxrow;
-  st->staged = e->staged ? 1 : 0;
+  st->staged = e->staged ? 1 : (e->tiled ? 2 : 0);
   st->stage_max = e->stage_max;
   st->ms_rhosum = e->ms[T_RHO];
   st->ms_tait = e->ms[T_TAIT];

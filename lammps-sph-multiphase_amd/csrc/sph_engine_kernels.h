@@ -70,6 +70,49 @@ static __global__ void k_final_integrate(int n, StepConst sc, double4 *__restric
   vr[i].w += sc.dtf * f.w;
 }
 
+// FixMeso::final_integrate of one step fused with initial_integrate of the next: nothing
+// between them touches these atoms (Verlet::run: output, then the next step's
+// initial_integrate, verlet.cpp:295-307, 230), so one streaming pass does both with the
+// two kernels' operations in their order (bit-identical results, half the traffic).
+static __global__ void k_final_initial(int n, StepConst sc, double4 *__restrict__ xf,
+                                       double4 *__restrict__ vr, double *__restrict__ en,
+                                       const int *__restrict__ ty, double4 *__restrict__ vel,
+                                       const double4 *__restrict__ fo,
+                                       const double *__restrict__ de) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int t = ty[i];
+  double4 vv = vr[i];
+  const double4 f = fo[i];
+  const double dei = de[i];
+  double e = en[i];
+  e += sc.dtf * dei;        // final
+  vv.w += sc.dtf * f.w;
+  e += sc.dtf * dei;        // initial
+  vv.w += sc.dtf * f.w;
+  if (!((sc.stationary_mask >> t) & 1)) {
+    double4 x = xf[i];
+    double4 v = vel[i];
+    const double dtfm = sc.dtf / sc.mass[t];
+    v.x += dtfm * f.x;      // final
+    v.y += dtfm * f.y;
+    v.z += dtfm * f.z;
+    vv.x = v.x + 2.0 * dtfm * f.x;   // initial
+    vv.y = v.y + 2.0 * dtfm * f.y;
+    vv.z = v.z + 2.0 * dtfm * f.z;
+    v.x += dtfm * f.x;
+    v.y += dtfm * f.y;
+    v.z += dtfm * f.z;
+    x.x += sc.dtv * v.x;
+    x.y += sc.dtv * v.y;
+    x.z += sc.dtv * v.z;
+    vel[i] = v;
+    xf[i] = x;
+  }
+  en[i] = e;
+  vr[i] = vv;
+}
+
 // FixMeso::setup_pre_force: vest = v (fix_meso.cpp:68-85)
 static __global__ void k_vest_from_v(int n, int stationary_mask, const int *__restrict__ ty,
                                      const double4 *__restrict__ vel,
@@ -367,13 +410,16 @@ __device__ __forceinline__ double slab_gap(double v, int b, int c, double lo, do
   return fmax(g - 1e-6 * size, 0.0);
 }
 
+// FILL with stride > 0: single pass into fixed-stride rows (row i at nbr + i*stride), the
+// row's count into cnt[i]; a row longer than stride keeps its first stride entries and
+// raises *ovf (the host then rebuilds with the counted CSR passes).
 template <int G, int U, bool FILL, bool NT1, int R, bool TRIM>
 __global__ void __launch_bounds__(256)
 k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
          const int *__restrict__ tb, const int *__restrict__ beg,
          const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-         int *__restrict__ nbr) {
+         int *__restrict__ nbr, int stride = 0, int *__restrict__ ovf = nullptr) {
   __shared__ double s_cns[NT2];
   const int nt1 = cf->ntypes + 1;
   if (!NT1) {
@@ -392,7 +438,9 @@ k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   const int zr = (dim == 3) ? R : 0;
   const double di = (double)i;
   int n = 0;
-  int pos = FILL ? off[i] : 0;
+  int *const row = FILL ? nbr + (stride > 0 ? (size_t)i * stride : (size_t)off[i]) : nullptr;
+  const int cap = stride > 0 ? stride : 0x7fffffff;
+  int pos = 0;
   const int gbase = (threadIdx.x & 63) & ~(G - 1);
   const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
   for (int bz = max(cz - zr, 0); bz <= min(cz + zr, q.nb[2] - 1); bz++) {
@@ -427,7 +475,8 @@ k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
                            rsq <= (NT1 ? cns1 : crow[tj[u]]);
           if (FILL) {
             const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
-            if (hit) nbr[pos + __popcll(m & ((1ull << lane) - 1ull))] = (int)xj[u].w;
+            const int q = pos + __popcll(m & ((1ull << lane) - 1ull));
+            if (hit && q < cap) row[q] = (int)xj[u].w;
             pos += __popcll(m);
           } else {
             n += hit ? 1 : 0;
@@ -439,6 +488,9 @@ k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   if (!FILL) {
     n = group_sum_i<G>(n);
     if (lane == 0) cnt[i] = n;
+  } else if (stride > 0 && lane == 0) {
+    cnt[i] = pos;
+    if (pos > stride) atomicOr(ovf, 1);
   }
 }
 

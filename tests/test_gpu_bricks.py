@@ -42,7 +42,7 @@ def at_rest(s):
     return s
 
 
-def run_bricks(sph_amd, s, ph, pg, nsteps, every=None):
+def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=1):
     nt = s.ntypes
     P = int(np.prod(pg))
     kw = {}
@@ -57,7 +57,7 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None):
     engines = []
     for r in range(P):
         cfg = sph_amd.make_config(s.dim, nt, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
-                                  neigh_every=every or ph.every, kernel_path=1,
+                                  neigh_every=every or ph.every, kernel_path=path,
                                   procgrid=pg, rank=r, **kw)
         eng = sph_amd.Engine(cfg)
         sel = np.nonzero(owner == r)[0]
@@ -112,34 +112,37 @@ def compare(out, ref, tol=TOL):
     assert rel_err(out["v"], s.v) < tol
 
 
-@pytest.mark.parametrize("pg", [(2, 1, 1), (1, 2, 2), (2, 2, 2)])
-def test_bricks_c2_setup_and_run(gpu, sph_amd, pg):
+@pytest.mark.parametrize("pg,path", [((2, 1, 1), 1), ((1, 2, 2), 1), ((2, 2, 2), 1),
+                                     ((2, 1, 1), 2), ((2, 2, 2), 2)])
+def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     s = at_rest(c2_system(12))
     ph = po.c2_physics()
     ph.every = 4
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(9)                       # rebuilds (and migrations) at steps 4 and 8
-    out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9)
+    out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9, path=path)
     assert sum(nloc) == s.n
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
 
 
-def test_bricks_c3_morris_heat(gpu, sph_amd):
+@pytest.mark.parametrize("path", [1, 2])
+def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     s = at_rest(c3_system(12))
     ph = po.c3_physics()
     ph.every = 3
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(7)
-    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 7)
+    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 7, path=path)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
     assert rel_err(out["e"], ref.s.e) < TOL
 
 
-def test_bricks_migration(gpu, sph_amd):
+@pytest.mark.parametrize("path", [1, 2])
+def test_bricks_migration(gpu, sph_amd, path):
     """Pressure-driven motion from rest with a larger step: atoms of the lattice plane that
     sits on the brick face (x = 6) cross it between rebuilds and migrate."""
     s = at_rest(c2_system(12))
@@ -151,21 +154,22 @@ def test_bricks_migration(gpu, sph_amd):
     ref.run(40)
     side0 = s.x[:, 0] < 6.0
     moved = (ref.s.x[:, 0] < 6.0) != side0
-    out, counts, nloc = run_bricks(sph_amd, s, ph, (2, 1, 1), 40)
+    out, counts, nloc = run_bricks(sph_amd, s, ph, (2, 1, 1), 40, path=path)
     assert moved.any(), "no atom crossed the brick face: the test would not exercise migration"
     assert sum(nloc) == s.n
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
 
 
-def test_bricks_2d(gpu, sph_amd):
+@pytest.mark.parametrize("path", [1, 2])
+def test_bricks_2d(gpu, sph_amd, path):
     s = at_rest(c2_system(30, dim=2))
     ph = po.c2_physics(2.5)
     ph.every = 4
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(9)
-    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 9)
+    out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 9, path=path)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
 

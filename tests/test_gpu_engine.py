@@ -47,16 +47,17 @@ def compare(eng, ref, tol=TOL):
     return got
 
 
-@pytest.mark.parametrize("sort,path", [(1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("sort,path", [(1, 0), (0, 1), (1, 1), (1, 2), (0, 2)])
 def test_setup_c2(gpu, sph_amd, sort, path):
-    """path 0 = LDS-staged bins (16-bit slot lists), 1 = CSR rows with global gathers."""
+    """path 0 = LDS-staged bins (16-bit slot lists), 1 = CSR rows with global gathers,
+    2 = LDS tiles (bin neighborhoods staged once, CSR list translated to slots)."""
     s = c2_system(12)
     ph = po.c2_physics()
     ref = po.RefRun(s, ph)
     ref.setup()
     eng = engine_for(sph_amd, s, ph, sort=sort, kernel_path=path)
     eng.setup()
-    assert eng.stats()["staged"] == (1 if path == 0 else 0)
+    assert eng.stats()["staged"] == {0: 1, 1: 0, 2: 2}[path]
     # neighbor membership: bit-exact counts per particle
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     st = eng.stats()
@@ -66,7 +67,7 @@ def test_setup_c2(gpu, sph_amd, sort, path):
     assert elem_rel_err(got["rho"], ref.s.rho) < 1e-13
 
 
-@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("path", [0, 1, 2])
 def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     s = c2_system(12)
     ph = po.c2_physics()
@@ -81,35 +82,38 @@ def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     assert eng.stats()["step"] == 25
 
 
-def test_run_c3_morris_heat(gpu, sph_amd):
+@pytest.mark.parametrize("path", [0, 2])
+def test_run_c3_morris_heat(gpu, sph_amd, path):
     s = c3_system(10)
     ph = po.c3_physics()
     ph.every = 5
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(12)
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(12)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     compare(eng, ref)
 
 
-def test_run_2d(gpu, sph_amd):
+@pytest.mark.parametrize("path", [0, 2])
+def test_run_2d(gpu, sph_amd, path):
     s = c2_system(30, dim=2)
     ph = po.c2_physics(2.5)
     ph.every = 4
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(9)
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(9)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     compare(eng, ref)
 
 
-def test_every_step_rebuild_and_nstep(gpu, sph_amd):
+@pytest.mark.parametrize("path", [0, 2])
+def test_every_step_rebuild_and_nstep(gpu, sph_amd, path):
     s = c2_system(9)
     ph = po.c2_physics()
     ph.every = 1
@@ -117,13 +121,14 @@ def test_every_step_rebuild_and_nstep(gpu, sph_amd):
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(7)
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(7)
     compare(eng, ref)
 
 
-def test_nonperiodic_box(gpu, sph_amd):
+@pytest.mark.parametrize("path", [0, 2])
+def test_nonperiodic_box(gpu, sph_amd, path):
     """No ghosts across non-periodic boundaries (sendneed = 0, comm_brick.cpp:226-274)."""
     s = c2_system(9)
     s.periodic = (1, 0, 1)
@@ -133,20 +138,21 @@ def test_nonperiodic_box(gpu, sph_amd):
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(3)
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(3)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     compare(eng, ref)
 
 
-def test_full_size_properties(gpu, sph_amd):
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_size_properties(gpu, sph_amd, path):
     """BASELINE C2 size (1M particles): size-independent checks -- total neighbor count
     equals the oracle's full_bin count, momentum is conserved by the pair forces
     (sum f = 0 up to roundoff), density is positive and near rho0."""
     s = c2_system(100)
     ph = po.c2_physics()
-    eng = engine_for(sph_amd, s, ph)
+    eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     nc = eng.neighbor_counts()
     cns, cmax = po.cutneighsq(1, ph.cutmax(1), ph.skin)

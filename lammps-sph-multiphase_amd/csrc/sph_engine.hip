@@ -55,6 +55,12 @@ static int neigh_q() {
   static int v = env_int("SPH_NEIGH", 2);
   return v == 1 ? 0 : v;
 }
+// SPH_NEIGH3 (default 1): the half-size-bin builder walks its candidates as one flat
+// range (k_neigh3) instead of bin-row by bin-row (k_neigh2); same list
+static bool neigh3() {
+  static bool v = env_int("SPH_NEIGH3", 1) != 0;
+  return v;
+}
 static int row_gen() {
   static int g = env_int("SPH_ROWK", 2);
   return g;
@@ -244,16 +250,27 @@ struct sph_engine {
                       bn.nb[2] <= 1024;
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p,
                        bidx.p, mort ? 1 : 0);
+    // key bits: 3 x (bits of the largest bin dimension) for Morton codes, else bits(nbins)
+    int kb = 1;
+    if (mort) {
+      const int mx3 = std::max(bn.nb[0], std::max(bn.nb[1], bn.nb[2]));
+      while ((1 << kb) < mx3) kb++;
+      kb *= 3;
+    } else {
+      while ((1u << kb) < (unsigned)nbins && kb < 32) kb++;
+    }
     size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, kb, s));
     tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, 32, s));
-    xf2.reserve(xf.cap);
-    vr2.reserve(vr.cap);
-    en2.reserve(en.cap);
-    ty2.reserve(ty.cap);
-    vel2.reserve(vel.cap);
-    tag2.reserve(tag.cap);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, kb, s));
+    // twins of equal capacity: the swaps below then never reallocate (a growing twin would
+    // cost a hipMalloc + a synchronising hipFree at every rebuild)
+    xf2.reserve_exact(xf.cap);
+    vr2.reserve_exact(vr.cap);
+    en2.reserve_exact(en.cap);
+    ty2.reserve_exact(ty.cap);
+    vel2.reserve_exact(vel.cap);
+    tag2.reserve_exact(tag.cap);
     hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, xf.p, vr.p,
                        en.p, ty.p, vel.p, tag.p, xf2.p, vr2.p, en2.p, ty2.p, vel2.p, tag2.p);
     std::swap(xf, xf2);
@@ -689,6 +706,17 @@ struct sph_engine {
                      ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? nbr.p : (int *)nullptr, stride, mx.p)
+      if (q2 && neigh3()) {
+#define SPH_N3(F, T)                                                                           \
+  hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xf.p, ty.p,   \
+                     xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
+                     (F && stride == 0) ? off.p : (const int *)nullptr,                        \
+                     F ? nbr.p : (int *)nullptr, stride, mx.p)
+        if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
+        else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
+#undef SPH_N3
+        return;
+      }
       if (fill) {
         if (q2) { if (t) SPH_NQ(true, true, 2, true); else SPH_NQ(true, false, 2, true); }
         else { if (t) SPH_NQ(true, true, 1, false); else SPH_NQ(true, false, 1, false); }

@@ -494,6 +494,120 @@ k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   }
 }
 
+// ---- full-list build v3: flattened candidate ranges ---------------------------------------
+// Same half-size bins (reach 2), per-row trimming, membership and entry ORDER as k_neigh2,
+// but restructured for latency: k_neigh2 walks its <= 25 (dz, dy) bin-rows one after the
+// other, each paying a dependent bin-start load and then its candidate loads.  Here the
+// row's G lanes first resolve all bin-row ranges at once (independent loads, into LDS),
+// then walk the concatenated candidates as ONE flat range in chunks of G*U -- each chunk
+// one round of independent record loads.  Hits are compacted in candidate order, so the
+// list is identical to k_neigh2's.  Modes as k_neigh2 (count | CSR fill | strided fill).
+template <int G, int U, bool FILL, bool NT1>
+__global__ void __launch_bounds__(256)
+k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
+         const int *__restrict__ ty, const double4 *__restrict__ xb,
+         const int *__restrict__ tb, const int *__restrict__ beg,
+         const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
+         int *__restrict__ nbr, int stride, int *__restrict__ ovf) {
+  constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
+  __shared__ double s_cns[NT2];
+  __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
+  __shared__ int s_pre[GR][NB + 1];  // candidates before each bin-row (flat numbering)
+  const int nt1 = cf->ntypes + 1;
+  if (!NT1)
+    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
+  const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1), grp = threadIdx.x / G;
+  const bool live = i < nlocal;
+  const double4 xi = xf[live ? i : 0];
+  const int cx = bin_coord(xi.x, q.lo[0], q.inv[0], q.nb[0]);
+  const int cy = bin_coord(xi.y, q.lo[1], q.inv[1], q.nb[1]);
+  const int cz = bin_coord(xi.z, q.lo[2], q.inv[2], q.nb[2]);
+  const int nbr_rows = (dim == 3) ? NB : (2 * R + 1);
+  // 1) this lane's bin-rows br = lane + k*G, in k_neigh2's (bz, by) loop order
+#pragma unroll
+  for (int k = 0; k < KB; k++) {
+    const int br = lane + k * G;
+    if (br >= NB) break;
+    int start = 0, len = 0;
+    if (live && br < nbr_rows) {
+      const int bz = (dim == 3) ? cz - R + br / (2 * R + 1) : cz;
+      const int by = cy - R + br % (2 * R + 1);
+      if (bz >= 0 && bz < q.nb[2] && by >= 0 && by < q.nb[1]) {
+        const double gz = (dim == 3) ? slab_gap(xi.z, bz, cz, q.lo[2], q.size[2]) : 0.0;
+        const double gy = slab_gap(xi.y, by, cy, q.lo[1], q.size[1]);
+        const double d2 = gy * gy + gz * gz;
+        if (d2 <= q.cutmaxsq) {
+          const double ext = sqrt(q.cutmaxsq - d2) * (1.0 + 1e-9) + 1e-9 * q.size[0];
+          const int bx0 = bin_coord(xi.x - ext, q.lo[0], q.inv[0], q.nb[0]);
+          const int bx1 = bin_coord(xi.x + ext, q.lo[0], q.inv[0], q.nb[0]);
+          const int brow = (bz * q.nb[1] + by) * q.nb[0];
+          start = beg[brow + bx0];
+          len = beg[brow + bx1 + 1] - start;
+        }
+      }
+    }
+    s_rs[grp][br] = start;
+    s_pre[grp][br + 1] = len;
+  }
+  __syncthreads();
+  if (lane == 0) {  // serial prefix over the row's <= 25 bin-rows
+    int acc = 0;
+    s_pre[grp][0] = 0;
+    for (int br = 0; br < NB; br++) {
+      acc += s_pre[grp][br + 1];
+      s_pre[grp][br + 1] = acc;
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const int T = s_pre[grp][NB];
+  const double *crow = s_cns + (NT1 ? 0 : ty[i] * nt1);
+  const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
+  const double di = (double)i;
+  int n = 0;
+  int *const row = FILL ? nbr + (stride > 0 ? (size_t)i * stride : (size_t)off[i]) : nullptr;
+  const int cap = stride > 0 ? stride : 0x7fffffff;
+  int pos = 0;
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+  int ptr = 0;  // bin-row holding this lane's next candidate (monotone)
+  for (int p0 = 0; p0 < T; p0 += G * U) {  // group-uniform trip count
+    double4 xj[U];
+    int tj[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int pp = min(p0 + lane + u * G, T - 1);
+      while (pp >= s_pre[grp][ptr + 1]) ptr++;
+      const int p = s_rs[grp][ptr] + (pp - s_pre[grp][ptr]);
+      xj[u] = xb[p];
+      tj[u] = NT1 ? 1 : tb[p];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      const bool hit = (p0 + lane + u * G < T) && (xj[u].w != di) &&
+                       rsq <= (NT1 ? cns1 : crow[tj[u]]);
+      if (FILL) {
+        const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
+        const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
+        if (hit && qq < cap) row[qq] = (int)xj[u].w;
+        pos += __popcll(m);
+      } else {
+        n += hit ? 1 : 0;
+      }
+    }
+  }
+  if (!FILL) {
+    n = group_sum_i<G>(n);
+    if (lane == 0) cnt[i] = n;
+  } else if (stride > 0 && lane == 0) {
+    cnt[i] = pos;
+    if (pos > stride) atomicOr(ovf, 1);
+  }
+}
+
 static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__restrict__ off) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) off[i] = cnt[i];

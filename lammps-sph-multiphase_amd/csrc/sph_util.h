@@ -65,6 +65,16 @@ struct DBuf {
     p = q;
     cap = nc;
   }
+  // grow to exactly n (no headroom): scratch twins that are swapped with a buffer of
+  // capacity n keep equal capacities, so the swap never triggers a reallocation
+  void reserve_exact(size_t n) {
+    if (n <= cap) return;
+    T *q = nullptr;
+    SPH_HIP_TRY(hipMalloc(&q, n * sizeof(T)));
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = n;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;

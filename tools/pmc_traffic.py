@@ -9,7 +9,8 @@ import sys
 
 
 def family(name):
-    for k in ("k_row_force", "k_row_rhosum", "k_bin_force", "k_bin_rhosum", "k_force",
+    for k in ("k_row2_force", "k_row2_rhosum", "k_tile_force", "k_tile_rhosum", "k_row_force",
+              "k_row_rhosum", "k_bin_force", "k_bin_rhosum", "k_force",
               "k_rhosum", "k_neigh2", "k_neigh"):
         if k in name:
             return name.split("(")[0]

@@ -6,7 +6,7 @@
 # Usage: tools/pmc_traffic.sh OUTDIR [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-OUT=$1; shift
+OUT=$(realpath -m "$1"); shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp

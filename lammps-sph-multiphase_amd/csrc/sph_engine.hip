@@ -61,21 +61,34 @@ static bool neigh3() {
   static bool v = env_int("SPH_NEIGH3", 1) != 0;
   return v;
 }
+// SPH_MORTON_DIV (default 4, the fastest of 1/2/4/8 on C2 1M): cells per bin edge of the
+// owned atoms' Morton sort key
+static int morton_div() {
+  static int v = std::max(1, env_int("SPH_MORTON_DIV", 4));
+  return v;
+}
 static int row_gen() {
   static int g = env_int("SPH_ROWK", 2);
   return g;
 }
 static bool row_kernels() { return row_gen() != 0; }
-// SPH_LP (default 1): lane-pair gathers in the row2 kernels; SPH_IV (default 0): 16-B
-// index vectors (4 consecutive entries per lane -- fewer index loads, but adjacent lanes
-// then gather records 4 entries apart and share fewer cache lines: slower on C2 1M,
-// profiles/r01/sweep_row2.log); SPH_EXP: study variants (kernel_sweep)
+// SPH_LP (default 1): lane-pair gathers in the row2 kernels; SPH_IV (default 1): the
+// strided list is stored chunk-transposed so each lane's four indices of a chunk are one
+// 16-B load (sph_row2_kernels.h); SPH_EXP: study variants (kernel_sweep)
 static bool row2_lp() {
   static bool v = env_int("SPH_LP", 1) != 0;
   return v;
 }
+// SPH_TIGHT (default 0): with a strided list, the rhosum pass writes this step's in-cut
+// list (k_row2_rhosum TIGHT) and the force pass walks it instead of the full list.
+// Measured on C2 1M: taitwater 0.57 -> 0.46 ms but rhosum 0.31 -> 0.48 ms (the stores
+// count in vmcnt, so the loop waits for them with the prefetched indices) -> off.
+static bool tight_on() {
+  static bool v = env_int("SPH_TIGHT", 0) != 0;
+  return v;
+}
 static bool row2_iv() {
-  static bool v = env_int("SPH_IV", 0) != 0;
+  static bool v = env_int("SPH_IV", 1) != 0;
   return v;
 }
 static int row2_exp() {
@@ -157,6 +170,9 @@ struct sph_engine {
   int nbr_builds = 0, nbr_maxrow = 0;
   bool strided = false;    // list in fixed-stride rows (row i at i*list_stride, ccnt[i])
   int list_stride = 0;
+  int list_perm_g = 0;     // strided rows stored chunk-transposed for G-lane rows (tpos)
+  // this step's in-cut ("tight") list, written by the rhosum pass for the force pass
+  DBuf<int> tnbr, tcnt;
   // LDS-tiled path: bin-sorted ghost index list and its inverse
   bool tiled = false;
   DBuf<int> gidx, gpos;
@@ -246,14 +262,25 @@ struct sph_engine {
     bidx.reserve(n);
     bidx2.reserve(n);
     // Morton order unless the staged path needs linear bins (and bins fit 10 bits/axis)
-    const bool mort = !want_staged() && !want_tiles() && bn.nb[0] <= 1024 && bn.nb[1] <= 1024 &&
-                      bn.nb[2] <= 1024;
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, bn, xf.p, bkey.p,
+    // Morton codes over cells of 1/div of a bin per axis (finer order inside a bin: a row's
+    // neighbors and the rows of one wave then occupy fewer, longer index runs, so the pair
+    // passes' gathers share more cache lines)
+    const int div = morton_div();
+    Bins kbn = bn;
+    for (int k = 0; k < 3; k++)
+      if (bn.nb[k] > 1) {
+        kbn.nb[k] = bn.nb[k] * div;
+        kbn.inv[k] = bn.inv[k] * div;
+      }
+    const bool mort = !want_staged() && !want_tiles() && kbn.nb[0] <= 1024 &&
+                      kbn.nb[1] <= 1024 && kbn.nb[2] <= 1024;
+    if (!mort) kbn = bn;
+    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, kbn, xf.p, bkey.p,
                        bidx.p, mort ? 1 : 0);
-    // key bits: 3 x (bits of the largest bin dimension) for Morton codes, else bits(nbins)
+    // key bits: 3 x (bits of the largest cell dimension) for Morton codes, else bits(nbins)
     int kb = 1;
     if (mort) {
-      const int mx3 = std::max(bn.nb[0], std::max(bn.nb[1], bn.nb[2]));
+      const int mx3 = std::max(kbn.nb[0], std::max(kbn.nb[1], kbn.nb[2]));
       while ((1 << kb) < mx3) kb++;
       kb *= 3;
     } else {
@@ -711,7 +738,7 @@ struct sph_engine {
   hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xf.p, ty.p,   \
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
-                     F ? nbr.p : (int *)nullptr, stride, mx.p)
+                     F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0)
         if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
         else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
@@ -730,6 +757,8 @@ struct sph_engine {
     // single pass into fixed-stride rows when a previous build sized them and nothing
     // needs the CSR form (the setup half list, the tile/staged paths, row kernels gen < 2)
     if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
+      // rows stored chunk-transposed for the row2 kernels' 16-B index loads (k_neigh3 only)
+      list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3()) ? row2_iv_g() : 0;
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -760,8 +789,9 @@ struct sph_engine {
     SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
     nbr.reserve(tot > 0 ? tot : 1);
     launch(true, 0);
-    // stride of later single-pass builds: this build's longest row + 25% + 16, 16-aligned
-    list_stride = ((hm[1] + hm[1] / 4 + 16) + 15) & ~15;
+    // stride of later single-pass builds: this build's longest row + 25% + 16, 64-aligned
+    // (whole chunks of the transposed layout, 16-B aligned rows)
+    list_stride = ((hm[1] + hm[1] / 4 + 16) + 63) & ~63;
     nbr_maxrow = hm[1];
     if (!staged) {
       nbr_total = tot;
@@ -1046,7 +1076,7 @@ struct sph_engine {
       b.rcnt = ccnt.p;
     }
     b.lp = row2_lp();
-    b.iv = row2_iv();
+    b.iv = strided && list_perm_g > 0 && list_perm_g == row2_iv_g();
     b.exp = row2_exp();
     return b;
   }
@@ -1056,6 +1086,7 @@ struct sph_engine {
 
   void pair_compute(bool do_rhosum, bool setup = false) {
     const int nall = nlocal + nghost;
+    bool tight = false;
     if (do_rhosum) {
       {
         Scope t(this, T_RHO);
@@ -1065,7 +1096,15 @@ struct sph_engine {
           launch_tile_rhosum();
         } else {
           if (use_row2()) {
-            row2_rhosum(nt1(), s, row2_args());
+            Row2Args b = row2_args();
+            if (strided && row2_lp() && tight_on() && force_mode && !setup) {
+              tnbr.reserve((size_t)list_span());
+              tcnt.reserve(nlocal > 0 ? nlocal : 1);
+              b.tnbr = tnbr.p;
+              b.tcnt = tcnt.p;
+              tight = true;
+            }
+            row2_rhosum(nt1(), s, b);
           } else if (row_kernels()) {
             row_rhosum(nt1(), s, row_args());
           } else {
@@ -1095,7 +1134,13 @@ struct sph_engine {
       launch_tile_force();
     } else if (force_mode && use_row2()) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      row2_force(nt1(), cfg.tait_visc, force_mode, s, row2_args());
+      Row2Args b = row2_args();
+      if (tight) {  // this step's in-cut list from the rhosum pass (same strided rows)
+        b.a.nbr = tnbr.p;
+        b.rcnt = tcnt.p;
+        b.iv = false;
+      }
+      row2_force(nt1(), cfg.tait_visc, force_mode, s, b);
     } else if (force_mode && row_kernels()) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       row_force(nt1(), cfg.tait_visc, force_mode, s, row_args());
@@ -1287,6 +1332,9 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     for (int i = 1; i <= nt; i++)
       for (int j = 1; j < i; j++) cutmax[i * (nt + 1) + j] = cutmax[j * (nt + 1) + i];
     e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin);
+    for (int k = 0; k < NT2; k++)  // tight-list test: the largest force-style cutoff
+      c.fcutsq[k] = std::max((e->force_mode & M_TAIT) ? c.tait[k].cutsq : 0.0,
+                             (e->force_mode & M_HEAT) ? c.heat[k].cutsq : 0.0);
     SPH_REQUIRE(e->cutneighmax > 0.0, SPH_HIP_EINVAL, "no pair style enabled / zero cutoff");
     e->cutghost = e->cutneighmax;  // CommBrick::setup: cutghost = cutneighmax (:166)
     if (pgn > 1) {
@@ -1381,6 +1429,8 @@ int sph_engine_destroy(sph_engine *e) {
   e->boff.release();
   e->gidx.release();
   e->gpos.release();
+  e->tnbr.release();
+  e->tcnt.release();
   e->nbr32.release();
   e->nbr16.release();
   if (e->dc) (void)hipFree(e->dc);

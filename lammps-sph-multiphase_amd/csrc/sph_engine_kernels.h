@@ -501,14 +501,15 @@ k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
 // row's G lanes first resolve all bin-row ranges at once (independent loads, into LDS),
 // then walk the concatenated candidates as ONE flat range in chunks of G*U -- each chunk
 // one round of independent record loads.  Hits are compacted in candidate order, so the
-// list is identical to k_neigh2's.  Modes as k_neigh2 (count | CSR fill | strided fill).
+// list is identical to k_neigh2's.  Modes as k_neigh2 (count | CSR fill | strided fill);
+// perm_g > 0 stores a strided row chunk-transposed (tpos, stride a multiple of 4*perm_g).
 template <int G, int U, bool FILL, bool NT1>
 __global__ void __launch_bounds__(256)
 k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
          const int *__restrict__ tb, const int *__restrict__ beg,
          const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-         int *__restrict__ nbr, int stride, int *__restrict__ ovf) {
+         int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g) {
   constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
   __shared__ double s_cns[NT2];
   __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
@@ -592,7 +593,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
-        if (hit && qq < cap) row[qq] = (int)xj[u].w;
+        if (hit && qq < cap) row[perm_g > 0 ? tpos(qq, perm_g) : qq] = (int)xj[u].w;
         pos += __popcll(m);
       } else {
         n += hit ? 1 : 0;

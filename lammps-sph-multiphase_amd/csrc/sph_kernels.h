@@ -49,6 +49,7 @@ struct Coefs {
   TaitPair tait[NT2];
   HeatPair heat[NT2];
   double cutneighsq[NT2];
+  double fcutsq[NT2];  // engine: max cutsq of the enabled force styles (tight-list test)
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, dispatch): give
@@ -58,6 +59,14 @@ __device__ __forceinline__ unsigned xcd_block() {
   const unsigned nwg = gridDim.x, orig = blockIdx.x;
   const unsigned q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// Storage position of entry q of a neighbor row in the chunk-transposed layout of the
+// strided engine list (chunks of 4G entries; entry u*G + l of a chunk at 4l + u), so the
+// row2 kernels' lane l loads its four strided entries of a chunk with one 16-B load.
+__host__ __device__ __forceinline__ int tpos(int q, int G) {
+  const int c = q % (4 * G);
+  return q - c + 4 * (c % G) + c / G;
 }
 
 template <int G>

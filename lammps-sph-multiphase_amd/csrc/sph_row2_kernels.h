@@ -13,9 +13,12 @@
 //  * LP (lane-pair gathers): the two lanes of an adjacent pair fetch each other's
 //    32-B records cooperatively -- each 16-B load then touches one record per lane PAIR
 //    -- and swap halves with a DPP quad permute (~24 extra 32-bit VALU ops per pair);
-//  * IV (index vectors, off by default): a lane's U = 4 entries consecutive and one
-//    16-B index load -- fewer index loads, but adjacent lanes then gather records four
-//    entries apart and share fewer lines (measured slower);
+//  * IV (index vectors): with a list stored chunk-transposed by the builder (entry
+//    c*4G + u*G + l at c*4G + 4l + u, k_neigh3's `perm`), lane l's four entries of a
+//    chunk are one 16-B load while the lane -> entry mapping (and so the line sharing
+//    of the record gathers) stays strided; a quarter of the index loads.  (Giving a
+//    lane four CONSECUTIVE entries instead was slower: adjacent lanes then gather
+//    records four entries apart and share fewer lines.)
 //  * buffer loads with 32-bit byte offsets: one shift per neighbor instead of a 64-bit
 //    address per array, hardware range check instead of clamped indices (an index slot
 //    past the row end reads the next row's entry or 0 -- a valid atom -- and is masked
@@ -113,8 +116,8 @@ __device__ __forceinline__ unsigned nbytes(int n) {
 }
 
 // A lane's U neighbor indices of the chunk starting at list entry k0 (row entries
-// [beg, end)): IV -> entries k0 + U*lane + u (one 16-B load when U = 4), else the
-// strided entries k0 + lane + u*G.  pos[u] = the entry number (masking: pos < end).
+// [beg, end)): entries k0 + lane + u*G -- with IV from a chunk-transposed list, where
+// they sit contiguously at k0 + 4*lane (one 16-B load; U = 4; k0 16-B aligned).
 template <int G, int U, bool IV>
 __device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int (&j)[U]) {
   if (IV) {
@@ -131,20 +134,32 @@ __device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int (&j)[U]
 }
 template <int G, int U, bool IV>
 __device__ __forceinline__ int chunk_pos(int k0, int lane, int u) {
-  return IV ? k0 + U * lane + u : k0 + lane + u * G;
+  return k0 + lane + u * G;
 }
 
-template <int G, int U, bool NT1, bool LP, bool IV>
+// TIGHT (strided list, LP): also write this step's in-cut neighbors -- rsq inside the
+// force styles' cutoff (fcutsq), the only pairs the force pass can use, positions being
+// fixed between the two passes -- as a compacted "tight" list: row rr at tnbr + rr*stride,
+// tcnt[rr] entries.  The group compacts its hits through LDS and stores them 16 B at a
+// time (a quarter of the store instructions of per-lane 4-B stores, which cost the TA as
+// much as gathers); the force pass then walks ~25% fewer chunks.
+template <int G, int U, bool NT1, bool LP, bool IV, bool TIGHT>
 __global__ void __launch_bounds__(256)
 k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride,
               const int *__restrict__ rcnt,
               const int *__restrict__ nbr, double4 *__restrict__ xf,
               const int *__restrict__ ty, double4 *__restrict__ vr,
-              const Coefs *__restrict__ cf) {
+              const Coefs *__restrict__ cf, int *__restrict__ tnbr, int *__restrict__ tcnt) {
+  static_assert(!TIGHT || LP, "the tight-list compaction needs wave-uniform trip counts");
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
+  __shared__ double s_fc[(NT1 || !TIGHT) ? 1 : NT2];
+  __shared__ __attribute__((aligned(16))) int s_tq[TIGHT ? 256 / G : 1][TIGHT ? 64 : 4];
   const int nt1 = cf->ntypes + 1;
   if (!NT1) {
-    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_c[t] = cf->rho[t];
+    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) {
+      s_c[t] = cf->rho[t];
+      if (TIGHT) s_fc[t] = cf->fcutsq[t];
+    }
     __syncthreads();
   }
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
@@ -163,6 +178,12 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
   // stride > 0: fixed-stride rows (row rr at rr*stride, rcnt[rr] entries), else CSR
   const int beg = stride > 0 ? rr * stride : off[rr];
   const int end = live ? (stride > 0 ? beg + rcnt[rr] : off[rr + 1]) : beg;
+  const double fc1 = (NT1 && TIGHT) ? cf->fcutsq[3] : 0.0;
+  const int gq = threadIdx.x / G, gbase = (threadIdx.x & 63) & ~(G - 1);
+  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  int *const trow = TIGHT ? tnbr + (size_t)rr * stride : nullptr;
+  int tq = 0, tw = 0;  // tight entries buffered in LDS / already stored (group-uniform)
   double acc = 0.0;
   int jn[U];
   chunk_idx<G, U, IV>(rn, beg, lane, jn);
@@ -170,9 +191,10 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
                         : chunk_pos<G, U, IV>(k0, lane, 0) < end;
        k0 += G * U) {
     double3 xj[U];
-    int tj[U];
+    int tj[U], jc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
+      jc[u] = jn[u];
       if (LP) {
         const unsigned jo = swap1((unsigned)jn[u]);
         const unsigned ja = odd ? jo : (unsigned)jn[u], jb = odd ? (unsigned)jn[u] : jo;
@@ -192,10 +214,33 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
       double wf = 1.0 - rsq * c.ihsq;
       wf = wf * wf;
       wf = wf * wf;
-      acc += (chunk_pos<G, U, IV>(k0, lane, u) < end && rsq < c.cutsq) ? c.mK * wf : 0.0;
+      const bool in = chunk_pos<G, U, IV>(k0, lane, u) < end;
+      acc += (in && rsq < c.cutsq) ? c.mK * wf : 0.0;
+      if (TIGHT) {
+        const bool hit = in && rsq < (NT1 ? fc1 : s_fc[it * nt1 + tj[u]]);
+        const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
+        if (hit) s_tq[gq][tq + __popcll(m & below)] = jc[u];
+        tq += __popcll(m);
+      }
+    }
+    if (TIGHT) {  // store the complete 16-B groups, keep the remainder (< 4) buffered
+      // (a group's lanes are one wave: its LDS accesses complete in program order, and
+      // the compiler keeps may-aliasing LDS accesses in order, so no barrier is needed)
+      const int nfull = tq & ~3, rem = tq - nfull;
+      for (int k = lane; 4 * k < nfull; k += G)
+        *reinterpret_cast<int4 *>(trow + tw + 4 * k) = *reinterpret_cast<const int4 *>(&s_tq[gq][4 * k]);
+      const int carry = lane < rem ? s_tq[gq][nfull + lane] : 0;
+      if (lane < rem) s_tq[gq][lane] = carry;
+      tw += nfull;
+      tq = rem;
     }
   }
   acc = group_sum<G>(acc);
+  if (TIGHT && live && lane == 0) {
+    if (tq > 0)
+      *reinterpret_cast<int4 *>(trow + tw) = *reinterpret_cast<const int4 *>(&s_tq[gq][0]);
+    tcnt[row] = tw + tq;
+  }
   if (lane == 0 && live) {
     const double rho = cf->self_rho[it] + acc;
     vr[row].w = rho;
@@ -353,6 +398,7 @@ struct Row2Args {
   int exp;   // study variants (SPH_EXP), 0 in production
   int stride = 0;                 // > 0: fixed-stride rows with counts rcnt (else a.off CSR)
   const int *rcnt = nullptr;
+  int *tnbr = nullptr, *tcnt = nullptr;  // rhosum: write the tight list here (strided, LP)
 };
 
 // 32-bit byte offsets of every array the row2 kernels read
@@ -360,17 +406,24 @@ inline bool row2_fits(long nall, long ntot) {
   return ntot * 4L < 0x7fffffffL && nall * 32L < 0x7fffffffL;
 }
 
-template <int G, int U, bool LP, bool IV>
-inline void row2_rhosum_k(bool nt1, hipStream_t s, const Row2Args &b) {
+template <int G, int U, bool LP, bool IV, bool TIGHT>
+inline void row2_rhosum_kt(bool nt1, hipStream_t s, const Row2Args &b) {
   const RowArgs &a = b.a;
   const int grid = (int)(((long long)a.n * G + 255) / 256);
   if (grid == 0) return;
   if (nt1)
-    hipLaunchKernelGGL((k_row2_rhosum<G, U, true, LP, IV>), dim3(grid), dim3(256), 0, s, a.n,
-                       b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr, a.cf);
+    hipLaunchKernelGGL((k_row2_rhosum<G, U, true, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
+                       a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
+                       a.cf, b.tnbr, b.tcnt);
   else
-    hipLaunchKernelGGL((k_row2_rhosum<G, U, false, LP, IV>), dim3(grid), dim3(256), 0, s, a.n,
-                       b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr, a.cf);
+    hipLaunchKernelGGL((k_row2_rhosum<G, U, false, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
+                       a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
+                       a.cf, b.tnbr, b.tcnt);
+}
+template <int G, int U, bool LP, bool IV>
+inline void row2_rhosum_k(bool nt1, hipStream_t s, const Row2Args &b) {
+  if (LP && b.tnbr) row2_rhosum_kt<G, U, LP, IV, LP>(nt1, s, b);
+  else row2_rhosum_kt<G, U, LP, IV, false>(nt1, s, b);
 }
 
 template <int G, int U>
@@ -435,6 +488,18 @@ inline void row2_force_gu(bool nt1, int visc, int mode, hipStream_t s, const Row
 #define SPH_ROW2_TILES(X) X(0, 16, 2) X(1, 8, 2) X(2, 16, 4) X(3, 8, 4) X(4, 4, 4)
 
 int row2_tile();
+
+// lanes per row of the selected shape when it can walk a chunk-transposed list (U = 4),
+// else 0
+inline int row2_iv_g() {
+  switch (row2_tile()) {
+#define SPH_CASE(k, G, U) \
+  case k: return U == 4 ? G : 0;
+    SPH_ROW2_TILES(SPH_CASE)
+#undef SPH_CASE
+    default: return 8;
+  }
+}
 
 inline void row2_rhosum(bool nt1, hipStream_t s, const Row2Args &b) {
   switch (row2_tile()) {

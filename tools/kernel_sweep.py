@@ -19,7 +19,7 @@ def main():
     eng = sph.Engine(cfg)
     eng.set_atoms(x, v, t, rho, e, cv)
     eng.setup()
-    eng.run(5)
+    eng.run(12)                 # past the first rebuild: the steady-state (strided) list
     eng.pair_passes(3)
     eng.sync()
     eng.set_timing(True)

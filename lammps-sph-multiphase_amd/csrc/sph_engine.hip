@@ -19,6 +19,7 @@
 #include "sph_comm.h"
 #include "sph_dispatch.h"
 #include "sph_bin_kernels.h"
+#include "sph_cluster_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_row_kernels.h"
 #include "sph_row2_kernels.h"
@@ -67,6 +68,16 @@ static int morton_div() {
   static int v = std::max(1, env_int("SPH_MORTON_DIV", 4));
   return v;
 }
+// SPH_CLX: study variants of the cluster passes (ClArgs::exp); 0 in production
+// SPH_CLUSTER (default 4): atoms per cluster of the cluster-pair paths (4 or 8)
+static int cl_size() {
+  static int v = env_int("SPH_CLUSTER", 4) == 8 ? 8 : 4;
+  return v;
+}
+static int cl_exp() {
+  static int v = env_int("SPH_CLX", 0);
+  return v;
+}
 static int row_gen() {
   static int g = env_int("SPH_ROWK", 2);
   return g;
@@ -85,6 +96,12 @@ static bool row2_lp() {
 // count in vmcnt, so the loop waits for them with the prefetched indices) -> off.
 static bool tight_on() {
   static bool v = env_int("SPH_TIGHT", 0) != 0;
+  return v;
+}
+// SPH_PI (default 0): pair-interleaved entry slots with lane-pair gathers (entry_slot).
+// Measured on C2 1M: taitwater 0.562 (off) vs 0.567 ms (on), rhosum equal -> off.
+static bool row2_pi() {
+  static bool v = env_int("SPH_PI", 0) != 0 && row2_lp();
   return v;
 }
 static bool row2_iv() {
@@ -171,8 +188,16 @@ struct sph_engine {
   bool strided = false;    // list in fixed-stride rows (row i at i*list_stride, ccnt[i])
   int list_stride = 0;
   int list_perm_g = 0;     // strided rows stored chunk-transposed for G-lane rows (tpos)
+  int list_perm_pi = 0;    // ... with pair-interleaved entry slots
   // this step's in-cut ("tight") list, written by the rhosum pass for the force pass
   DBuf<int> tnbr, tcnt;
+  // cluster-pair path (kernel_path 3): rows of CL_CI consecutive owned atoms, fixed
+  // stride cl_stride, counts ccl; rhosum accumulator racc
+  bool clustered = false;
+  DBuf<int> cnbr, ccl;
+  DBuf<double> racc;
+  int cl_stride = 0, cl_maxrow = 0;
+  bool full_counts = false;  // ccnt holds this build's full-list row counts
   // LDS-tiled path: bin-sorted ghost index list and its inverse
   bool tiled = false;
   DBuf<int> gidx, gpos;
@@ -312,6 +337,13 @@ struct sph_engine {
 
   bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2 && !multi(); }
   bool want_tiles() const { return cfg.kernel_path == 2; }
+  // cluster-pair path: kernel_path 3 = full cluster lists (gather only), 4 = half lists
+  // (Newton-3 updates by atomics); SPH_CLUSTER = atoms per cluster (4 or 8)
+  bool want_clusters() const {
+    return (cfg.kernel_path == 3 || cfg.kernel_path == 4) && neigh_q() == 2;
+  }
+  bool cl_half() const { return cfg.kernel_path == 4; }
+  int cl_ci() const { return cl_size(); }
 
   // order the ghost segment by bin too (the staged ranges need it contiguous)
   void sort_ghosts() {
@@ -693,8 +725,13 @@ struct sph_engine {
   // Full list over half-size bins and a bin-ordered copy of all atoms: CSR (count pass,
   // scan, fill pass) or, when `csr` is false and an earlier build sized the rows, one
   // fill pass into fixed-stride rows (ccnt = row counts; `strided` records which).
-  void build_list_q(bool csr) {
-    const int n = nlocal, nall = nlocal + nghost;
+  void build_list_q(bool csr, bool rebin = true) {
+    if (rebin) bin_q();
+    list_q(csr);
+  }
+  // bin-ordered copy of all atoms over the half-size bins (xb, tb, qbeg)
+  void bin_q() {
+    const int nall = nlocal + nghost;
     Bins b;
     for (int k = 0; k < 3; k++) {
       b.lo[k] = qb.lo[k];
@@ -720,6 +757,12 @@ struct sph_engine {
                        0, bkey2.p, qbeg.p);
     hipLaunchKernelGGL(k_bin_copy, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bidx2.p, xf.p,
                        ty.p, xb.p, tb.p);
+  }
+  // xi: positions of the owned rows (default: the current ones, as binned by bin_q)
+  void list_q(bool csr, const double4 *xi = nullptr) {
+    const int n = nlocal, nall = nlocal + nghost;
+    const double4 *const xi_src = xi ? xi : xf.p;
+    full_counts = true;
     ccnt.reserve(n + 1);
     off.reserve(n + 1);
     constexpr int G = 8, U = 2;
@@ -729,16 +772,17 @@ struct sph_engine {
       const bool t = nt1(), q2 = neigh_q() == 2;
       int *const cnt_out = (!fill || stride > 0) ? ccnt.p : (int *)nullptr;
 #define SPH_NQ(F, T, R, TR)                                                                  \
-  hipLaunchKernelGGL((k_neigh2<G, U, F, T, R, TR>), grid, block, 0, s, n, qb, cfg.dim, xf.p, \
+  hipLaunchKernelGGL((k_neigh2<G, U, F, T, R, TR>), grid, block, 0, s, n, qb, cfg.dim, xi_src, \
                      ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? nbr.p : (int *)nullptr, stride, mx.p)
       if (q2 && neigh3()) {
 #define SPH_N3(F, T)                                                                           \
-  hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xf.p, ty.p,   \
+  hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xi_src, ty.p, \
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
-                     F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0)
+                     F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,   \
+                     list_perm_pi)
         if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
         else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
@@ -759,6 +803,7 @@ struct sph_engine {
     if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
       // rows stored chunk-transposed for the row2 kernels' 16-B index loads (k_neigh3 only)
       list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3()) ? row2_iv_g() : 0;
+      list_perm_pi = row2_pi() ? 1 : 0;
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -797,6 +842,150 @@ struct sph_engine {
       nbr_total = tot;
       nbr_builds++;
     }
+  }
+
+  // Cluster-pair list (sph_cluster_kernels.h) over the half-size bins: one pass into
+  // fixed-stride rows when an earlier build sized them (and no row overflows), else a
+  // count pass sizes the rows first.  False if the list would not fit 32-bit offsets.
+  template <int CI, bool HALF>
+  void cl_neigh_launch(int *nbrp, int stride) {
+    const int nc = (nlocal + CI - 1) / CI;
+    const dim3 grid((nc + 3) / 4), block(256);
+    if (nt1())
+      hipLaunchKernelGGL((k_cl_neigh<CI, HALF, true>), grid, block, 0, s, nlocal, qb, cfg.dim,
+                         xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, ccl.p, nbrp, stride, mx.p);
+    else
+      hipLaunchKernelGGL((k_cl_neigh<CI, HALF, false>), grid, block, 0, s, nlocal, qb, cfg.dim,
+                         xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, ccl.p, nbrp, stride, mx.p);
+  }
+  void cl_neigh(int *nbrp, int stride) {
+    const bool h = cl_half();
+    if (cl_ci() == 8) { if (h) cl_neigh_launch<8, true>(nbrp, stride); else cl_neigh_launch<8, false>(nbrp, stride); }
+    else { if (h) cl_neigh_launch<4, true>(nbrp, stride); else cl_neigh_launch<4, false>(nbrp, stride); }
+  }
+  int cl_count() const { return (nlocal + cl_ci() - 1) / cl_ci(); }
+  bool build_clusters() {
+    const int n = nlocal, nall = nlocal + nghost;
+    const int nc = cl_count();
+    ccl.reserve(nc + 1);
+    mx.reserve(4);
+    if (n == 0) return true;
+    for (int pass = 0; pass < 2; pass++) {
+      if (cl_stride > 0 && row2_fits((long)nall, (long)nc * cl_stride)) {
+        cnbr.reserve((size_t)nc * cl_stride);
+        SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
+        cl_neigh(cnbr.p, cl_stride);
+        if (read_scalar(mx.p) == 0) {
+          nbr_builds++;
+          return true;
+        }
+      }
+      cl_neigh(nullptr, 0);  // row counts only
+      size_t tb3 = 0;
+      SPH_HIP_TRY(hipcub::DeviceReduce::Max(nullptr, tb3, ccl.p, mx.p + 1, nc, s));
+      tmp_reserve(tb3);
+      SPH_HIP_TRY(hipcub::DeviceReduce::Max(tmp.p, tb3, ccl.p, mx.p + 1, nc, s));
+      cl_maxrow = read_scalar(mx.p + 1);
+      // longest row + 25% + 16 (a later build's rows may grow), whole 64-entry blocks
+      cl_stride = ((cl_maxrow + cl_maxrow / 4 + 16) + 63) & ~63;
+      if (!row2_fits((long)nall, (long)nc * cl_stride)) return false;
+    }
+    return false;
+  }
+  // the full list's row counts of the current build (stats, sph_engine_neighbor_counts):
+  // built on demand on the cluster path, which does not need the full list
+  // (the owned rows' positions as of the build are recovered from the binned copy xb)
+  void ensure_full_counts() {
+    if (full_counts || !clustered) return;
+    const int builds = nbr_builds, nall = nlocal + nghost;
+    DBuf<double4> xbuild;
+    xbuild.reserve(nall);
+    hipLaunchKernelGGL(k_unbin, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xb.p, xbuild.p);
+    list_q(true, xbuild.p);
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    xbuild.release();
+    nbr_builds = builds;
+  }
+  ClArgs cl_args() {
+    ClArgs a{};
+    a.n = nlocal;
+    a.nall = nlocal + nghost;
+    a.stride = cl_stride;
+    a.ntot = (int)((long)cl_count() * cl_stride);
+    a.cnt = ccl.p;
+    a.nbr = cnbr.p;
+    a.xf = xf.p;
+    a.vr = vr.p;
+    a.ty = ty.p;
+    a.en = en.p;
+    a.cf = dc;
+    a.fo = fo.p;
+    a.de = de.p;
+    a.racc = racc.p;
+    a.gx = cfg.gravity[0];
+    a.gy = cfg.gravity[1];
+    a.gz = cfg.gravity[2];
+    a.exp = cl_exp();
+    return a;
+  }
+  template <int CI, bool HALF>
+  void cl_rhosum_ci(const ClArgs &a) {
+    const dim3 grid((cl_count() + 3) / 4), block(256);
+    if (nt1()) hipLaunchKernelGGL((k_cl_rhosum<CI, HALF, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((k_cl_rhosum<CI, HALF, false>), grid, block, 0, s, a);
+  }
+  void cl_rhosum() {
+    const int n = nlocal;
+    if (n == 0) return;
+    const bool h = cl_half();
+    if (h) {
+      racc.reserve(n);
+      SPH_HIP_TRY(hipMemsetAsync(racc.p, 0, n * sizeof(double), s));
+    }
+    const ClArgs a = cl_args();
+    if (cl_ci() == 8) { if (h) cl_rhosum_ci<8, true>(a); else cl_rhosum_ci<8, false>(a); }
+    else { if (h) cl_rhosum_ci<4, true>(a); else cl_rhosum_ci<4, false>(a); }
+    if (h)
+      hipLaunchKernelGGL(k_cl_rho_final<true>, dim3(blocks(n)), dim3(BLK), 0, s, n, racc.p,
+                         ty.p, dc, xf.p, vr.p);
+  }
+  template <int CI, int V, int M>
+  void cl_force_t(const ClArgs &a) {
+    const dim3 grid((cl_count() + 3) / 4), block(256);
+    const bool h = cl_half();
+    if (nt1()) {
+      if (h) hipLaunchKernelGGL((k_cl_force<CI, V, M, true, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_cl_force<CI, V, M, true, false>), grid, block, 0, s, a);
+    } else {
+      if (h) hipLaunchKernelGGL((k_cl_force<CI, V, M, false, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((k_cl_force<CI, V, M, false, false>), grid, block, 0, s, a);
+    }
+  }
+  template <int CI>
+  void cl_force_ci(const ClArgs &a) {
+    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
+    switch (force_mode) {
+      case M_TAIT:
+        if (mor) cl_force_t<CI, 1, M_TAIT>(a);
+        else cl_force_t<CI, 0, M_TAIT>(a);
+        break;
+      case M_TAIT | M_HEAT:
+        if (mor) cl_force_t<CI, 1, M_TAIT | M_HEAT>(a);
+        else cl_force_t<CI, 0, M_TAIT | M_HEAT>(a);
+        break;
+      default: cl_force_t<CI, 0, M_HEAT>(a); break;
+    }
+  }
+  void cl_force() {
+    const int n = nlocal;
+    if (n == 0) return;
+    if (cl_half()) {
+      SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, n * sizeof(double4), s));
+      SPH_HIP_TRY(hipMemsetAsync(de.p, 0, n * sizeof(double), s));
+    }
+    const ClArgs a = cl_args();
+    if (cl_ci() == 8) cl_force_ci<8>(a);
+    else cl_force_ci<4>(a);
   }
 
   void build_bins() {
@@ -997,7 +1186,7 @@ struct sph_engine {
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
     if (multi()) exchange_multi();
     const bool st = want_staged();
-    if (st || cfg.sort || want_tiles()) sort_owned();
+    if (st || cfg.sort || want_tiles() || want_clusters()) sort_owned();
     borders();
     staged = false;
     tiled = false;
@@ -1005,7 +1194,13 @@ struct sph_engine {
       sort_ghosts();
       staged = build_staged();
     }
-    if (!staged || need_csr) {
+    clustered = false;
+    full_counts = false;
+    if (want_clusters()) {
+      bin_q();
+      clustered = build_clusters();
+      if (need_csr || !clustered) build_list_q(true, /*rebin=*/false);
+    } else if (!staged || need_csr) {
       if (neigh_q()) {
         build_list_q(need_csr || st || want_tiles() || row_gen() != 2);
       } else {
@@ -1076,7 +1271,9 @@ struct sph_engine {
       b.rcnt = ccnt.p;
     }
     b.lp = row2_lp();
-    b.iv = strided && list_perm_g > 0 && list_perm_g == row2_iv_g();
+    b.pi = row2_pi();
+    b.iv = strided && list_perm_g > 0 && list_perm_g == row2_iv_g() &&
+           list_perm_pi == (b.pi ? 1 : 0);
     b.exp = row2_exp();
     return b;
   }
@@ -1090,7 +1287,9 @@ struct sph_engine {
     if (do_rhosum) {
       {
         Scope t(this, T_RHO);
-        if (staged) {
+        if (clustered && !setup) {
+          cl_rhosum();
+        } else if (staged) {
           launch_bin_rhosum();
         } else if (tiled) {
           launch_tile_rhosum();
@@ -1126,6 +1325,9 @@ struct sph_engine {
     }
     if (force_mode && setup) {
       setup_forces_half();
+    } else if (force_mode && clustered) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      cl_force();
     } else if (force_mode && staged) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       launch_bin_force();
@@ -1570,6 +1772,7 @@ int sph_engine_neighbor_counts(sph_engine *e, int *numneigh) {
   SPH_HIP_TRY(hipSetDevice(e->device));
   const int n = e->nlocal;
   if (n == 0) return SPH_HIP_OK;
+  e->ensure_full_counts();
   std::vector<int> hc(n), ht(n);
   SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->staged ? e->cnt.p : e->ccnt.p, n * sizeof(int),
                              hipMemcpyDeviceToHost, e->s));
@@ -1588,10 +1791,11 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->step = e->step;
   st->nlocal = e->nlocal;
   st->nghost = e->nghost;
+  e->ensure_full_counts();
   st->nbr_full = e->list_entries();
   st->nbr_builds = e->nbr_builds;
   st->nbr_maxrow = e->nbr_maxrow;
-  st->staged = e->staged ? 1 : (e->tiled ? 2 : 0);
+  st->staged = e->staged ? 1 : (e->tiled ? 2 : (e->clustered ? 3 : 0));
   st->stage_max = e->stage_max;
   st->ms_rhosum = e->ms[T_RHO];
   st->ms_tait = e->ms[T_TAIT];

@@ -509,7 +509,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
          const int *__restrict__ tb, const int *__restrict__ beg,
          const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-         int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g) {
+         int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g, int perm_pi) {
   constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
   __shared__ double s_cns[NT2];
   __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
@@ -593,7 +593,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
-        if (hit && qq < cap) row[perm_g > 0 ? tpos(qq, perm_g) : qq] = (int)xj[u].w;
+        if (hit && qq < cap) row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] = (int)xj[u].w;
         pos += __popcll(m);
       } else {
         n += hit ? 1 : 0;
@@ -607,6 +607,14 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
     cnt[i] = pos;
     if (pos > stride) atomicOr(ovf, 1);
   }
+}
+
+// positions as binned (xb[p].w = atom index) back in atom order
+static __global__ void k_unbin(int n, const double4 *__restrict__ xb, double4 *__restrict__ xo) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const double4 v = xb[p];
+  xo[(int)v.w] = v;
 }
 
 static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__restrict__ off) {

@@ -61,12 +61,25 @@ __device__ __forceinline__ unsigned xcd_block() {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// Entry slot (0..G-1) of lane l in each G-entry group of a row2 chunk.  pi = 0: slot l.
+// pi = 1 (pair-interleaved, for lane-pair gathers): lane 2p takes slot p and lane 2p+1
+// slot G/2 + p, so the lane-pair load that fetches the even lanes' records covers the G/2
+// CONSECUTIVE entries 0..G/2-1 (mostly consecutive atoms: fewer distinct 128-B lines)
+// and the odd lanes' load the next G/2, instead of both striding over all G.
+template <int G>
+__host__ __device__ __forceinline__ int entry_slot(int l, int pi) {
+  return pi ? (l & 1) * (G / 2) + (l >> 1) : l;
+}
+__host__ __device__ __forceinline__ int slot_lane(int m, int G, int pi) {
+  return pi ? 2 * (m % (G / 2)) + m / (G / 2) : m;
+}
 // Storage position of entry q of a neighbor row in the chunk-transposed layout of the
-// strided engine list (chunks of 4G entries; entry u*G + l of a chunk at 4l + u), so the
-// row2 kernels' lane l loads its four strided entries of a chunk with one 16-B load.
-__host__ __device__ __forceinline__ int tpos(int q, int G) {
+// strided engine list (chunks of 4G entries; entry u*G + m of a chunk, taken by lane
+// l = slot_lane(m), at 4l + u), so the row2 kernels' lane l loads its four entries of a
+// chunk with one 16-B load.
+__host__ __device__ __forceinline__ int tpos(int q, int G, int pi) {
   const int c = q % (4 * G);
-  return q - c + 4 * (c % G) + c / G;
+  return q - c + 4 * slot_lane(c % G, G, pi) + c / G;
 }
 
 template <int G>

@@ -116,10 +116,11 @@ __device__ __forceinline__ unsigned nbytes(int n) {
 }
 
 // A lane's U neighbor indices of the chunk starting at list entry k0 (row entries
-// [beg, end)): entries k0 + lane + u*G -- with IV from a chunk-transposed list, where
-// they sit contiguously at k0 + 4*lane (one 16-B load; U = 4; k0 16-B aligned).
+// [beg, end)): entries k0 + el + u*G, el = the lane's entry slot (entry_slot) -- with IV
+// from a chunk-transposed list, where they sit contiguously at k0 + 4*lane (one 16-B
+// load; U = 4; k0 16-B aligned).
 template <int G, int U, bool IV>
-__device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int (&j)[U]) {
+__device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int el, int (&j)[U]) {
   if (IV) {
     static_assert(!IV || U == 4, "index vectors hold 4 entries");
     const v4u v = ld_b128(rn, (unsigned)(k0 + 4 * lane) * 4u);
@@ -129,12 +130,12 @@ __device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int (&j)[U]
     j[3] = (int)v.w;
   } else {
 #pragma unroll
-    for (int u = 0; u < U; u++) j[u] = ld_i32(rn, (unsigned)(k0 + lane + u * G) * 4u);
+    for (int u = 0; u < U; u++) j[u] = ld_i32(rn, (unsigned)(k0 + el + u * G) * 4u);
   }
 }
 template <int G, int U, bool IV>
-__device__ __forceinline__ int chunk_pos(int k0, int lane, int u) {
-  return k0 + lane + u * G;
+__device__ __forceinline__ int chunk_pos(int k0, int el, int u) {
+  return k0 + el + u * G;
 }
 
 // TIGHT (strided list, LP): also write this step's in-cut neighbors -- rsq inside the
@@ -149,7 +150,8 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
               const int *__restrict__ rcnt,
               const int *__restrict__ nbr, double4 *__restrict__ xf,
               const int *__restrict__ ty, double4 *__restrict__ vr,
-              const Coefs *__restrict__ cf, int *__restrict__ tnbr, int *__restrict__ tcnt) {
+              const Coefs *__restrict__ cf, int *__restrict__ tnbr, int *__restrict__ tcnt,
+              int pi) {
   static_assert(!TIGHT || LP, "the tight-list compaction needs wave-uniform trip counts");
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   __shared__ double s_fc[(NT1 || !TIGHT) ? 1 : NT2];
@@ -164,6 +166,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
   }
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
+  const int el = entry_slot<G>(lane, pi);
   // LP: lanes of rows past n stay in the loop (masked) so every DPP partner is active
   if (!LP && row >= n) return;
   const bool live = row < n;
@@ -186,9 +189,9 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
   int tq = 0, tw = 0;  // tight entries buffered in LDS / already stored (group-uniform)
   double acc = 0.0;
   int jn[U];
-  chunk_idx<G, U, IV>(rn, beg, lane, jn);
-  for (int k0 = beg; LP ? __any(chunk_pos<G, U, IV>(k0, lane, 0) < end)
-                        : chunk_pos<G, U, IV>(k0, lane, 0) < end;
+  chunk_idx<G, U, IV>(rn, beg, lane, el, jn);
+  for (int k0 = beg; LP ? __any(chunk_pos<G, U, IV>(k0, el, 0) < end)
+                        : chunk_pos<G, U, IV>(k0, el, 0) < end;
        k0 += G * U) {
     double3 xj[U];
     int tj[U], jc[U];
@@ -205,7 +208,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
       }
       tj[u] = NT1 ? 1 : ld_i32(rt, (unsigned)jn[u] * 4u);
     }
-    chunk_idx<G, U, IV>(rn, k0 + G * U, lane, jn);
+    chunk_idx<G, U, IV>(rn, k0 + G * U, lane, el, jn);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
@@ -214,7 +217,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
       double wf = 1.0 - rsq * c.ihsq;
       wf = wf * wf;
       wf = wf * wf;
-      const bool in = chunk_pos<G, U, IV>(k0, lane, u) < end;
+      const bool in = chunk_pos<G, U, IV>(k0, el, u) < end;
       acc += (in && rsq < c.cutsq) ? c.mK * wf : 0.0;
       if (TIGHT) {
         const bool hit = in && rsq < (NT1 ? fc1 : s_fc[it * nt1 + tj[u]]);
@@ -256,7 +259,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
              const double4 *__restrict__ vr, const int *__restrict__ ty,
              const double *__restrict__ en, const Coefs *__restrict__ cf,
              double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-             double gz) {
+             double gz, int pi) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   __shared__ TaitPair s_t[(TAIT && !NT1) ? NT2 : 1];
@@ -271,6 +274,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
   }
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
+  const int el = entry_slot<G>(lane, pi);
   if (!LP && row >= n) return;
   const bool live = row < n;
   const bool odd = (threadIdx.x & 1) != 0;
@@ -295,9 +299,9 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
   const int end = live ? (stride > 0 ? beg + rcnt[rr] : off[rr + 1]) : beg;
   double fx = 0.0, fy = 0.0, fz = 0.0, drho = 0.0, dE = 0.0;
   int jn[U];
-  chunk_idx<G, U, IV>(rn, beg, lane, jn);
-  for (int k0 = beg; LP ? __any(chunk_pos<G, U, IV>(k0, lane, 0) < end)
-                        : chunk_pos<G, U, IV>(k0, lane, 0) < end;
+  chunk_idx<G, U, IV>(rn, beg, lane, el, jn);
+  for (int k0 = beg; LP ? __any(chunk_pos<G, U, IV>(k0, el, 0) < end)
+                        : chunk_pos<G, U, IV>(k0, el, 0) < end;
        k0 += G * U) {
     double4 xj[U], vj[U];
     double ej[U];
@@ -321,7 +325,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
       ej[u] = HEAT ? ld_d1(re, o * 8u) : 0.0;
       tj[u] = NT1 ? 1 : ld_i32(rt, o * 4u);
     }
-    chunk_idx<G, U, IV>(rn, k0 + G * U, lane, jn);
+    chunk_idx<G, U, IV>(rn, k0 + G * U, lane, el, jn);
 #pragma unroll
     for (int u = 0; u < U; u++) {
       if (EXP == 1) {
@@ -334,13 +338,16 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
       const double rsq = dx * dx + dy * dy + dz * dz;
       const int pidx = NT1 ? 3 : it * nt1 + tj[u];
-      const bool ok = chunk_pos<G, U, IV>(k0, lane, u) < end;
+      const bool ok = chunk_pos<G, U, IV>(k0, el, u) < end;
       const double r = sqrt1(rsq);
       if (TAIT) {
         const TaitPair c = NT1 ? t1 : s_t[pidx];
+        // masked slots may hold any record (or zeros past the range check): wfd = 0
+        // zeroes every finite term below; the 1/(rho_i rho_j) terms are selected away
+        const bool hit = ok && rsq < c.cutsq;
         double wfd = c.h - r;
         wfd = c.wK * (wfd * wfd);
-        wfd = (ok && rsq < c.cutsq) ? wfd : 0.0;   // zeroes every term below
+        wfd = hit ? wfd : 0.0;
         const double velx = vi.x - vj[u].x, vely = vi.y - vj[u].y, velz = vi.z - vj[u].z;
         const double dvdr = dx * velx + dy * vely + dz * velz;
         if (VISC == SPH_VISC_MONAGHAN) {
@@ -353,7 +360,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
           dE += -0.5 * fpair * dvdr;
         } else {
           double fvisc = c.viscC * rcp1(vi.w * vj[u].w);
-          fvisc *= (-c.mm) * wfd;
+          fvisc = hit ? fvisc * ((-c.mm) * wfd) : 0.0;
           const double fpair = c.mm * (xi.w + xj[u].w) * wfd;
           fx += dx * fpair + velx * fvisc;
           fy += dy * fpair + vely * fvisc;
@@ -364,12 +371,13 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
       }
       if (HEAT) {
         const HeatPair c = NT1 ? h1 : s_h[pidx];
+        const bool hit = ok && rsq < c.cutsq;
         double wfd = c.h - r;
         wfd = c.wK * (wfd * wfd);
-        wfd = (ok && rsq < c.cutsq) ? wfd : 0.0;
+        wfd = hit ? wfd : 0.0;
         double deltaE = c.hmD;
         deltaE *= (vi.w + vj[u].w) * rcp1(vi.w * vj[u].w);
-        deltaE *= (ei - ej[u]) * wfd;
+        deltaE = hit ? deltaE * ((ei - ej[u]) * wfd) : 0.0;
         dE += deltaE;
       }
     }
@@ -395,6 +403,7 @@ struct Row2Args {
   int nall, ntot;
   bool lp;   // lane-pair gathers
   bool iv;   // index vectors
+  bool pi;   // pair-interleaved entry slots (entry_slot)
   int exp;   // study variants (SPH_EXP), 0 in production
   int stride = 0;                 // > 0: fixed-stride rows with counts rcnt (else a.off CSR)
   const int *rcnt = nullptr;
@@ -414,11 +423,11 @@ inline void row2_rhosum_kt(bool nt1, hipStream_t s, const Row2Args &b) {
   if (nt1)
     hipLaunchKernelGGL((k_row2_rhosum<G, U, true, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0);
   else
     hipLaunchKernelGGL((k_row2_rhosum<G, U, false, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0);
 }
 template <int G, int U, bool LP, bool IV>
 inline void row2_rhosum_k(bool nt1, hipStream_t s, const Row2Args &b) {
@@ -445,7 +454,7 @@ inline void row2_force_t(hipStream_t s, const Row2Args &b) {
   if (grid == 0) return;
   hipLaunchKernelGGL((k_row2_force<G, U, VISC, MODE, NT1, LP, IV, EXP>), dim3(grid), dim3(256),
                      0, s, a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.vr,
-                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz);
+                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz, b.pi ? 1 : 0);
 }
 
 template <int G, int U, bool NT1, bool LP, bool IV>

@@ -80,7 +80,16 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=1):
     for t in th:
         t.join(timeout=300)
     assert not any(t.is_alive() for t in th), "brick threads hung"
-    assert not errors, errors
+    try:
+        assert not errors, errors
+        return collect(engines, s)
+    finally:
+        for e in engines:
+            e.close()
+        world.close()
+
+
+def collect(engines, s):
     n = s.n
     out = {k: np.zeros((n, 3)) for k in ("x", "v", "f")}
     out.update({k: np.zeros(n) for k in ("rho", "e", "drho", "de")})
@@ -96,9 +105,6 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=1):
         counts[tags] = eng.neighbor_counts()
         nloc.append(eng.nlocal)
     assert (seen == 1).all(), "every atom owned by exactly one brick"
-    for e in engines:
-        e.close()
-    world.close()
     return out, counts, nloc
 
 
@@ -113,7 +119,8 @@ def compare(out, ref, tol=TOL):
 
 
 @pytest.mark.parametrize("pg,path", [((2, 1, 1), 1), ((1, 2, 2), 1), ((2, 2, 2), 1),
-                                     ((2, 1, 1), 2), ((2, 2, 2), 2)])
+                                     ((2, 1, 1), 2), ((2, 2, 2), 2), ((2, 1, 1), 3),
+                                     ((2, 2, 2), 3), ((1, 2, 2), 4)])
 def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     s = at_rest(c2_system(12))
     ph = po.c2_physics()
@@ -127,7 +134,7 @@ def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     compare(out, ref)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     s = at_rest(c3_system(12))
     ph = po.c3_physics()
@@ -141,7 +148,7 @@ def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     assert rel_err(out["e"], ref.s.e) < TOL
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_bricks_migration(gpu, sph_amd, path):
     """Pressure-driven motion from rest with a larger step: atoms of the lattice plane that
     sits on the brick face (x = 6) cross it between rebuilds and migrate."""
@@ -161,7 +168,7 @@ def test_bricks_migration(gpu, sph_amd, path):
     compare(out, ref)
 
 
-@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("path", [1, 2, 3])
 def test_bricks_2d(gpu, sph_amd, path):
     s = at_rest(c2_system(30, dim=2))
     ph = po.c2_physics(2.5)

@@ -147,6 +147,13 @@ int sph_hip_heatconduction_phasechange(sph_hip_ctx *ctx, double *de);
 int sph_hip_colorgradient_coeff(sph_hip_ctx *ctx, const double *alpha, const double *cut);
 int sph_hip_colorgradient(sph_hip_ctx *ctx, double *cg);
 
+/* PairSPHSurfaceTension (pair_sph_surfacetension.cpp:50-192, coeff :222-247): cut = h per
+   pair.  cg (nall*3, atom->colorgradient of owned atoms and ghosts) is read; f (nall*3) is
+   ACCUMULATED; HALF lists (the style's default request) scatter onto j when newton_pair or
+   j < nlocal, as the reference. */
+int sph_hip_surfacetension_coeff(sph_hip_ctx *ctx, const double *cut);
+int sph_hip_surfacetension(sph_hip_ctx *ctx, const double *cg, double *f);
+
 /* ======================================================================================
  * 1c. fix phase_change (FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-352)
  * ==================================================================================== */

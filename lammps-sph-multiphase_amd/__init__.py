@@ -102,6 +102,8 @@ EXPORTS = {
     "sph_hip_heatconduction_phasechange": (_i, [_vp, _dp]),
     "sph_hip_colorgradient_coeff": (_i, [_vp, _dp, _dp]),
     "sph_hip_colorgradient": (_i, [_vp, _dp]),
+    "sph_hip_surfacetension_coeff": (_i, [_vp, _dp]),
+    "sph_hip_surfacetension": (_i, [_vp, _dp, _dp]),
     "sph_hip_phasechange": (_i, [_vp, _vp, C.POINTER(_i), _dp, _dp, _dp, _dp, _i,
                                  C.POINTER(_i), _vp, _vp]),
     "sph_hip_phasechange_finish": (_i, [_i, _dp, _dp, _dp]),
@@ -294,6 +296,15 @@ class PairContext:
     def colorgradient(self, cg):
         _chk(self.L.sph_hip_colorgradient(self.h, cg))
         return cg
+
+    def surfacetension_coeff(self, cut):
+        _chk(self.L.sph_hip_surfacetension_coeff(self.h, self._t(cut)))
+
+    def surfacetension(self, cg, f):
+        """cg: (nall, 3) colorgradient of every atom; f (nall, 3) is accumulated."""
+        _chk(self.L.sph_hip_surfacetension(self.h, np.ascontiguousarray(cg, dtype=np.float64),
+                                           f))
+        return f
 
 
 # ------------------------------------------------------------------------------------------

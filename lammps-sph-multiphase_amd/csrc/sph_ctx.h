@@ -25,9 +25,11 @@ struct sph_hip_ctx {
   DBuf<int> ty, ilist, off, nbr;
   // multiphase styles (atom_style meso/multiphase): per-atom rmass and cv, own coefficients
   DBuf<double> rm, cv;
-  DBuf<double4> cg;
+  DBuf<double4> cg, cgin;
   bool have_mp_atoms = false;
   bool have_mp_rho = false, have_mp_tait = false, have_mp_heat = false, have_mp_cg = false;
+  bool have_mp_st = false;
+  std::vector<double4> h4in;
   MpCoefs hm{};
   MpCoefs *dm = nullptr;
   bool mp_dirty = true;

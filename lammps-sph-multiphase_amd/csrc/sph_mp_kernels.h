@@ -4,6 +4,7 @@
 //   sph/taitwater/multiphase       pair_sph_taitwater_multiphase.cpp:95-183    (half list)
 //   sph/heatconduction/phasechange pair_sph_heatconduction_phasechange.cpp:81-138 (half)
 //   sph/colorgradient              pair_sph_colorgradient.cpp:118-187          (full list)
+//   sph/surfacetension             pair_sph_surfacetension.cpp:50-192          (half list)
 // Same walk as sph_kernels.h: G lanes per list row, register accumulation, xor-shuffle
 // group reduction; half lists scatter the Newton-3 share onto j with fp64 atomics, as the
 // reference does.  The two half-list styles are NOT pair-symmetric in the reference
@@ -29,6 +30,8 @@ struct MpCoefs {
   int hfix[NT2];
   // colorgradient
   double calpha[NT2], ccut[NT2], ccutsq[NT2];
+  // surfacetension: h = cut[it][jt]
+  double scut[NT2], scutsq[NT2];
 };
 
 // Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r, pow() of the reference kept)
@@ -68,6 +71,7 @@ struct MpArgs {
   double4 *fo;    // taitwater out (nall, x y z used)
   double *de;     // heat out (nall)
   double4 *cg;    // colorgradient out (nall)
+  const double4 *cgi;  // surfacetension: colorgradient of every atom (nall, x y z used)
 };
 
 template <int G>
@@ -255,6 +259,92 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
   gy = group_sum<G>(gy);
   gz = group_sum<G>(gz);
   if (lane == 0) a.cg[i] = make_double4(gx, gy, gz, 0.0);
+}
+
+// Surface stress vector S = (|c|^2/ndim I - c c^T) e / |c| of colorgradient c along the
+// pair direction e (pair_sph_surfacetension.cpp:135-168; zero for |c| <= EPSILON = 1e-12,
+// :29), written term by term as the reference does.
+__device__ __forceinline__ double3 st_vector(int dim, double4 c, double absc, double3 e) {
+  if (!(absc > 1.0e-12)) return make_double3(0.0, 0.0, 0.0);
+  if (dim == 2)
+    return make_double3(
+        (e.x * ((c.y * c.y + c.x * c.x) / 2 - c.x * c.x) - c.x * e.y * c.y) / absc,
+        (e.y * ((c.y * c.y + c.x * c.x) / 2 - c.y * c.y) - e.x * c.x * c.y) / absc, 0.0);
+  return make_double3(
+      (e.x * (0.3333333333333333 * c.z * c.z + 0.3333333333333333 * c.y * c.y -
+              0.6666666666666666 * c.x * c.x) -
+       1.0 * c.x * e.z * c.z - 1.0 * c.x * e.y * c.y) / absc,
+      (e.y * (0.3333333333333333 * c.z * c.z - 0.6666666666666666 * c.y * c.y +
+              0.3333333333333333 * c.x * c.x) -
+       1.0 * c.y * e.z * c.z - 1.0 * e.x * c.x * c.y) / absc,
+      (e.z * (-0.6666666666666666 * c.z * c.z + 0.3333333333333333 * c.y * c.y +
+              0.3333333333333333 * c.x * c.x) -
+       1.0 * e.y * c.y * c.z - 1.0 * e.x * c.x * c.z) / absc);
+}
+__device__ __forceinline__ double st_abs(int dim, double4 c) {
+  return dim == 3 ? sqrt(c.x * c.x + c.y * c.y + c.z * c.z) : sqrt(c.x * c.x + c.y * c.y);
+}
+
+// sph/surfacetension: F = (S_i V_i^2 + S_j V_j^2) dW_quintic, V = rmass/rho; i gets +F, j
+// gets -F on a half list (newton_pair or j < nlocal), like the reference.
+template <int G>
+__global__ void __launch_bounds__(256) k_mp_surface(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int nt1 = c->ntypes + 1;
+  const int dim = a.dim;
+  const int i = a.ilist[row];
+  const double4 xi = a.xf[i];
+  const int it = a.ty[i];
+  const double4 cgi = a.cgi[i];
+  const double abscgi = st_abs(dim, cgi);
+  const double Vi = a.rm[i] / a.vr[i].w;
+  double fx = 0.0, fy = 0.0, fz = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int j = a.nbr[k];
+    const double4 xj = a.xf[j];
+    const int jt = a.ty[j];
+    const int p = it * nt1 + jt;
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (!(rsq < c->scutsq[p])) continue;
+    const double ih = 1.0 / c->scut[p];
+    const double r = sqrt(rsq);
+    const double wfd = (dim == 3) ? quintic_dw(3, r * ih) * ih * ih * ih * ih
+                                  : quintic_dw(2, r * ih) * ih * ih * ih;
+    const double3 e = make_double3(dx / r, dy / r, dim == 3 ? dz / r : 0.0);
+    const double4 cgj = a.cgi[j];
+    const double3 Si = st_vector(dim, cgi, abscgi, e);
+    const double3 Sj = st_vector(dim, cgj, st_abs(dim, cgj), e);
+    const double Vj = a.rm[j] / a.vr[j].w;
+    const double tx = (Si.x * Vi * Vi + Sj.x * Vj * Vj) * wfd;
+    const double ty_ = (Si.y * Vi * Vi + Sj.y * Vj * Vj) * wfd;
+    const double tz = dim == 3 ? (Si.z * Vi * Vi + Sj.z * Vj * Vj) * wfd : 0.0;
+    fx += tx;
+    fy += ty_;
+    fz += tz;
+    if (a.half && (a.newton || j < a.nlocal)) {
+      atomicAdd(&a.fo[j].x, -tx);
+      atomicAdd(&a.fo[j].y, -ty_);
+      if (dim == 3) atomicAdd(&a.fo[j].z, -tz);
+    }
+  }
+  fx = group_sum<G>(fx);
+  fy = group_sum<G>(fy);
+  fz = group_sum<G>(fz);
+  if (lane == 0) {
+    if (a.half) {
+      atomicAdd(&a.fo[i].x, fx);
+      atomicAdd(&a.fo[i].y, fy);
+      atomicAdd(&a.fo[i].z, fz);
+    } else {
+      a.fo[i].x += fx;
+      a.fo[i].y += fy;
+      a.fo[i].z += fz;
+    }
+  }
 }
 
 }  // namespace sph

@@ -1,6 +1,7 @@
 // sph_multiphase.hip -- multiphase styles of the pair-style layer (include/sph_hip.h,
 // section 1b): what PairSPHRhoSumMultiphase, PairSPHTaitwaterMultiphase,
-// PairSPHHeatConductionPhaseChange and PairSPHColorGradient call from compute().
+// PairSPHHeatConductionPhaseChange, PairSPHColorGradient and PairSPHSurfaceTension call
+// from compute().
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -230,6 +231,49 @@ int sph_hip_colorgradient(sph_hip_ctx *c, double *cg) {
     cg[3 * i + 1] = c->h4[i].y;
     cg[3 * i + 2] = c->h4[i].z;
   }
+  SPH_API_END
+}
+
+int sph_hip_surfacetension_coeff(sph_hip_ctx *c, const double *cut) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && cut, SPH_HIP_EINVAL, "sph_hip_surfacetension_coeff: NULL argument");
+  mirror(c->hm.scut, cut, c->ntypes);
+  for (int k = 0; k < NT2; k++) c->hm.scutsq[k] = c->hm.scut[k] * c->hm.scut[k];
+  c->have_mp_st = true;
+  c->mp_dirty = true;
+  SPH_API_END
+}
+
+int sph_hip_surfacetension(sph_hip_ctx *c, const double *cg, double *f) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && cg && f, SPH_HIP_EINVAL, "sph_hip_surfacetension: bad argument");
+  mp_ready(c, "sph_hip_surfacetension", c->have_mp_st);
+  const int nall = c->nlocal + c->nghost;
+  if (c->inum == 0 || nall == 0) return SPH_HIP_OK;
+  c->h4in.resize(nall);
+  for (int i = 0; i < nall; i++)
+    c->h4in[i] = make_double4(cg[3 * i], cg[3 * i + 1], cg[3 * i + 2], 0.0);
+  c->cgin.reserve(nall);
+  SPH_HIP_TRY(hipMemcpyAsync(c->cgin.p, c->h4in.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
+  c->fo.reserve(nall);
+  SPH_HIP_TRY(hipMemsetAsync(c->fo.p, 0, nall * sizeof(double4), c->stream));
+  MpArgs a = mp_args(c);
+  a.fo = c->fo.p;
+  a.cgi = c->cgin.p;
+  hipLaunchKernelGGL(k_mp_surface<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  SPH_HIP_TRY(hipGetLastError());
+  c->h4.resize(nall);
+  SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));
+  SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  auto add = [&](int i) {
+    f[3 * i] += c->h4[i].x;
+    f[3 * i + 1] += c->h4[i].y;
+    f[3 * i + 2] += c->h4[i].z;
+  };
+  if (a.half)
+    for (int i = 0; i < nall; i++) add(i);
+  else
+    for (int r = 0; r < c->inum; r++) add(c->hilist[r]);
   SPH_API_END
 }
 

@@ -27,7 +27,7 @@ SPH="atom_vec_meso.cpp atom_vec_meso_multiphase.cpp pair_sph_rhosum.cpp
      pair_sph_taitwater.cpp pair_sph_taitwater_morris.cpp pair_sph_heatconduction.cpp
      pair_sph_rhosum_multiphase.cpp pair_sph_taitwater_multiphase.cpp
      pair_sph_heatconduction_phasechange.cpp pair_sph_colorgradient.cpp
-     sph_kernel_quintic.cpp sph_energy_equation.cpp"
+     pair_sph_surfacetension.cpp sph_kernel_quintic.cpp sph_energy_equation.cpp"
 
 # the reference's own serial build: g++ -O3 at the compiler's default C++ dialect (src/MAKE/
 # Makefile.serial:9-10); the dialect matters -- under C++98 pow(double,int) is __builtin_powi

@@ -110,6 +110,8 @@ def lib():
                                                      _dp, _dp, _lp, _ip, _dp]
         L.orc_colorgradient.argtypes = [_i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp, _lp,
                                         _ip, _dp]
+        L.orc_surfacetension.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp, _dp,
+                                         _lp, _ip, _dp]
         L.orc_park_uniform.argtypes = [C.POINTER(_i)]
         L.orc_park_uniform.restype = _d
         L.orc_phasechange.argtypes = [C.POINTER(PcParams), C.POINTER(_i), _i, _i, _dp, _dp,
@@ -154,6 +156,8 @@ def ref():
                                                      _dp, _lp, _ip, _dp]
         R.ref_colorgradient.argtypes = [_i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _lp,
                                         _ip, _dp]
+        R.ref_surfacetension.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
+                                         _lp, _ip, _dp]
         for n in ("ref_kernel_quintic2d", "ref_kernel_quintic3d", "ref_dw_quintic2d",
                   "ref_dw_quintic3d"):
             getattr(R, n).argtypes = [_d]

@@ -45,6 +45,7 @@
 #include "pair_sph_taitwater_multiphase.h"
 #include "pair_sph_heatconduction_phasechange.h"
 #include "pair_sph_colorgradient.h"
+#include "pair_sph_surfacetension.h"
 
 using namespace LAMMPS_NS;
 
@@ -134,6 +135,12 @@ struct HHeatPC : public PairSPHHeatConductionPhaseChange {
   using PairSPHHeatConductionPhaseChange::fixflag;
   using PairSPHHeatConductionPhaseChange::tc;
 };
+struct HST : public PairSPHSurfaceTension {
+  HST(LAMMPS *l) : PairSPHSurfaceTension(l) {}
+  using PairSPHSurfaceTension::allocate;
+  using PairSPHSurfaceTension::cut;
+};
+
 struct HCG : public PairSPHColorGradient {
   HCG(LAMMPS *l) : PairSPHColorGradient(l) {}
   using PairSPHColorGradient::allocate;
@@ -567,6 +574,33 @@ int ref_colorgradient(int dim, int ntypes, int nlocal, int nghost, const double 
   p->compute(0, 0);
   for (int i = 0; i < nlocal; i++)
     for (int k = 0; k < 3; k++) cg[3 * i + k] = w.lmp->atom->colorgradient[i][k];
+  free_list(l);
+  return 0;
+}
+
+// PairSPHSurfaceTension (coeff pair_sph_surfacetension.cpp:222-247: cut per pair).  cg is
+// the caller's colorgradient for all nall atoms (atom->colorgradient); f (nall*3) out.
+int ref_surfacetension(int dim, int ntypes, int nlocal, int nghost, int newton,
+                       const double *x, const double *rho, const double *rmass,
+                       const int *type, const double *cg, const double *cut, const long *off,
+                       const int *neigh, double *f) {
+  World w(dim, ntypes, nlocal, nghost, newton, 1);
+  fill_atoms(w, x, NULL, rho, NULL, NULL, type, rmass);
+  for (int i = 0; i < nlocal + nghost; i++)
+    for (int k = 0; k < 3; k++) w.lmp->atom->colorgradient[i][k] = cg[3 * i + k];
+  HST *p = new HST(w.lmp);
+  p->allocate();
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      p->cut[i][j] = cut[i * (ntypes + 1) + j];
+      p->setflag[i][j] = 1;
+    }
+  pair_init_cutsq(p, ntypes);
+  NeighList *l = make_list(w, nlocal, off, neigh);
+  p->list = l;
+  p->compute(0, 0);
+  for (int i = 0; i < nlocal + nghost; i++)
+    for (int k = 0; k < 3; k++) f[3 * i + k] = w.lmp->atom->f[i][k];
   free_list(l);
   return 0;
 }

@@ -730,6 +730,77 @@ void orc_colorgradient(int dim, int nlocal, const double *x, const double *rho,
   }
 }
 
+/* PairSPHSurfaceTension::compute, src/USER-SPH/pair_sph_surfacetension.cpp:50-192.
+   S = (|c|^2/ndim I - c c^T) e / |c| for c = the atom's colorgradient (zero when
+   |c| <= EPSILON = 1e-12, :29), F = (S_i V_i^2 + S_j V_j^2) dW, V = rmass/rho; the
+   reference's expressions and operation order are kept term by term.  cg is nall*3. */
+static void st_vector(int dim, const double *c, double absc, const double *e, double *S) {
+  S[0] = S[1] = S[2] = 0.0;
+  if (!(absc > 1.0e-12)) return;
+  if (dim == 2) {
+    S[0] = (e[0] * ((c[1] * c[1] + c[0] * c[0]) / 2 - c[0] * c[0]) - c[0] * e[1] * c[1]) / absc;
+    S[1] = (e[1] * ((c[1] * c[1] + c[0] * c[0]) / 2 - c[1] * c[1]) - e[0] * c[0] * c[1]) / absc;
+  } else {
+    S[0] = (e[0] * (0.3333333333333333 * c[2] * c[2] + 0.3333333333333333 * c[1] * c[1] -
+                    0.6666666666666666 * c[0] * c[0]) -
+            1.0 * c[0] * e[2] * c[2] - 1.0 * c[0] * e[1] * c[1]) / absc;
+    S[1] = (e[1] * (0.3333333333333333 * c[2] * c[2] - 0.6666666666666666 * c[1] * c[1] +
+                    0.3333333333333333 * c[0] * c[0]) -
+            1.0 * c[1] * e[2] * c[2] - 1.0 * e[0] * c[0] * c[1]) / absc;
+    S[2] = (e[2] * (-0.6666666666666666 * c[2] * c[2] + 0.3333333333333333 * c[1] * c[1] +
+                    0.3333333333333333 * c[0] * c[0]) -
+            1.0 * e[1] * c[1] * c[2] - 1.0 * e[0] * c[0] * c[2]) / absc;
+  }
+}
+static double st_abs(int dim, const double *c) {
+  return dim == 3 ? sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2])
+                  : sqrt(c[0] * c[0] + c[1] * c[1]);
+}
+void orc_surfacetension(int dim, int nlocal, int newton_pair, const double *x,
+                        const double *rho, const double *rmass, const int *type, int ntypes,
+                        const double *cg, const double *cut, const double *cutsq,
+                        const long *off, const int *neigh, double *f) {
+  for (int i = 0; i < nlocal; i++) {
+    const int itype = type[i];
+    const double xtmp = x[3 * i], ytmp = x[3 * i + 1], ztmp = x[3 * i + 2];
+    const double imass = rmass[i];
+    const double abscgi = st_abs(dim, cg + 3 * i);
+    for (long jj = off[i]; jj < off[i + 1]; jj++) {
+      const int j = neigh[jj];
+      const double delx = xtmp - x[3 * j];
+      const double dely = ytmp - x[3 * j + 1];
+      const double delz = ztmp - x[3 * j + 2];
+      const double rsq = delx * delx + dely * dely + delz * delz;
+      const int jtype = type[j];
+      const double jmass = rmass[j];
+      if (rsq < cutsq[IDX2(ntypes, itype, jtype)]) {
+        const double h = cut[IDX2(ntypes, itype, jtype)];
+        const double ih = 1.0 / h;
+        double wfd;
+        if (dim == 3) {
+          wfd = orc_dw_quintic3d(sqrt(rsq) * ih);
+          wfd = wfd * ih * ih * ih * ih;
+        } else {
+          wfd = orc_dw_quintic2d(sqrt(rsq) * ih);
+          wfd = wfd * ih * ih * ih;
+        }
+        double eij[3] = {delx / sqrt(rsq), dely / sqrt(rsq), 0.0};
+        if (dim == 3) eij[2] = delz / sqrt(rsq);
+        double Si[3], Sj[3];
+        st_vector(dim, cg + 3 * i, abscgi, eij, Si);
+        st_vector(dim, cg + 3 * j, st_abs(dim, cg + 3 * j), eij, Sj);
+        const double Vi = imass / rho[i];
+        const double Vj = jmass / rho[j];
+        for (int k = 0; k < dim; k++) {
+          const double fk = (Si[k] * Vi * Vi + Sj[k] * Vj * Vj) * wfd;
+          f[3 * i + k] += fk;
+          if (newton_pair || j < nlocal) f[3 * j + k] -= fk;
+        }
+      }
+    }
+  }
+}
+
 /* ------------------------------------------------------------------------------------
    FixMeso, src/USER-SPH/fix_meso.cpp:68-85 (setup_pre_force), :91-140, :144-180
    ------------------------------------------------------------------------------------ */

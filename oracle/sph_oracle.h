@@ -23,6 +23,7 @@
  *   orc_taitwater_multiphase   src/USER-SPH/pair_sph_taitwater_multiphase.cpp:55-186
  *   orc_heatconduction_phasechange src/USER-SPH/pair_sph_heatconduction_phasechange.cpp:52-141
  *   orc_colorgradient          src/USER-SPH/pair_sph_colorgradient.cpp:70-191
+ *   orc_surfacetension         src/USER-SPH/pair_sph_surfacetension.cpp:50-192
  *
  * Data model mirrors LAMMPS: per-atom arrays hold nlocal owned atoms followed by nghost
  * ghosts; vectors (x, v, vest, f) are AoS double[n][3] like atom->x's contiguous backing
@@ -137,6 +138,13 @@ void orc_colorgradient(int dim, int nlocal, const double *x, const double *rho,
                        const double *rmass, const int *type, int ntypes,
                        const double *alpha, const double *cut, const double *cutsq,
                        const long *off, const int *neigh, double *colorgradient);
+
+/* cg: nall*3 colorgradient (owned + ghosts); f (nall*3) accumulated, Newton-3 onto j when
+   newton_pair or j < nlocal (half lists) */
+void orc_surfacetension(int dim, int nlocal, int newton_pair, const double *x,
+                        const double *rho, const double *rmass, const int *type, int ntypes,
+                        const double *cg, const double *cut, const double *cutsq,
+                        const long *off, const int *neigh, double *f);
 
 /* ---- integrator (fix meso) -------------------------------------------------------- */
 void orc_meso_setup(int nlocal, const double *v, double *vest);

@@ -94,8 +94,8 @@ def single_phase_case(name, s, ph, out):
 
 def multiphase_case(name, out):
     """Two-phase system with per-atom rmass (atom_style meso/multiphase) through the
-    reference's rhosum/multiphase, taitwater/multiphase, heatconduction/phasechange and
-    colorgradient."""
+    reference's rhosum/multiphase, taitwater/multiphase, heatconduction/phasechange,
+    colorgradient and surfacetension."""
     R = po.ref()
     s = c3_system(5)
     nt = 2
@@ -144,12 +144,21 @@ def multiphase_case(name, out):
     cg = np.zeros((g.nall, 3))
     R.ref_colorgradient(3, nt, g.nlocal, g.nghost, g.x, rho, rmass, g.type, cga, cut, foff,
                         nz(fnb), cg)
+    # surfacetension on the half list, colorgradient of every atom (ghosts copy their owner:
+    # the gradient is translation invariant)
+    cg_all = g.gather(cg[:g.nlocal])
+    st_cut = np.zeros((3, 3))
+    st_cut[1:, 1:] = h
+    f_st = np.zeros((g.nall, 3))
+    R.ref_surfacetension(3, nt, g.nlocal, g.nghost, 1, g.x, rho, rmass, g.type, cg_all, st_cut,
+                         hoff, nz(hnb), f_st)
     np.savez_compressed(
         os.path.join(HERE, name + ".npz"), dim=3, ntypes=nt, nlocal=g.nlocal, nghost=g.nghost,
         x=g.x, type=g.type, rmass=rmass, rho=rho, e=e, cv=cv, vest=vest, cut=cut,
         full_off=foff, full_nbr=fnb, half_off=hoff, half_nbr=hnb, rho0=rho0, c0=c0,
         gamma=gamma, rbg=rbg, visc=visc, alpha=alpha, fixflag=fixflag, tc=tc, cg_alpha=cga,
-        out_rho=rho_mp[:g.nlocal], out_f=f, out_de=de, out_cg=cg[:g.nlocal])
+        out_rho=rho_mp[:g.nlocal], out_f=f, out_de=de, out_cg=cg[:g.nlocal], cg_all=cg_all,
+        st_cut=st_cut, out_f_st=f_st)
     out.append((name, g.nlocal, g.nghost, int(foff[-1])))
 
 

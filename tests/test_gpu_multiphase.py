@@ -1,8 +1,10 @@
-"""GPU parity of the multiphase styles (sph_hip_*_multiphase, _phasechange, colorgradient):
+"""GPU parity of the multiphase styles (sph_hip_*_multiphase, _phasechange, colorgradient,
+surfacetension):
 
 * the golden vectors the reference's own code wrote (tests/golden/multiphase_n5.npz):
-  rhosum/multiphase and colorgradient on the reference's full list, taitwater/multiphase
-  and heatconduction/phasechange on its half list with newton on (ghost slots included);
+  rhosum/multiphase and colorgradient on the reference's full list, taitwater/multiphase,
+  heatconduction/phasechange and surfacetension on its half list with newton on (ghost
+  slots included);
 * the oracle on a larger two-phase box (fresh seed), same lists;
 * the 2-3 atom KAT geometries of examples/USER/sph/multiphase_two_atoms.
 Tolerance 1e-10 normwise (north_star)."""
@@ -49,6 +51,10 @@ def test_golden_multiphase(gpu, sph_amd):
     de = np.zeros(nall)
     ctx.heatconduction_phasechange(de)
     assert rel_err(de, d["out_de"]) < TOL
+    ctx.surfacetension_coeff(d["st_cut"])
+    f = np.zeros((nall, 3))
+    ctx.surfacetension(d["cg_all"], f)
+    assert rel_err(f, d["out_f_st"]) < TOL
 
 
 def two_phase(nside=8, seed=4321):
@@ -68,7 +74,7 @@ def two_phase(nside=8, seed=4321):
                cv=np.where(liq, 0.04, 0.06), vest=s.v + 0.05 * rng.normal(size=s.v.shape))
     d = {k: g.gather(v) for k, v in own.items()}
     d.update(dim=3, ntypes=nt, nlocal=g.nlocal, nghost=g.nghost, x=g.x, type=g.type, cut=cut,
-             full_off=foff, full_nbr=fnb, half_off=hoff, half_nbr=hnb)
+             full_off=foff, full_nbr=fnb, half_off=hoff, half_nbr=hnb, owner=g.owner)
     return d
 
 
@@ -115,6 +121,28 @@ def test_multiphase_vs_oracle(gpu, sph_amd):
                                      d["type"], 2, alpha, ff.ctypes.data, tc.ctypes.data, cut,
                                      cut * cut, d["half_off"], d["half_nbr"], dw)
     assert rel_err(de, dw) < TOL
+    # surfacetension: colorgradient of every atom (ghosts copy their owner), half list
+    cga = np.zeros((3, 3))
+    cga[1, 2] = cga[2, 1] = 1.0
+    cg = np.zeros((nall, 3))
+    L.orc_colorgradient(3, n, d["x"], d["rho"], d["rmass"], d["type"], 2, cga, cut, cut * cut,
+                        d["full_off"], d["full_nbr"], cg)
+    cg_all = np.ascontiguousarray(np.concatenate([cg[:n], cg[:n][d["owner"]]]))
+    ctx.surfacetension_coeff(cut)
+    f = np.zeros((nall, 3))
+    ctx.surfacetension(cg_all, f)
+    fw = np.zeros((nall, 3))
+    L.orc_surfacetension(3, n, 1, d["x"], d["rho"], d["rmass"], d["type"], 2, cg_all, cut,
+                         cut * cut, d["half_off"], d["half_nbr"], fw)
+    assert rel_err(f, fw) < TOL
+    # ... and on the full list (gather only, owned rows) = the half-list result with the
+    # ghost slots folded into their owners (reverse comm; the pair force is antisymmetric)
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, d["full_off"], d["full_nbr"])
+    f = np.zeros((nall, 3))
+    ctx.surfacetension(cg_all, f)
+    want = fw[:n].copy()
+    np.add.at(want, d["owner"], fw[n:])
+    assert rel_err(f[:n], want) < TOL
 
 
 def test_kat_geometry(gpu, sph_amd):

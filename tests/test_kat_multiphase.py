@@ -149,3 +149,46 @@ def test_colorgradient_kat(po):
     # the script prints |dC_i| for i = 1, 2
     got = np.linalg.norm(cg, axis=1)
     assert np.allclose(got[:2], np.linalg.norm(want, axis=1)[:2], rtol=1e-12, atol=0)
+
+
+def test_surfacetension_kat(po):
+    """surfacetension.mac (with surfacetension.lmp): 3 atoms, m = rho = 1, types (1, 2, 2),
+    h = 1, colorgradient alpha(1,2) = 1.  dC_i = sum_{j: type_j != type_i}
+    sigma_i (C_l(i)/sigma_i^2 + C_l(j)/sigma_j^2) dw(x_i - x_j);
+    Pm_i = (|dC_i|^2/3 I - dC_i dC_i^T)/|dC_i|;
+    Fs_i = sum_{j != i} alpha(k,l) dw(x_i - x_j) . (Pm_i/sigma_i^2 + Pm_j/sigma_j^2).
+    The script prints Fs[1] (atom 1's neighbours are both of the other type, so the
+    alpha(k,l) factor of the .mac is 1 for every pair the LAMMPS style sums for it); Pm is
+    even in dC, so the colorgradient's sign convention does not enter."""
+    X = np.array([[4.6, 5.3, 5.0], [5.5, 5.0, 5.2], [5.0, 5.0, 5.0]])
+    T = np.array([1, 2, 2], dtype=np.int32)
+    m = np.ones(3)
+    rho = np.ones(3)
+    sig = rho / m
+
+    def dwv(d):
+        r = np.linalg.norm(d)
+        return d / r * dw(r, H)
+
+    dC = np.zeros((3, 3))
+    for i in range(3):
+        for j in range(3):
+            if i != j and T[i] != T[j]:
+                dC[i] += sig[i] * (0.0 / sig[i] ** 2 + 1.0 / sig[j] ** 2) * dwv(X[i] - X[j])
+    Pm = [(np.dot(c, c) / 3 * np.eye(3) - np.outer(c, c)) / np.linalg.norm(c) for c in dC]
+    want1 = sum(dwv(X[0] - X[j]) @ (Pm[0] / sig[0] ** 2 + Pm[j] / sig[j] ** 2) for j in (1, 2))
+    # the LAMMPS side: colorgradient (full list) then surfacetension (half list, newton on)
+    foff, fnb, hoff, hnb = lists(3)
+    cut = table(H)
+    alpha = np.zeros((3, 3))
+    alpha[1, 2] = alpha[2, 1] = 1.0
+    cg = np.zeros((3, 3))
+    L = po.lib()
+    L.orc_colorgradient(3, 3, np.ascontiguousarray(X), rho, m, T, 2, alpha, cut, cut * cut,
+                        foff, fnb, cg)
+    # (atom 2's gradient is a near-cancellation ~1e-5 of atom 1's: normwise bar)
+    assert np.allclose(np.abs(cg), np.abs(dC), rtol=0, atol=1e-12 * np.abs(dC).max())
+    f = np.zeros((3, 3))
+    L.orc_surfacetension(3, 3, 1, np.ascontiguousarray(X), rho, m, T, 2, cg, cut, cut * cut,
+                         hoff, hnb, f)
+    assert np.allclose(f[0], want1, rtol=1e-12, atol=1e-14 * np.abs(want1).max())

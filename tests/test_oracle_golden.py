@@ -142,6 +142,12 @@ def test_multiphase_bit_exact(po):
     L.orc_colorgradient(3, n, x, d["rho"], rm, ty, 2, d["cg_alpha"], cut, cutsq, d["full_off"],
                         d["full_nbr"], cg)
     assert np.array_equal(cg[:n], d["out_cg"])
+    # surfacetension (half list, Newton-3 onto owned and ghost j)
+    st_cut = d["st_cut"]
+    f = np.zeros((nall, 3))
+    L.orc_surfacetension(3, n, 1, x, d["rho"], rm, ty, 2, d["cg_all"], st_cut, st_cut * st_cut,
+                         d["half_off"], d["half_nbr"], f)
+    assert np.array_equal(f, d["out_f_st"])
 
 
 def test_quintic_kernels(po):

@@ -168,14 +168,192 @@ def cpu_baseline(n_cpu, steps=2):
             "pair_only_particle_steps_per_s": s.n / (t_rho + t_tait)}
 
 
+# ---- C5 multiphase pair passes (SURVEY.md 8(d) C5 physics, 8(a) rows a6-a8 + 8(f) rank 2) --
+def c5_pair_system(n, seed=2024):
+    """Two-phase n^3 block (bubble_growth physics in dx = 1 units: h = 3, rho_l = 1,
+    rho_v = 0.1, c = 200/sqrt(rho), eta 1 / 0.69, gamma 1, rbackground 0, cv 0.04 / 0.06):
+    a vapour sphere (type 2, radius n/4) in liquid (type 1), jittered sc lattice, open
+    boundaries (no ghosts).  Full and half (i < j) lists within h from a k-d tree."""
+    from scipy.spatial import cKDTree
+    rng = np.random.default_rng(seed)
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij"), -1)
+    x = g.reshape(-1, 3).astype(np.float64) + rng.uniform(-0.1, 0.1, size=(n ** 3, 3))
+    c = (n - 1) / 2.0
+    vap = np.linalg.norm(x - c, axis=1) < n / 4.0
+    ty = np.where(vap, 2, 1).astype(np.int32)
+    rho0 = np.where(vap, 0.1, 1.0)
+    d = dict(x=x, type=ty, rmass=rho0.copy(), rho=rho0 * (1 + 0.01 * rng.uniform(-1, 1, n ** 3)),
+             cv=np.where(vap, 0.06, 0.04), vest=rng.normal(0.0, 0.01, size=x.shape))
+    d["e"] = d["cv"] * np.where(vap, 0.1, 0.02) * (1 + 0.1 * rng.uniform(-1, 1, n ** 3))
+    h = 3.0
+    pairs = cKDTree(x).query_pairs(h, output_type="ndarray")
+    pairs = pairs[np.lexsort((pairs[:, 1], pairs[:, 0]))]
+    N = x.shape[0]
+    hoff = np.zeros(N + 1, dtype=np.int64)
+    np.add.at(hoff, pairs[:, 0] + 1, 1)
+    d["half_off"], d["half_nbr"] = np.cumsum(hoff), pairs[:, 1].astype(np.int32)
+    both = np.concatenate([pairs, pairs[:, ::-1]])
+    both = both[np.lexsort((both[:, 1], both[:, 0]))]
+    foff = np.zeros(N + 1, dtype=np.int64)
+    np.add.at(foff, both[:, 0] + 1, 1)
+    d["full_off"], d["full_nbr"] = np.cumsum(foff), both[:, 1].astype(np.int32)
+    t2 = lambda a11, a12, a22: np.array([[0, 0, 0], [0, a11, a12], [0, a12, a22]], float)
+    cl, cvap = 200.0, 200.0 / np.sqrt(0.1)
+    d.update(h=h, cut=t2(h, h, h), rho0=np.array([0.0, 1.0, 0.1]),
+             c0=np.array([0.0, cl, cvap]), gamma=np.array([0.0, 1.0, 1.0]),
+             rbg=np.zeros(3), visc=t2(1.0, 2 * 0.69 / 1.69, 0.69),
+             cg_alpha=t2(0.0, 1.0, 0.0), alpha=t2(0.1, 2 * 0.1 * 0.05 / 0.15, 0.05),
+             fixflag=np.array([[0, 0, 0], [0, 0, 2], [0, 2, 0]], np.int32), tc=t2(0, 0.0, 0))
+    return d
+
+
+def c5_pair_bytes(n_half, n_full):
+    """Compulsory bytes per particle of each pass (SURVEY.md 8(d) convention: each array read
+    or written once, int32 CSR, fp64; x 24, v 24, rho 8, rmass 8, type 4, e 8, cv 8, cg 24)."""
+    return {"rhosum/multiphase": 24 + 4 + 8 + 4 + 4 * n_full + 8,
+            "colorgradient": 24 + 4 + 8 + 8 + 4 + 4 * n_full + 24,
+            "taitwater/multiphase": 24 + 24 + 8 + 8 + 4 + 4 + 4 * n_half + 24,
+            "surfacetension": 24 + 24 + 8 + 8 + 4 + 4 + 4 * n_half + 24,
+            "heatconduction/phasechange": 24 + 8 + 8 + 8 + 8 + 4 + 4 + 4 * n_half + 8}
+
+
+def c5_pair_main(args, sph):
+    """The C5 pair passes through the pair-style layer (sph_hip_* entry points), the calls a
+    LAMMPS run of bubble_growth's hybrid/overlay makes per step: rhosum/multiphase and
+    colorgradient on the full list, taitwater/multiphase, surfacetension and
+    heatconduction/phasechange on the half list.  `value` is particle-steps/s of the five
+    passes' DEVICE time (HIP events around the kernels; inputs staged once, so the per-call
+    PCIe staging a LAMMPS run adds is excluded and reported separately)."""
+    n = args.edge
+    d = c5_pair_system(n)
+    N = d["x"].shape[0]
+    ctx = sph.PairContext(3, 2, 1)
+    ctx.atoms(N, 0, d["x"], d["type"], vest=d["vest"], rho=d["rho"], e=d["e"])
+    ctx.atoms_multiphase(d["rmass"], d["cv"])
+    ctx.rhosum_multiphase_coeff(d["cut"])
+    ctx.colorgradient_coeff(d["cg_alpha"], d["cut"])
+    ctx.taitwater_multiphase_coeff(d["rho0"], d["c0"], d["gamma"], d["rbg"], d["visc"], d["cut"])
+    ctx.surfacetension_coeff(d["cut"])
+    ctx.heatconduction_phasechange_coeff(d["alpha"], d["cut"], fixflag=d["fixflag"], tc=d["tc"])
+    rho, cg = np.zeros(N), np.zeros((N, 3))
+    f, de = np.zeros((N, 3)), np.zeros(N)
+
+    def step():
+        ms = {}
+        t0 = time.perf_counter()
+        ctx.list_csr(sph.SPH_LIST_FULL, d["full_off"], d["full_nbr"])
+        ctx.rhosum_multiphase(rho)
+        ms["rhosum/multiphase"] = ctx.last_kernel_ms()
+        ctx.colorgradient(cg)
+        ms["colorgradient"] = ctx.last_kernel_ms()
+        ctx.list_csr(sph.SPH_LIST_HALF, d["half_off"], d["half_nbr"])
+        ctx.taitwater_multiphase(f)
+        ms["taitwater/multiphase"] = ctx.last_kernel_ms()
+        ctx.surfacetension(cg, f)
+        ms["surfacetension"] = ctx.last_kernel_ms()
+        ctx.heatconduction_phasechange(de)
+        ms["heatconduction/phasechange"] = ctx.last_kernel_ms()
+        return ms, time.perf_counter() - t0
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    acc = {}
+    wall = 0.0
+    for _ in range(args.steps):
+        ms, w = step()
+        wall += w
+        for k, v in ms.items():
+            acc[k] = acc.get(k, 0.0) + v / args.steps
+    t_dev = sum(acc.values()) * 1e-3
+    n_full = d["full_off"][-1] / N
+    n_half = d["half_off"][-1] / N
+    by = c5_pair_bytes(n_half, n_full)
+    kern = {k: {"ms_per_call": acc[k], "bytes_per_particle": by[k],
+                "achieved_GBs": by[k] * N / (acc[k] * 1e-3) / 1e9} for k in acc}
+    dom = max(acc, key=acc.get)
+    out = {
+        "metric": "kernel particle-steps/s, C5 multiphase pair passes (pair-style layer)",
+        "value": N / t_dev, "unit": "particle-steps/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": t_dev * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic two-phase block (vapour sphere in liquid), seeded",
+        "config": {"workload": f"C5 pair passes: {N} particles, bubble_growth physics (h = 3 dx), "
+                               "open box, rhosum/multiphase + colorgradient (full list), "
+                               "taitwater/multiphase + surfacetension + "
+                               "heatconduction/phasechange (half list, newton on)",
+                   "n_full_per_particle": n_full, "n_half_per_particle": n_half,
+                   "wall_ms_per_step_incl_pcie": wall / args.steps * 1e3},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": kern[dom]["achieved_GBs"],
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": kern[dom]["achieved_GBs"] / PEAK_HBM_GBS, "traffic": None},
+        "kernels": kern,
+    }
+    if not args.no_cpu:
+        out["cpu_baseline"] = c5_pair_cpu(d)
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
+def c5_pair_cpu(d):
+    """The reference's own compute() of the five styles (oracle/_ref) on the same input, one
+    core, one call each."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    if not po.ref_available():
+        return None
+    R = po.ref()
+    N = d["x"].shape[0]
+    x, ty, rm = np.ascontiguousarray(d["x"]), d["type"], d["rmass"]
+    nz = lambda a: a if a.size else np.zeros(1, np.int32)
+    cut = d["cut"]
+    B = d["c0"] ** 2 * d["rho0"] / np.where(d["gamma"] > 0, d["gamma"], 1.0)
+    t = {}
+    t0 = time.perf_counter()
+    rho = d["rho"].copy()
+    R.ref_rhosum_multiphase(3, 2, N, 0, x, ty, rm, cut, d["full_off"], nz(d["full_nbr"]), rho)
+    t["rhosum/multiphase"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cg = np.zeros((N, 3))
+    R.ref_colorgradient(3, 2, N, 0, x, d["rho"], rm, ty, d["cg_alpha"], cut, d["full_off"],
+                        nz(d["full_nbr"]), cg)
+    t["colorgradient"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    f = np.zeros((N, 3))
+    R.ref_taitwater_multiphase(3, 2, N, 0, 1, x, d["vest"], d["rho"], ty, rm, d["rho0"],
+                               d["c0"], d["gamma"], d["rbg"], d["visc"], cut, d["half_off"],
+                               nz(d["half_nbr"]), f)
+    t["taitwater/multiphase"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    R.ref_surfacetension(3, 2, N, 0, 1, x, d["rho"], rm, ty, cg, cut, d["half_off"],
+                         nz(d["half_nbr"]), f)
+    t["surfacetension"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    de = np.zeros(N)
+    R.ref_heatconduction_phasechange(3, 2, N, 0, 1, x, d["e"], d["cv"], d["rho"], rm, ty,
+                                     d["alpha"], d["fixflag"].ctypes.data, d["tc"].ctypes.data,
+                                     cut, d["half_off"], nz(d["half_nbr"]), de)
+    t["heatconduction/phasechange"] = time.perf_counter() - t0
+    tot = sum(t.values())
+    return {"value": N / tot, "unit": "particle-steps/s", "cores": 1, "kind": "reference",
+            "sample": f"reference compute() of the five styles (oracle/_ref) on the same "
+                      f"{N} particles, one call each: " +
+                      ", ".join(f"{k} {v:.3f} s" for k, v in t.items())}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--edge", type=int, default=100, help="lattice edge (edge^3 particles per GPU)")
+    ap.add_argument("--edge", type=int, default=None,
+                    help="lattice edge (edge^3 particles per GPU; default 100, c5pair 80: "
+                         "C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
+    ap.add_argument("--workload", choices=["c2", "c5pair"], default="c2",
+                    help="c2: the headline engine step (default); c5pair: the multiphase "
+                         "pair passes through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
                     help="pair-kernel path: 0 = LDS-staged bins, 1 = CSR rows")
     args = ap.parse_args()
@@ -191,6 +369,11 @@ def main():
     sph = load_pkg()
     ndev = sph.device_count()
     assert ndev > 0, "bench.py needs a HIP device"
+    if args.workload == "c5pair":
+        assert world == 1, "the c5pair workload runs on one GPU"
+        args.edge = args.edge or 80
+        return c5_pair_main(args, sph)
+    args.edge = args.edge or 100
     dev = local % ndev
 
     pg = procgrid_for(world)

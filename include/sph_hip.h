@@ -72,6 +72,11 @@ typedef struct sph_hip_ctx sph_hip_ctx;
    atom->ntypes, newton_pair = force->newton_pair. */
 int sph_hip_create(int device, int dim, int ntypes, int newton_pair, sph_hip_ctx **out);
 int sph_hip_destroy(sph_hip_ctx *ctx);
+/* Device time of the last style call's kernels, in ms (HIP events recorded around the
+   launches on the context's stream; staging and result copies excluded), when enabled by
+   sph_hip_set_timing(ctx, 1).  Measurement support; not part of the LAMMPS pair API. */
+int sph_hip_set_timing(sph_hip_ctx *ctx, int on);
+int sph_hip_last_kernel_ms(sph_hip_ctx *ctx, double *ms);
 
 /* PairSPHRhoSum::coeff/init_one: cut (nt+1)^2 (h per type pair), mass = atom->mass. */
 int sph_hip_rhosum_coeff(sph_hip_ctx *ctx, const double *cut, const double *mass);

@@ -102,6 +102,8 @@ EXPORTS = {
     "sph_hip_heatconduction_phasechange": (_i, [_vp, _dp]),
     "sph_hip_colorgradient_coeff": (_i, [_vp, _dp, _dp]),
     "sph_hip_colorgradient": (_i, [_vp, _dp]),
+    "sph_hip_set_timing": (_i, [_vp, _i]),
+    "sph_hip_last_kernel_ms": (_i, [_vp, _dp]),
     "sph_hip_surfacetension_coeff": (_i, [_vp, _dp]),
     "sph_hip_surfacetension": (_i, [_vp, _dp, _dp]),
     "sph_hip_phasechange": (_i, [_vp, _vp, C.POINTER(_i), _dp, _dp, _dp, _dp, _i,
@@ -296,6 +298,14 @@ class PairContext:
     def colorgradient(self, cg):
         _chk(self.L.sph_hip_colorgradient(self.h, cg))
         return cg
+
+    def set_timing(self, on=True):
+        _chk(self.L.sph_hip_set_timing(self.h, 1 if on else 0))
+
+    def last_kernel_ms(self) -> float:
+        v = np.zeros(1)
+        _chk(self.L.sph_hip_last_kernel_ms(self.h, v))
+        return float(v[0])
 
     def surfacetension_coeff(self, cut):
         _chk(self.L.sph_hip_surfacetension_coeff(self.h, self._t(cut)))

@@ -37,6 +37,23 @@ struct sph_hip_ctx {
   std::vector<double> h1;
   std::vector<int> hoff, hnbr, hilist;
   bool coef_dirty = true;
+  // optional device timing of each style call's kernels (sph_hip_set_timing)
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double kernel_ms = 0.0;
+  void tstart() {
+    if (timing) SPH_HIP_TRY(hipEventRecord(ev0, stream));
+  }
+  void tstop() {
+    if (timing) SPH_HIP_TRY(hipEventRecord(ev1, stream));
+  }
+  // after the stream synchronised
+  void tread() {
+    if (!timing) return;
+    float ms = 0.f;
+    SPH_HIP_TRY(hipEventElapsedTime(&ms, ev0, ev1));
+    kernel_ms = ms;
+  }
 
   void upload_mp() {
     if (!mp_dirty) return;

@@ -34,25 +34,32 @@ struct MpCoefs {
   double scut[NT2], scutsq[NT2];
 };
 
-// Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r, pow() of the reference kept)
+// Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r).  The reference's pow(x, n) with
+// small integer n are evaluated as products (a few ulp apart from libm pow; the golden
+// vectors hold at 1e-13), and the branches as selects of one polynomial per piece.
+__device__ __forceinline__ double p5(double x) {
+  const double x2 = x * x;
+  return x2 * x2 * x;
+}
 __device__ __forceinline__ double quintic_w(int dim, double r) {
   const double norm = (dim == 3) ? 0.0716197243913529 : 0.04195297663091802;
   const double s = 3.0 * r;
-  if (s < 1.0) return norm * (pow(3 - s, 5) - 6 * pow(2 - s, 5) + 15 * pow(1 - s, 5));
-  if (s < 2.0) return norm * (pow(3 - s, 5) - 6 * pow(2 - s, 5));
-  if (s < 3.0) return norm * pow(3 - s, 5);
-  return 0.0;
+  const double a = s < 3.0 ? p5(3 - s) : 0.0;
+  const double b = s < 2.0 ? 6 * p5(2 - s) : 0.0;
+  const double c = s < 1.0 ? 15 * p5(1 - s) : 0.0;
+  return norm * (a - b + c);
 }
 __device__ __forceinline__ double quintic_dw(int dim, double r) {
   const double norm = 3.0 * ((dim == 3) ? 0.0716197243913529 : 0.04195297663091802);
   const double s = 3.0 * r;
+  const double s2 = s * s, s3 = s2 * s, s4 = s2 * s2;
   double wfd;
   if (s < 1) {
-    wfd = -50 * pow(s, 4) + 120 * pow(s, 3) - 120 * s;
+    wfd = -50 * s4 + 120 * s3 - 120 * s;
   } else if (s < 2) {
-    wfd = 25 * pow(s, 4) - 180 * pow(s, 3) + 450 * pow(s, 2) - 420 * s + 75;
+    wfd = 25 * s4 - 180 * s3 + 450 * s2 - 420 * s + 75;
   } else if (s < 3.0) {
-    wfd = -5 * pow(s, 4) + 60 * pow(s, 3) - 270 * pow(s, 2) + 540 * s - 405;
+    wfd = -5 * s4 + 60 * s3 - 270 * s2 + 540 * s - 405;
   } else {
     wfd = 0.0;
   }
@@ -72,6 +79,7 @@ struct MpArgs {
   double *de;     // heat out (nall)
   double4 *cg;    // colorgradient out (nall)
   const double4 *cgi;  // surfacetension: colorgradient of every atom (nall, x y z used)
+  int exp;             // study (SPH_MPX): 1 = skip the Newton-3 atomics onto j
 };
 
 template <int G>
@@ -155,7 +163,7 @@ __global__ void __launch_bounds__(256) k_mp_tait(MpArgs a) {
     fx += tx;
     fy += ty_;
     fz += tz;
-    if (a.half && (a.newton || j < a.nlocal)) {
+    if (a.half && (a.newton || j < a.nlocal) && !(a.exp & 1)) {
       atomicAdd(&a.fo[j].x, -tx);
       atomicAdd(&a.fo[j].y, -ty_);
       atomicAdd(&a.fo[j].z, -tz);
@@ -325,7 +333,7 @@ __global__ void __launch_bounds__(256) k_mp_surface(MpArgs a) {
     fx += tx;
     fy += ty_;
     fz += tz;
-    if (a.half && (a.newton || j < a.nlocal)) {
+    if (a.half && (a.newton || j < a.nlocal) && !(a.exp & 1)) {
       atomicAdd(&a.fo[j].x, -tx);
       atomicAdd(&a.fo[j].y, -ty_);
       if (dim == 3) atomicAdd(&a.fo[j].z, -tz);

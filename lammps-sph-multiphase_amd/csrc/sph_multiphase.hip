@@ -4,6 +4,7 @@
 // from compute().
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "sph_ctx.h"
@@ -38,6 +39,11 @@ MpArgs mp_args(sph_hip_ctx *c) {
   a.en = c->en.p;
   a.cv = c->cv.p;
   a.mc = c->dm;
+  static const int mpx = [] {
+    const char *v = getenv("SPH_MPX");
+    return v ? atoi(v) : 0;
+  }();
+  a.exp = mpx;
   return a;
 }
 
@@ -98,11 +104,14 @@ int sph_hip_rhosum_multiphase(sph_hip_ctx *c, double *rho) {
   c->rho_out.reserve(nall);
   MpArgs a = mp_args(c);
   a.rho = c->rho_out.p;
+  c->tstart();
   hipLaunchKernelGGL(k_mp_rhosum<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->rho_out.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   for (int r = 0; r < c->inum; r++) rho[c->hilist[r]] = c->h1[c->hilist[r]];
   SPH_API_END
 }
@@ -141,11 +150,14 @@ int sph_hip_taitwater_multiphase(sph_hip_ctx *c, double *f) {
   SPH_HIP_TRY(hipMemsetAsync(c->fo.p, 0, nall * sizeof(double4), c->stream));
   MpArgs a = mp_args(c);
   a.fo = c->fo.p;
+  c->tstart();
   hipLaunchKernelGGL(k_mp_tait<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h4.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   auto add = [&](int i) {
     f[3 * i] += c->h4[i].x;
     f[3 * i + 1] += c->h4[i].y;
@@ -188,11 +200,14 @@ int sph_hip_heatconduction_phasechange(sph_hip_ctx *c, double *de) {
   SPH_HIP_TRY(hipMemsetAsync(c->de.p, 0, nall * sizeof(double), c->stream));
   MpArgs a = mp_args(c);
   a.de = c->de.p;
+  c->tstart();
   hipLaunchKernelGGL(k_mp_heat<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->de.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   if (a.half)
     for (int i = 0; i < nall; i++) de[i] += c->h1[i];
   else
@@ -220,11 +235,14 @@ int sph_hip_colorgradient(sph_hip_ctx *c, double *cg) {
   c->cg.reserve(nall);
   MpArgs a = mp_args(c);
   a.cg = c->cg.p;
+  c->tstart();
   hipLaunchKernelGGL(k_mp_colorgradient<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h4.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->cg.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   for (int r = 0; r < c->inum; r++) {
     const int i = c->hilist[r];
     cg[3 * i] = c->h4[i].x;
@@ -260,11 +278,14 @@ int sph_hip_surfacetension(sph_hip_ctx *c, const double *cg, double *f) {
   MpArgs a = mp_args(c);
   a.fo = c->fo.p;
   a.cgi = c->cgin.p;
+  c->tstart();
   hipLaunchKernelGGL(k_mp_surface<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h4.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   auto add = [&](int i) {
     f[3 * i] += c->h4[i].x;
     f[3 * i + 1] += c->h4[i].y;

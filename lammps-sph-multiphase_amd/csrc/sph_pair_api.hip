@@ -80,10 +80,32 @@ int sph_hip_create(int device, int dim, int ntypes, int newton_pair, sph_hip_ctx
   SPH_API_END
 }
 
+int sph_hip_set_timing(sph_hip_ctx *c, int on) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c, SPH_HIP_EINVAL, "sph_hip_set_timing: NULL context");
+  SPH_HIP_TRY(hipSetDevice(c->device));
+  if (on && !c->ev0) {
+    SPH_HIP_TRY(hipEventCreate(&c->ev0));
+    SPH_HIP_TRY(hipEventCreate(&c->ev1));
+  }
+  c->timing = on != 0;
+  c->kernel_ms = 0.0;
+  SPH_API_END
+}
+
+int sph_hip_last_kernel_ms(sph_hip_ctx *c, double *ms) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && ms, SPH_HIP_EINVAL, "sph_hip_last_kernel_ms: bad argument");
+  *ms = c->kernel_ms;
+  SPH_API_END
+}
+
 int sph_hip_destroy(sph_hip_ctx *c) {
   if (!c) return SPH_HIP_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
   c->xf.release();
   c->vr.release();
   c->fo.release();
@@ -255,11 +277,14 @@ int sph_hip_rhosum(sph_hip_ctx *c, double *rho) {
   c->rho_out.reserve(nall);
   RhoArgs ra{c->inum, c->ilist.p, c->off.p, c->nbr.p, c->xf.p, c->ty.p, c->vr.p, c->rho_out.p,
              c->dc};
+  c->tstart();
   launch_rhosum(c->dim, false, c->ntypes == 1, c->stream, ra);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->rho_out.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   for (int r = 0; r < c->inum; r++) {
     const int i = c->hilist[r];
     rho[i] = c->h1[i];
@@ -281,6 +306,7 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
     c->virial.reserve(6);
     SPH_HIP_TRY(hipMemsetAsync(c->virial.p, 0, 6 * sizeof(double), c->stream));
   }
+  c->tstart();
   if (mode & M_TAIT)  // p/rho^2 of every atom (owned + ghost) from the staged rho
     hipLaunchKernelGGL(k_eos, dim3((nall + 255) / 256), dim3(256), 0, c->stream, nall, c->xf.p,
                        c->vr.p, c->ty.p, c->dc);
@@ -302,6 +328,7 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
   a.virial = virial ? c->virial.p : nullptr;
   if (c->list_kind == SPH_LIST_HALF) mode |= M_HALF;
   launch_force(c->dim, c->ntypes == 1, c->stream, c->tait_visc, mode, a);
+  c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   double hv[6] = {0, 0, 0, 0, 0, 0};
   if (mode & M_TAIT) {
@@ -312,6 +339,7 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->de.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (virial) SPH_HIP_TRY(hipMemcpyAsync(hv, c->virial.p, 6 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->tread();
   const int n = (c->list_kind == SPH_LIST_HALF) ? nall : 0;
   auto add_atom = [&](int i) {
     if (mode & M_TAIT) {

@@ -169,12 +169,103 @@ def cpu_baseline(n_cpu, steps=2):
 
 
 # ---- C5 multiphase pair passes (SURVEY.md 8(d) C5 physics, 8(a) rows a6-a8 + 8(f) rank 2) --
+def kd_lists(x, rc):
+    """Full and half (i < j) CSR lists of all pairs within rc (k-d tree; open boundaries)."""
+    from scipy.spatial import cKDTree
+    N = x.shape[0]
+    pairs = cKDTree(x).query_pairs(rc, output_type="ndarray")
+    pairs = pairs[np.lexsort((pairs[:, 1], pairs[:, 0]))]
+    hoff = np.zeros(N + 1, dtype=np.int64)
+    np.add.at(hoff, pairs[:, 0] + 1, 1)
+    half = (np.cumsum(hoff), pairs[:, 1].astype(np.int32))
+    both = np.concatenate([pairs, pairs[:, ::-1]])
+    del pairs
+    both = both[np.lexsort((both[:, 1], both[:, 0]))]
+    foff = np.zeros(N + 1, dtype=np.int64)
+    np.add.at(foff, both[:, 0] + 1, 1)
+    return (np.cumsum(foff), both[:, 1].astype(np.int32)), half
+
+
+def c2_pair_main(args, sph):
+    """The headline styles through the drop-in pair-style layer, as LAMMPS calls them:
+    sph/rhosum on its FULL list (pair_sph_rhosum.cpp:57-62), sph/taitwater on the default
+    HALF list with newton on (Newton-3 j share gathered through the reverse half list),
+    C2 physics, lists within h + skin.  Device time of the kernels (HIP events); the per-call
+    PCIe staging of a LAMMPS-driven call is reported separately."""
+    n = args.edge
+    x, v, t, rho, e, cv = make_system(n, 12345)
+    N = x.shape[0]
+    (foff, fnb), (hoff, hnb) = kd_lists(x, 3.3)
+    h = 3.0
+    cut = np.zeros((2, 2))
+    cut[1, 1] = h
+    visc = np.zeros((2, 2))
+    visc[1, 1] = 0.1
+    mass = np.array([0.0, 1.0])
+    rho0, c0 = np.array([0.0, 1.0]), np.array([0.0, 10.0])
+    ctx = sph.PairContext(3, 1, 1)
+    ctx.atoms(N, 0, x, t, vest=v, rho=rho, e=e)
+    ctx.rhosum_coeff(cut, mass)
+    ctx.taitwater_coeff(rho0, c0, c0 ** 2 * rho0 / 7.0, visc, cut, mass)
+    r = np.zeros(N)
+    f, drho, de = np.zeros((N, 3)), np.zeros(N), np.zeros(N)
+
+    def step(first_half_call_after_upload=True):
+        ms = {}
+        t0 = time.perf_counter()
+        ctx.list_csr(sph.SPH_LIST_FULL, foff, fnb)
+        ctx.rhosum(r)
+        ms["rhosum"] = ctx.last_kernel_ms()
+        ctx.list_csr(sph.SPH_LIST_HALF, hoff, hnb)
+        ctx.taitwater(f, drho, de)
+        ms["taitwater"] = ctx.last_kernel_ms()   # includes the reverse-list build
+        ctx.taitwater(f, drho, de)
+        ms["taitwater_list_reused"] = ctx.last_kernel_ms()
+        return ms, time.perf_counter() - t0
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_timing(True)
+    acc, wall = {}, 0.0
+    for _ in range(args.steps):
+        ms, w = step()
+        wall += w
+        for k, val in ms.items():
+            acc[k] = acc.get(k, 0.0) + val / args.steps
+    n_full, n_half = foff[-1] / N, hoff[-1] / N
+    by = {"rhosum": 40 + 4 * n_half, "taitwater": 104 + 4 * n_half}   # SURVEY.md 8(d)
+    by["taitwater_list_reused"] = by["taitwater"]
+    kern = {k: {"ms_per_call": acc[k], "bytes_per_particle": by[k],
+                "achieved_GBs": by[k] * N / (acc[k] * 1e-3) / 1e9} for k in acc}
+    t_dev = (acc["rhosum"] + acc["taitwater"]) * 1e-3
+    out = {
+        "metric": "kernel particle-steps/s, C2 rhosum + taitwater via the pair-style layer",
+        "value": N / t_dev, "unit": "particle-steps/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": t_dev * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (jittered sc lattice, gaussian velocities, seeded)",
+        "config": {"workload": f"C2 physics on {N} particles, open box, rhosum on the full list "
+                               "+ taitwater on the half list (newton on), lists within h + skin "
+                               "= 3.3; the taitwater call after a list upload includes the "
+                               "reverse half-list build",
+                   "n_full_per_particle": n_full, "n_half_per_particle": n_half,
+                   "wall_ms_per_step_incl_pcie": wall / args.steps * 1e3},
+        "roofline": {"bound": "hbm", "kernel": "taitwater (half list: forward + reverse "
+                                               "gather)",
+                     "achieved": kern["taitwater"]["achieved_GBs"], "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": kern["taitwater"]["achieved_GBs"] / PEAK_HBM_GBS,
+                     "traffic": None},
+        "kernels": kern,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def c5_pair_system(n, seed=2024):
     """Two-phase n^3 block (bubble_growth physics in dx = 1 units: h = 3, rho_l = 1,
     rho_v = 0.1, c = 200/sqrt(rho), eta 1 / 0.69, gamma 1, rbackground 0, cv 0.04 / 0.06):
     a vapour sphere (type 2, radius n/4) in liquid (type 1), jittered sc lattice, open
     boundaries (no ghosts).  Full and half (i < j) lists within h from a k-d tree."""
-    from scipy.spatial import cKDTree
     rng = np.random.default_rng(seed)
     g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(n), indexing="ij"), -1)
     x = g.reshape(-1, 3).astype(np.float64) + rng.uniform(-0.1, 0.1, size=(n ** 3, 3))
@@ -186,17 +277,7 @@ def c5_pair_system(n, seed=2024):
              cv=np.where(vap, 0.06, 0.04), vest=rng.normal(0.0, 0.01, size=x.shape))
     d["e"] = d["cv"] * np.where(vap, 0.1, 0.02) * (1 + 0.1 * rng.uniform(-1, 1, n ** 3))
     h = 3.0
-    pairs = cKDTree(x).query_pairs(h, output_type="ndarray")
-    pairs = pairs[np.lexsort((pairs[:, 1], pairs[:, 0]))]
-    N = x.shape[0]
-    hoff = np.zeros(N + 1, dtype=np.int64)
-    np.add.at(hoff, pairs[:, 0] + 1, 1)
-    d["half_off"], d["half_nbr"] = np.cumsum(hoff), pairs[:, 1].astype(np.int32)
-    both = np.concatenate([pairs, pairs[:, ::-1]])
-    both = both[np.lexsort((both[:, 1], both[:, 0]))]
-    foff = np.zeros(N + 1, dtype=np.int64)
-    np.add.at(foff, both[:, 0] + 1, 1)
-    d["full_off"], d["full_nbr"] = np.cumsum(foff), both[:, 1].astype(np.int32)
+    (d["full_off"], d["full_nbr"]), (d["half_off"], d["half_nbr"]) = kd_lists(x, h)
     t2 = lambda a11, a12, a22: np.array([[0, 0, 0], [0, a11, a12], [0, a12, a22]], float)
     cl, cvap = 200.0, 200.0 / np.sqrt(0.1)
     d.update(h=h, cut=t2(h, h, h), rho0=np.array([0.0, 1.0, 0.1]),
@@ -351,9 +432,10 @@ def main():
                          "C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
-    ap.add_argument("--workload", choices=["c2", "c5pair"], default="c2",
-                    help="c2: the headline engine step (default); c5pair: the multiphase "
-                         "pair passes through the pair-style layer (--edge sets n^3)")
+    ap.add_argument("--workload", choices=["c2", "c2pair", "c5pair"], default="c2",
+                    help="c2: the headline engine step (default); c2pair: rhosum + taitwater "
+                         "through the pair-style layer; c5pair: the multiphase pair passes "
+                         "through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
                     help="pair-kernel path: 0 = LDS-staged bins, 1 = CSR rows")
     args = ap.parse_args()
@@ -369,10 +451,10 @@ def main():
     sph = load_pkg()
     ndev = sph.device_count()
     assert ndev > 0, "bench.py needs a HIP device"
-    if args.workload == "c5pair":
-        assert world == 1, "the c5pair workload runs on one GPU"
+    if args.workload in ("c2pair", "c5pair"):
+        assert world == 1, "the pair-layer workloads run on one GPU"
         args.edge = args.edge or 80
-        return c5_pair_main(args, sph)
+        return (c2_pair_main if args.workload == "c2pair" else c5_pair_main)(args, sph)
     args.edge = args.edge or 100
     dev = local % ndev
 

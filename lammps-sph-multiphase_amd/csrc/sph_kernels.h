@@ -205,7 +205,10 @@ static __global__ void k_eos(int n, double4 *__restrict__ xf, const double4 *__r
 // ------------------------------------------------------------------------------------
 // Force pass: sph/taitwater (VISC=0 Monaghan, 1 Morris) and/or sph/heatconduction.
 // MODE bits: TAIT | HEAT | HALF.  FULL lists: overwrite (accum=0) or add (accum=1) the
-// owned row's results.  HALF lists: atomics on both i and j (reference scatter).
+// owned row's results.  HALF lists: atomics on both i and j (reference scatter), or, with
+// nojside, the i share only, added without atomics (the j share is then gathered by a
+// FULL-mode pass over the reverse half list: each pair value seen from j is exactly the
+// negated/mirrored j share -- the formulas are symmetric up to the sign of dx and dv).
 // ------------------------------------------------------------------------------------
 enum { M_TAIT = 1, M_HEAT = 2, M_HALF = 4 };
 
@@ -216,7 +219,7 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
         const double4 *__restrict__ xf, const double4 *__restrict__ vr,
         const int *__restrict__ ty, const double *__restrict__ en, double4 *__restrict__ fo,
         double *__restrict__ de, int accum, const Coefs *__restrict__ cf, double gx,
-        double gy, double gz, double *__restrict__ virial) {
+        double gy, double gz, double *__restrict__ virial, int nojside) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr bool HALF = (MODE & M_HALF) != 0;
@@ -334,7 +337,7 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
         dE += deltaE;
         if (HALF) jdE -= deltaE;
       }
-      if (HALF && (newton || j < nlocal)) {
+      if (HALF && !nojside && (newton || j < nlocal)) {
         if (TAIT) {
           atomicAdd(&fo[j].x, jfx);
           atomicAdd(&fo[j].y, jfy);
@@ -361,7 +364,17 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
   }
   dE = group_sum<G>(dE);
   if (lane == 0) {
-    if (HALF) {
+    if (HALF && nojside) {  // one row per atom: plain read-modify-write
+      if (TAIT) {
+        double4 o = fo[i];
+        o.x += fx;
+        o.y += fy;
+        o.z += fz;
+        o.w += drho;
+        fo[i] = o;
+      }
+      de[i] += dE;
+    } else if (HALF) {
       if (TAIT) {
         atomicAdd(&fo[i].x, fx);
         atomicAdd(&fo[i].y, fy);

@@ -80,6 +80,9 @@ struct MpArgs {
   double4 *cg;    // colorgradient out (nall)
   const double4 *cgi;  // surfacetension: colorgradient of every atom (nall, x y z used)
   int exp;             // study (SPH_MPX): 1 = skip the Newton-3 atomics onto j
+  int rev;             // half list with its reverse list: j share gathered (k_mp_half REV)
+  const int *roff, *rnbr;  // reverse half list: row j holds the atoms whose half row has j
+  int nrows;               // reverse rows (nall with newton_pair, else nlocal)
 };
 
 template <int G>
@@ -120,116 +123,63 @@ __device__ __forceinline__ double mp_pressure(double B, double rho0, double gamm
   return B * (pow(rho / rho0, gamma) - rbg);
 }
 
-template <int G>
-__global__ void __launch_bounds__(256) k_mp_tait(MpArgs a) {
-  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
-  const int lane = threadIdx.x & (G - 1);
-  if (row >= a.inum) return;
-  const MpCoefs *c = a.mc;
-  const int nt1 = c->ntypes + 1;
-  const int i = a.ilist[row];
-  const double4 xi = a.xf[i], vi = a.vr[i];
-  const int it = a.ty[i];
-  const double rhoi = vi.w;
+
+// ---- half-list styles: taitwater/multiphase, heatconduction/phasechange, surfacetension ----
+// The reference's per-pair arithmetic as device functions of the pair (i = the list row's
+// atom, j = the entry), so the same value can be added to i and subtracted from j.
+enum { MP_TAIT = 0, MP_HEAT = 1, MP_SURF = 2 };
+
+// taitwater/multiphase (pair_sph_taitwater_multiphase.cpp:128-170): force on i
+__device__ __forceinline__ bool mp_tait_pair(const MpCoefs *c, int dim, double4 xi, double4 vi,
+                                             int it, double mi, double4 xj, double4 vj, int jt,
+                                             double mj, double3 &F) {
+  const int p = it * (c->ntypes + 1) + jt;
+  const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+  const double rsq = dx * dx + dy * dy + dz * dz;
+  if (!(rsq < c->tcutsq[p])) return false;
+  const double ih = 1.0 / c->tcut[p];
+  const double r = sqrt(rsq);
+  double wfd;
+  if (dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih / r;
+  else wfd = quintic_dw(2, r * ih) * ih * ih * ih / r;
+  const double rhoi = vi.w, rhoj = vj.w;
+  const double Vi = mi / rhoi, Vj = mj / rhoj;
+  const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
   const double pi = mp_pressure(c->B[it], c->rho0[it], c->gamma[it], c->rbg[it], rhoi);
-  const double Vi = a.rm[i] / rhoi;
-  const double Vi2 = Vi * Vi;
-  double fx = 0.0, fy = 0.0, fz = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int j = a.nbr[k];
-    const double4 xj = a.xf[j], vj = a.vr[j];
-    const int jt = a.ty[j];
-    const int p = it * nt1 + jt;
-    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    if (!(rsq < c->tcutsq[p])) continue;
-    const double ih = 1.0 / c->tcut[p];
-    const double r = sqrt(rsq);
-    double wfd;
-    if (a.dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih / r;
-    else wfd = quintic_dw(2, r * ih) * ih * ih * ih / r;
-    const double rhoj = vj.w;
-    const double Vj = a.rm[j] / rhoj;
-    const double Vj2 = Vj * Vj;
-    // reference quirk kept: p_j with gamma[itype] (pair_sph_taitwater_multiphase.cpp:148)
-    const double pj = mp_pressure(c->B[jt], c->rho0[jt], c->gamma[it], c->rbg[jt], rhoj);
-    const double pij = (rhoj * pi + rhoi * pj) / (rhoi + rhoj);
-    const double velx = vi.x - vj.x, vely = vi.y - vj.y, velz = vi.z - vj.z;
-    const double fvisc = (Vi2 + Vj2) * c->tvisc[p] * wfd;
-    const double fpair = -(Vi2 + Vj2) * pij * wfd;
-    const double tx = dx * fpair + velx * fvisc;
-    const double ty_ = dy * fpair + vely * fvisc;
-    const double tz = dz * fpair + velz * fvisc;
-    fx += tx;
-    fy += ty_;
-    fz += tz;
-    if (a.half && (a.newton || j < a.nlocal) && !(a.exp & 1)) {
-      atomicAdd(&a.fo[j].x, -tx);
-      atomicAdd(&a.fo[j].y, -ty_);
-      atomicAdd(&a.fo[j].z, -tz);
-    }
-  }
-  fx = group_sum<G>(fx);
-  fy = group_sum<G>(fy);
-  fz = group_sum<G>(fz);
-  if (lane == 0) {
-    if (a.half) {
-      atomicAdd(&a.fo[i].x, fx);
-      atomicAdd(&a.fo[i].y, fy);
-      atomicAdd(&a.fo[i].z, fz);
-    } else {
-      a.fo[i].x += fx;
-      a.fo[i].y += fy;
-      a.fo[i].z += fz;
-    }
-  }
+  // reference quirk kept: p_j with gamma[itype] (pair_sph_taitwater_multiphase.cpp:148)
+  const double pj = mp_pressure(c->B[jt], c->rho0[jt], c->gamma[it], c->rbg[jt], rhoj);
+  const double pij = (rhoj * pi + rhoi * pj) / (rhoi + rhoj);
+  const double velx = vi.x - vj.x, vely = vi.y - vj.y, velz = vi.z - vj.z;
+  const double fvisc = (Vi2 + Vj2) * c->tvisc[p] * wfd;
+  const double fpair = -(Vi2 + Vj2) * pij * wfd;
+  F = make_double3(dx * fpair + velx * fvisc, dy * fpair + vely * fvisc, dz * fpair + velz * fvisc);
+  return true;
 }
 
-template <int G>
-__global__ void __launch_bounds__(256) k_mp_heat(MpArgs a) {
-  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
-  const int lane = threadIdx.x & (G - 1);
-  if (row >= a.inum) return;
-  const MpCoefs *c = a.mc;
-  const int nt1 = c->ntypes + 1;
-  const int i = a.ilist[row];
-  const double4 xi = a.xf[i];
-  const int it = a.ty[i];
-  const double rhoi = a.vr[i].w;
-  const double mi = a.rm[i];
-  const double Ti0 = a.en[i] / a.cv[i];   // sph_energy2t, sph_energy_equation.cpp:16-18
-  double dE = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int j = a.nbr[k];
-    const double4 xj = a.xf[j];
-    const int jt = a.ty[j];
-    const int p = it * nt1 + jt;
-    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    if (!(rsq < c->hcutsq[p])) continue;
-    const double ih = 1.0 / c->hcut[p];
-    double wfd;
-    if (a.dim == 3) {
-      wfd = quintic_dw(3, sqrt(rsq) * ih);
-      wfd = wfd * ih * ih * ih * ih / sqrt(rsq);
-    } else {
-      wfd = quintic_dw(2, sqrt(rsq) * ih);
-      wfd = wfd * ih * ih * ih / sqrt(rsq);
-    }
-    double Ti = Ti0;
-    double Tj = a.en[j] / a.cv[j];
-    const int ff = c->hfix[p];
-    if (ff == it && Ti < Tj) Ti = c->htc[p];
-    if (ff == jt && Tj < Ti) Tj = c->htc[p];
-    const double deltaE = 2.0 * c->halpha[p] * (Ti - Tj) * wfd / (rhoi * a.vr[j].w);
-    dE += deltaE * a.rm[j];
-    if (a.half && (a.newton || j < a.nlocal)) atomicAdd(&a.de[j], -deltaE * mi);
+// heatconduction/phasechange (pair_sph_heatconduction_phasechange.cpp:101-136): deltaE;
+// de_i += deltaE m_j, de_j -= deltaE m_i
+__device__ __forceinline__ bool mp_heat_pair(const MpCoefs *c, int dim, double4 xi, int it,
+                                             double rhoi, double Ti0, double4 xj, int jt,
+                                             double rhoj, double Tj0, double &deltaE) {
+  const int p = it * (c->ntypes + 1) + jt;
+  const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+  const double rsq = dx * dx + dy * dy + dz * dz;
+  if (!(rsq < c->hcutsq[p])) return false;
+  const double ih = 1.0 / c->hcut[p];
+  double wfd;
+  if (dim == 3) {
+    wfd = quintic_dw(3, sqrt(rsq) * ih);
+    wfd = wfd * ih * ih * ih * ih / sqrt(rsq);
+  } else {
+    wfd = quintic_dw(2, sqrt(rsq) * ih);
+    wfd = wfd * ih * ih * ih / sqrt(rsq);
   }
-  dE = group_sum<G>(dE);
-  if (lane == 0) {
-    if (a.half) atomicAdd(&a.de[i], dE);
-    else a.de[i] += dE;
-  }
+  double Ti = Ti0, Tj = Tj0;
+  const int ff = c->hfix[p];
+  if (ff == it && Ti < Tj) Ti = c->htc[p];
+  if (ff == jt && Tj < Ti) Tj = c->htc[p];
+  deltaE = 2.0 * c->halpha[p] * (Ti - Tj) * wfd / (rhoi * rhoj);
+  return true;
 }
 
 template <int G>
@@ -293,66 +243,155 @@ __device__ __forceinline__ double st_abs(int dim, double4 c) {
   return dim == 3 ? sqrt(c.x * c.x + c.y * c.y + c.z * c.z) : sqrt(c.x * c.x + c.y * c.y);
 }
 
-// sph/surfacetension: F = (S_i V_i^2 + S_j V_j^2) dW_quintic, V = rmass/rho; i gets +F, j
-// gets -F on a half list (newton_pair or j < nlocal), like the reference.
-template <int G>
-__global__ void __launch_bounds__(256) k_mp_surface(MpArgs a) {
+
+// surfacetension (pair_sph_surfacetension.cpp:100-190): F = (S_i V_i^2 + S_j V_j^2) dW
+__device__ __forceinline__ bool mp_surf_pair(const MpCoefs *c, int dim, double4 xi, int it,
+                                             double Vi, double4 cgi, double abscgi, double4 xj,
+                                             int jt, double Vj, double4 cgj, double3 &F) {
+  const int p = it * (c->ntypes + 1) + jt;
+  const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+  const double rsq = dx * dx + dy * dy + dz * dz;
+  if (!(rsq < c->scutsq[p])) return false;
+  const double ih = 1.0 / c->scut[p];
+  const double r = sqrt(rsq);
+  const double wfd = (dim == 3) ? quintic_dw(3, r * ih) * ih * ih * ih * ih
+                                : quintic_dw(2, r * ih) * ih * ih * ih;
+  const double3 e = make_double3(dx / r, dy / r, dim == 3 ? dz / r : 0.0);
+  const double3 Si = st_vector(dim, cgi, abscgi, e);
+  const double3 Sj = st_vector(dim, cgj, st_abs(dim, cgj), e);
+  F = make_double3((Si.x * Vi * Vi + Sj.x * Vj * Vj) * wfd, (Si.y * Vi * Vi + Sj.y * Vj * Vj) * wfd,
+                   dim == 3 ? (Si.z * Vi * Vi + Sj.z * Vj * Vj) * wfd : 0.0);
+  return true;
+}
+
+// One pass of a half-list style over list rows (REV = false: rows = the caller's list, the
+// pair's share onto i; full lists add into i only, half lists without a reverse list also
+// scatter the j share with fp64 atomics, as the reference scatters) or over the REVERSE
+// half list (REV = true: row = atom j, entries = the atoms i whose half row holds j; the
+// same pair value, recomputed with i as the row atom, is subtracted from j).  With a
+// reverse list the j share is gathered: no atomics (device fp64 atomics run at ~35 G/s).
+template <int G, int STYLE, bool REV>
+__global__ void __launch_bounds__(256) k_mp_half(MpArgs a) {
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
-  if (row >= a.inum) return;
+  const int nrows = REV ? a.nrows : a.inum;
+  if (row >= nrows) return;
   const MpCoefs *c = a.mc;
-  const int nt1 = c->ntypes + 1;
   const int dim = a.dim;
-  const int i = a.ilist[row];
-  const double4 xi = a.xf[i];
-  const int it = a.ty[i];
-  const double4 cgi = a.cgi[i];
-  const double abscgi = st_abs(dim, cgi);
-  const double Vi = a.rm[i] / a.vr[i].w;
-  double fx = 0.0, fy = 0.0, fz = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int j = a.nbr[k];
-    const double4 xj = a.xf[j];
-    const int jt = a.ty[j];
-    const int p = it * nt1 + jt;
-    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    if (!(rsq < c->scutsq[p])) continue;
-    const double ih = 1.0 / c->scut[p];
-    const double r = sqrt(rsq);
-    const double wfd = (dim == 3) ? quintic_dw(3, r * ih) * ih * ih * ih * ih
-                                  : quintic_dw(2, r * ih) * ih * ih * ih;
-    const double3 e = make_double3(dx / r, dy / r, dim == 3 ? dz / r : 0.0);
-    const double4 cgj = a.cgi[j];
-    const double3 Si = st_vector(dim, cgi, abscgi, e);
-    const double3 Sj = st_vector(dim, cgj, st_abs(dim, cgj), e);
-    const double Vj = a.rm[j] / a.vr[j].w;
-    const double tx = (Si.x * Vi * Vi + Sj.x * Vj * Vj) * wfd;
-    const double ty_ = (Si.y * Vi * Vi + Sj.y * Vj * Vj) * wfd;
-    const double tz = dim == 3 ? (Si.z * Vi * Vi + Sj.z * Vj * Vj) * wfd : 0.0;
-    fx += tx;
-    fy += ty_;
-    fz += tz;
-    if (a.half && (a.newton || j < a.nlocal) && !(a.exp & 1)) {
-      atomicAdd(&a.fo[j].x, -tx);
-      atomicAdd(&a.fo[j].y, -ty_);
-      if (dim == 3) atomicAdd(&a.fo[j].z, -tz);
-    }
-  }
-  fx = group_sum<G>(fx);
-  fy = group_sum<G>(fy);
-  fz = group_sum<G>(fz);
-  if (lane == 0) {
-    if (a.half) {
-      atomicAdd(&a.fo[i].x, fx);
-      atomicAdd(&a.fo[i].y, fy);
-      atomicAdd(&a.fo[i].z, fz);
+  const int r = REV ? row : a.ilist[row];  // this row's atom
+  const double4 xr = a.xf[r], vrr = a.vr[r];
+  const int tr = a.ty[r];
+  const double mr = a.rm[r];
+  const double Tr = STYLE == MP_HEAT ? a.en[r] / a.cv[r] : 0.0;  // sph_energy2t
+  const double4 cgr = STYLE == MP_SURF ? a.cgi[r] : make_double4(0, 0, 0, 0);
+  const double abscgr = STYLE == MP_SURF ? st_abs(dim, cgr) : 0.0;
+  const double Vr = STYLE == MP_SURF ? mr / vrr.w : 0.0;
+  const int *off = REV ? a.roff : a.off;
+  const int *nbr = REV ? a.rnbr : a.nbr;
+  const bool scatter = !REV && a.half && !a.rev && !(a.exp & 1);
+  double sx = 0.0, sy = 0.0, sz = 0.0;
+  for (int k = off[row] + lane; k < off[row + 1]; k += G) {
+    const int o = nbr[k];  // the other atom of the pair
+    const double4 xo = a.xf[o], vo = a.vr[o];
+    const int to = a.ty[o];
+    const double mo = a.rm[o];
+    // pair (i, j): i = row atom for REV = false, the entry for REV = true
+    if (STYLE == MP_TAIT) {
+      double3 F;
+      const bool hit = REV ? mp_tait_pair(c, dim, xo, vo, to, mo, xr, vrr, tr, mr, F)
+                           : mp_tait_pair(c, dim, xr, vrr, tr, mr, xo, vo, to, mo, F);
+      if (!hit) continue;
+      if (REV) {
+        sx -= F.x;
+        sy -= F.y;
+        sz -= F.z;
+      } else {
+        sx += F.x;
+        sy += F.y;
+        sz += F.z;
+        if (scatter && (a.newton || o < a.nlocal)) {
+          atomicAdd(&a.fo[o].x, -F.x);
+          atomicAdd(&a.fo[o].y, -F.y);
+          atomicAdd(&a.fo[o].z, -F.z);
+        }
+      }
+    } else if (STYLE == MP_SURF) {
+      double3 F;
+      const double Vo = mo / vo.w;
+      const double4 cgo = a.cgi[o];
+      const bool hit = REV ? mp_surf_pair(c, dim, xo, to, Vo, cgo, st_abs(dim, cgo), xr, tr, Vr,
+                                          cgr, F)
+                           : mp_surf_pair(c, dim, xr, tr, Vr, cgr, abscgr, xo, to, Vo, cgo, F);
+      if (!hit) continue;
+      if (REV) {
+        sx -= F.x;
+        sy -= F.y;
+        sz -= F.z;
+      } else {
+        sx += F.x;
+        sy += F.y;
+        sz += F.z;
+        if (scatter && (a.newton || o < a.nlocal)) {
+          atomicAdd(&a.fo[o].x, -F.x);
+          atomicAdd(&a.fo[o].y, -F.y);
+          if (dim == 3) atomicAdd(&a.fo[o].z, -F.z);
+        }
+      }
     } else {
-      a.fo[i].x += fx;
-      a.fo[i].y += fy;
-      a.fo[i].z += fz;
+      const double To = a.en[o] / a.cv[o];
+      double dE;
+      const bool hit = REV ? mp_heat_pair(c, dim, xo, to, vo.w, To, xr, tr, vrr.w, Tr, dE)
+                           : mp_heat_pair(c, dim, xr, tr, vrr.w, Tr, xo, to, vo.w, To, dE);
+      if (!hit) continue;
+      if (REV) {
+        sx -= dE * mo;
+      } else {
+        sx += dE * mo;
+        if (scatter && (a.newton || o < a.nlocal)) atomicAdd(&a.de[o], -dE * mr);
+      }
     }
   }
+  sx = group_sum<G>(sx);
+  if (STYLE != MP_HEAT) {
+    sy = group_sum<G>(sy);
+    sz = group_sum<G>(sz);
+  }
+  if (lane != 0) return;
+  if (STYLE == MP_HEAT) {
+    if (scatter) atomicAdd(&a.de[r], sx);
+    else a.de[r] += sx;  // one row per atom per pass: plain read-modify-write
+  } else if (scatter) {
+    atomicAdd(&a.fo[r].x, sx);
+    atomicAdd(&a.fo[r].y, sy);
+    atomicAdd(&a.fo[r].z, sz);
+  } else {
+    a.fo[r].x += sx;
+    a.fo[r].y += sy;
+    a.fo[r].z += sz;
+  }
+}
+
+// reverse half list: entry owner (the row's atom) of every list entry
+static __global__ void __launch_bounds__(256)
+k_entry_owner(int inum, const int *__restrict__ off, const int *__restrict__ ilist,
+              int *__restrict__ owner) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= inum) return;
+  const int i = ilist[row];
+  for (int k = off[row]; k < off[row + 1]; k++) owner[k] = i;
+}
+// reverse CSR offsets: roff[j] = first position of key >= j in the sorted keys
+static __global__ void __launch_bounds__(256)
+k_rev_offsets(int nrows, int tot, const int *__restrict__ skey, int *__restrict__ roff) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > nrows) return;
+  int lo = 0, hi = tot;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if (skey[m] < j) lo = m + 1;
+    else hi = m;
+  }
+  roff[j] = lo;
 }
 
 }  // namespace sph

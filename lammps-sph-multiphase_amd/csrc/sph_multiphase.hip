@@ -3,6 +3,7 @@
 // PairSPHHeatConductionPhaseChange, PairSPHColorGradient and PairSPHSurfaceTension call
 // from compute().
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
 #include <vector>
@@ -60,6 +61,25 @@ void mp_ready(sph_hip_ctx *c, const char *who, bool have) {
 }
 
 dim3 mp_grid(int inum) { return dim3((unsigned)(((long long)inum * MPG + 255) / 256)); }
+
+// one half-list style: forward rows (+ reverse rows when gathering the j share)
+template <int STYLE>
+void run_half(sph_hip_ctx *c, MpArgs a) {
+  const bool rev = a.half && sph_rev_on();
+  c->tstart();  // the reverse build (first half-list style after a list upload) is timed too
+  if (rev) {
+    c->build_rev();
+    a.rev = 1;
+    a.roff = c->roff.p;
+    a.rnbr = c->rnbr.p;
+    a.nrows = c->newton ? c->nlocal + c->nghost : c->nlocal;
+  }
+  hipLaunchKernelGGL((k_mp_half<MPG, STYLE, false>), mp_grid(c->inum), dim3(256), 0, c->stream, a);
+  if (rev && a.nrows > 0)
+    hipLaunchKernelGGL((k_mp_half<MPG, STYLE, true>), mp_grid(a.nrows), dim3(256), 0, c->stream,
+                       a);
+  c->tstop();
+}
 
 }  // namespace
 
@@ -150,9 +170,7 @@ int sph_hip_taitwater_multiphase(sph_hip_ctx *c, double *f) {
   SPH_HIP_TRY(hipMemsetAsync(c->fo.p, 0, nall * sizeof(double4), c->stream));
   MpArgs a = mp_args(c);
   a.fo = c->fo.p;
-  c->tstart();
-  hipLaunchKernelGGL(k_mp_tait<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
-  c->tstop();
+  run_half<MP_TAIT>(c, a);
   SPH_HIP_TRY(hipGetLastError());
   c->h4.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));
@@ -200,9 +218,7 @@ int sph_hip_heatconduction_phasechange(sph_hip_ctx *c, double *de) {
   SPH_HIP_TRY(hipMemsetAsync(c->de.p, 0, nall * sizeof(double), c->stream));
   MpArgs a = mp_args(c);
   a.de = c->de.p;
-  c->tstart();
-  hipLaunchKernelGGL(k_mp_heat<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
-  c->tstop();
+  run_half<MP_HEAT>(c, a);
   SPH_HIP_TRY(hipGetLastError());
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->de.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -278,9 +294,7 @@ int sph_hip_surfacetension(sph_hip_ctx *c, const double *cg, double *f) {
   MpArgs a = mp_args(c);
   a.fo = c->fo.p;
   a.cgi = c->cgin.p;
-  c->tstart();
-  hipLaunchKernelGGL(k_mp_surface<MPG>, mp_grid(c->inum), dim3(256), 0, c->stream, a);
-  c->tstop();
+  run_half<MP_SURF>(c, a);
   SPH_HIP_TRY(hipGetLastError());
   c->h4.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));

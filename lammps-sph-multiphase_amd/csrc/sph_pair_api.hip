@@ -109,6 +109,11 @@ int sph_hip_destroy(sph_hip_ctx *c) {
   c->xf.release();
   c->vr.release();
   c->fo.release();
+  c->rkey.release();
+  c->rnbr.release();
+  c->rown.release();
+  c->roff.release();
+  c->tmp.release();
   c->en.release();
   c->ty.release();
   c->de.release();
@@ -221,6 +226,7 @@ static void upload_list(sph_hip_ctx *c, int kind, int inum) {
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   c->list_kind = kind;
   c->inum = inum;
+  c->rev_ok = false;
 }
 
 int sph_hip_list(sph_hip_ctx *c, int kind, int inum, const int *ilist, const int *numneigh,
@@ -326,8 +332,23 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
   a.accum = 0;
   a.cf = c->dc;
   a.virial = virial ? c->virial.p : nullptr;
+  const bool rev = c->list_kind == SPH_LIST_HALF && sph_rev_on();
+  if (rev) c->build_rev();  // timed with the kernels (once per list upload)
   if (c->list_kind == SPH_LIST_HALF) mode |= M_HALF;
+  a.nojside = rev ? 1 : 0;
   launch_force(c->dim, c->ntypes == 1, c->stream, c->tait_visc, mode, a);
+  if (rev && c->rev_rows() > 0) {
+    // the j share: FULL-mode gather over the reverse half list, added to the i shares
+    ForceArgs b = a;
+    b.inum = c->rev_rows();
+    b.ilist = nullptr;
+    b.off = c->roff.p;
+    b.nbr = c->rnbr.p;
+    b.accum = 1;
+    b.virial = nullptr;
+    b.nojside = 0;
+    launch_force(c->dim, c->ntypes == 1, c->stream, c->tait_visc, mode & ~M_HALF, b);
+  }
   c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   double hv[6] = {0, 0, 0, 0, 0, 0};

@@ -36,6 +36,13 @@ struct Transport {
   // exchange device buffers (stream-ordered on s)
   virtual void exchange(const void *sbuf, size_t sbytes, int dest, void *rbuf, size_t rbytes,
                         int src, hipStream_t s) = 0;
+  // two independent exchanges (the two directions of one dimension) at once
+  virtual void exchange2(const void *s0, size_t sb0, int d0, void *r0, size_t rb0, int src0,
+                         const void *s1, size_t sb1, int d1, void *r1, size_t rb1, int src1,
+                         hipStream_t s) {
+    exchange(s0, sb0, d0, r0, rb0, src0, s);
+    exchange(s1, sb1, d1, r1, rb1, src1, s);
+  }
   virtual void barrier(hipStream_t s) = 0;
 };
 
@@ -73,6 +80,17 @@ class RcclTransport : public Transport {
     SPH_NCCL_TRY(ncclGroupStart());
     if (sbytes) SPH_NCCL_TRY(ncclSend(sbuf, sbytes, ncclUint8, dest, comm_, s));
     if (rbytes) SPH_NCCL_TRY(ncclRecv(rbuf, rbytes, ncclUint8, src, comm_, s));
+    SPH_NCCL_TRY(ncclGroupEnd());
+  }
+  // one RCCL group for both directions of a dimension: one launch/sync round instead of two
+  void exchange2(const void *s0, size_t sb0, int d0, void *r0, size_t rb0, int src0,
+                 const void *s1, size_t sb1, int d1, void *r1, size_t rb1, int src1,
+                 hipStream_t s) override {
+    SPH_NCCL_TRY(ncclGroupStart());
+    if (sb0) SPH_NCCL_TRY(ncclSend(s0, sb0, ncclUint8, d0, comm_, s));
+    if (rb0) SPH_NCCL_TRY(ncclRecv(r0, rb0, ncclUint8, src0, comm_, s));
+    if (sb1) SPH_NCCL_TRY(ncclSend(s1, sb1, ncclUint8, d1, comm_, s));
+    if (rb1) SPH_NCCL_TRY(ncclRecv(r1, rb1, ncclUint8, src1, comm_, s));
     SPH_NCCL_TRY(ncclGroupEnd());
   }
   void barrier(hipStream_t s) override {

@@ -529,38 +529,59 @@ struct sph_engine {
     nghost = nall - nlocal;
   }
 
-  // Comm::forward_comm (x, vest, rho, e) swap by swap
-  void forward_multi() {
-    for (int k = 0; k < nswap; k++) {
-      Swap &sw = swaps[k];
-      cbs.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * 9 * sizeof(double), true, s);
-      cbr.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * 9 * sizeof(double), true, s);
-      if (sw.nsend)
-        hipLaunchKernelGGL(k_pack_forward, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
-                           sw.list.p, sw.dim, sw.shift, xf.p, vr.p, en.p, (double *)cbs.p);
-      swap_move(sw.remote, (size_t)sw.nsend * 9 * sizeof(double), sw.sendproc,
-                (size_t)sw.nrecv * 9 * sizeof(double), sw.recvproc);
-      if (sw.nrecv)
-        hipLaunchKernelGGL(k_unpack_forward, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
-                           sw.firstrecv, (const double *)cbr.p, xf.p, vr.p, en.p);
+  // Per-step forward traffic, one dimension at a time: the two swaps of a dimension send
+  // from the same atoms (owned + earlier dimensions' ghosts, see borders_multi) and
+  // receive into disjoint ghost ranges, so both are packed into one buffer and moved as
+  // ONE exchange (one RCCL group over xGMI per dimension instead of one per swap).
+  template <class Pack, class Unpack>
+  void forward_dims(size_t rec, Pack pack, Unpack unpack) {
+    for (int k = 0; k + 1 < nswap; k += 2) {
+      Swap &a = swaps[k], &b = swaps[k + 1];
+      const size_t sa = (size_t)a.nsend * rec, sb = (size_t)b.nsend * rec;
+      const size_t ra = (size_t)a.nrecv * rec, rb = (size_t)b.nrecv * rec;
+      const size_t so = (sa + 255) & ~(size_t)255, ro = (ra + 255) & ~(size_t)255;
+      cbs.reserve(std::max<size_t>(so + sb, 1), true, s);
+      cbr.reserve(std::max<size_t>(ro + rb, 1), true, s);
+      if (a.nsend) pack(a, cbs.p);
+      if (b.nsend) pack(b, cbs.p + so);
+      if (a.remote) {
+        tr->exchange2(cbs.p, sa, a.sendproc, cbr.p, ra, a.recvproc, cbs.p + so, sb, b.sendproc,
+                      cbr.p + ro, rb, b.recvproc, s);
+      } else {  // this brick is its own neighbour along this dimension (periodic self swap)
+        if (ra) SPH_HIP_TRY(hipMemcpyAsync(cbr.p, cbs.p, ra, hipMemcpyDeviceToDevice, s));
+        if (rb) SPH_HIP_TRY(hipMemcpyAsync(cbr.p + ro, cbs.p + so, rb, hipMemcpyDeviceToDevice, s));
+      }
+      if (a.nrecv) unpack(a, cbr.p);
+      if (b.nrecv) unpack(b, cbr.p + ro);
     }
   }
 
-  // comm->forward_comm_pair of sph/rhosum: rho (+ the EOS term) swap by swap
+  // Comm::forward_comm (x, vest, rho, e)
+  void forward_multi() {
+    forward_dims(
+        9 * sizeof(double),
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_pack_forward, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                             sw.list.p, sw.dim, sw.shift, xf.p, vr.p, en.p, (double *)buf);
+        },
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_unpack_forward, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s,
+                             sw.nrecv, sw.firstrecv, (const double *)buf, xf.p, vr.p, en.p);
+        });
+  }
+
+  // comm->forward_comm_pair of sph/rhosum: rho (+ the EOS term)
   void forward_rho_multi() {
-    for (int k = 0; k < nswap; k++) {
-      Swap &sw = swaps[k];
-      cbs.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * sizeof(double2), true, s);
-      cbr.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * sizeof(double2), true, s);
-      if (sw.nsend)
-        hipLaunchKernelGGL(k_pack_rho, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
-                           sw.list.p, xf.p, vr.p, (double2 *)cbs.p);
-      swap_move(sw.remote, (size_t)sw.nsend * sizeof(double2), sw.sendproc,
-                (size_t)sw.nrecv * sizeof(double2), sw.recvproc);
-      if (sw.nrecv)
-        hipLaunchKernelGGL(k_unpack_rho, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
-                           sw.firstrecv, (const double2 *)cbr.p, xf.p, vr.p);
-    }
+    forward_dims(
+        sizeof(double2),
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_pack_rho, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                             sw.list.p, xf.p, vr.p, (double2 *)buf);
+        },
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_unpack_rho, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
+                             sw.firstrecv, (const double2 *)buf, xf.p, vr.p);
+        });
   }
 
   // Comm::reverse_comm (f, drho, de): swaps in reverse order, ghosts back to senders

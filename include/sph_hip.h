@@ -229,8 +229,9 @@ typedef struct {
   int rank;                    /* my rank in the brick, x fastest */
   /* spatially sort owned particles at every rebuild (atom->sort analogue) */
   int sort;
-  /* pair-pass kernels: 0 = LDS-staged bins + 16-bit slot lists (needs sort),
-     1 = full-list rows with global gathers, 2 = LDS tiles,
+  /* pair-pass kernels: 1 = full-list rows with global gathers (second-generation row
+     kernels over strided, chunk-transposed lists: the fastest, use this),
+     0 = LDS-staged bins + 16-bit slot lists (needs sort), 2 = LDS tiles,
      3 = cluster pairs (a wave takes a cluster of 4 consecutive owned atoms and the union
          of their neighbours, each neighbour record loaded once for the cluster; gather
          only), 4 = as 3 over half lists with Newton-3 updates by fp64 atomics */

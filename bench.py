@@ -86,6 +86,21 @@ def share_uid(dist, rank, make_uid):
     return obj[0]
 
 
+class stdout_to_stderr:
+    """RCCL prints its version banner on fd 1 at communicator init; keep stdout for the one
+    JSON line of the bench contract."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def c2_config(sph, n, pg=(1, 1, 1), rank=0):
     h = 3.0
     cut = np.zeros((2, 2))
@@ -438,6 +453,10 @@ def main():
                          "through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
                     help="pair-kernel path: 0 = LDS-staged bins, 1 = CSR rows")
+    ap.add_argument("--comm-loopback", action="store_true",
+                    help="one GPU: route the periodic self swaps through a one-rank RCCL "
+                         "communicator (send/recv to itself) -- the multi-GPU halo path's cost "
+                         "without the xGMI transfer")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -466,9 +485,15 @@ def main():
     eng.set_atoms(x, v, t, rho, e, cv)
     if world > 1:
         eng.set_tags(tags)
-        eng.comm_init(share_uid(dist, rank, sph.comm_uid), world, rank)
-    eng.setup()
-    eng.run(args.warmup)
+    uid = share_uid(dist, rank, sph.comm_uid) if world > 1 else None
+    with stdout_to_stderr():  # communicator init, first exchanges and warmup
+        if world > 1:
+            eng.comm_init(uid, world, rank)
+        elif args.comm_loopback:
+            eng.comm_init(sph.comm_uid(), 1, 0)
+            eng.comm_loopback(True)
+        eng.setup()
+        eng.run(args.warmup)
     eng.sync()
 
     def barrier():
@@ -524,7 +549,8 @@ def main():
                                   f"in {pg[0]}x{pg[1]}x{pg[2]} bricks (C4 at 8 GPUs)"),
                    "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "parallelism": ("single GPU" if world == 1 else
+                   "parallelism": (("single GPU, halos through RCCL loopback"
+                                    if args.comm_loopback else "single GPU") if world == 1 else
                                    f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo "
                                    "exchange + migration, one rank per GPU"),
                    "kernel_path": {1: "lds-staged bins", 2: "lds tiles"}.get(st["staged"],

@@ -265,6 +265,10 @@ int sph_engine_destroy(sph_engine *e);
    local order with their tags (sph_engine_set_tags sets global tags; default = index). */
 int sph_engine_comm_uid(void *uid128);
 int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank);
+/* One-brick engine with a communicator attached: on != 0 routes its periodic self swaps
+   (borders, forward, rho, reverse) through the communicator -- RCCL send/recv to itself --
+   instead of device copies, so the multi-brick data path runs on one GPU.  Before setup. */
+int sph_engine_comm_loopback(sph_engine *e, int on);
 typedef struct sph_local_world sph_local_world;
 int sph_local_world_create(int nranks, sph_local_world **out);
 int sph_local_world_destroy(sph_local_world *w);

@@ -113,6 +113,7 @@ EXPORTS = {
     "sph_engine_destroy": (_i, [_vp]),
     "sph_engine_comm_uid": (_i, [_vp]),
     "sph_engine_comm_init": (_i, [_vp, _vp, _i, _i]),
+    "sph_engine_comm_loopback": (_i, [_vp, _i]),
     "sph_local_world_create": (_i, [_i, C.POINTER(_vp)]),
     "sph_local_world_destroy": (_i, [_vp]),
     "sph_engine_comm_local": (_i, [_vp, _vp, _i]),
@@ -460,6 +461,10 @@ class Engine:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = C.create_string_buffer(bytes(uid), 128)
         _chk(self.L.sph_engine_comm_init(self.h, buf, nranks, rank))
+
+    def comm_loopback(self, on: bool = True):
+        """One brick, self swaps through the attached communicator (RCCL send/recv to self)."""
+        _chk(self.L.sph_engine_comm_loopback(self.h, 1 if on else 0))
 
     def neighbor_counts(self):
         c = np.zeros(self.nlocal, dtype=np.int32)

@@ -149,7 +149,11 @@ struct sph_engine {
   int nswap = 0;
   DBuf<unsigned char> cbs, cbr, flag2;
   DBuf<int> sel2;
-  bool multi() const { return pg[0] * pg[1] * pg[2] > 1; }
+  // loopback: a one-brick run whose periodic self swaps go through the attached
+  // communicator (RCCL send/recv to itself) instead of device copies -- the multi-brick
+  // data path (slab selection, packing, RCCL groups, unpacking) on one GPU
+  bool loopback = false;
+  bool multi() const { return pg[0] * pg[1] * pg[2] > 1 || loopback; }
   int64_t step = 0;
   bool setup_done = false;
   bool global_tags = false;
@@ -491,7 +495,7 @@ struct sph_engine {
         sw.dir = dir;
         sw.sendproc = procneigh[d][dir];
         sw.recvproc = procneigh[d][1 - dir];
-        sw.remote = pg[d] > 1;
+        sw.remote = pg[d] > 1 || loopback;
         bool sendflag = true;  // sendneed/recvneed across a non-periodic boundary (:226-274)
         if (!box.periodic[d]) sendflag = dir == 0 ? myloc[d] > 0 : myloc[d] < pg[d] - 1;
         sw.lo = dir == 0 ? -1.0e20 : subhi[d] - cutghost;
@@ -1881,6 +1885,16 @@ int sph_engine_comm_init(sph_engine *e, const void *uid128, int nranks, int rank
   ncclUniqueId id;
   memcpy(&id, uid128, sizeof(id));
   attach(e, new RcclTransport(id, nranks, rank));
+  SPH_API_END
+}
+
+int sph_engine_comm_loopback(sph_engine *e, int on) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_comm_loopback: NULL engine");
+  SPH_REQUIRE(e->nprocs == 1 && e->tr, SPH_HIP_ECOMM,
+              "sph_engine_comm_loopback: needs a one-brick engine with a communicator attached");
+  e->loopback = on != 0;
+  e->setup_done = false;
   SPH_API_END
 }
 

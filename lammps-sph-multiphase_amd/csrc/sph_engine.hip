@@ -112,6 +112,15 @@ static int row2_exp() {
   static int v = env_int("SPH_EXP", 0);
   return v;
 }
+// SPH_OVERLAP (default 0): with a brick decomposition, run the pair passes of interior
+// rows (no ghost in the list) on a second stream while the forward / rho halos are in
+// flight, then the boundary rows after them (sph_engine::pair_compute_overlap).  Parity
+// holds (tests/test_gpu_bricks.py with SPH_OVERLAP=1), but on one GPU through the RCCL
+// loopback it measured 1.29 (serial) -> 1.35 ms per step at C2 1M: the split launches
+// cost more than the loopback halo they hide.  Whether xGMI transfers (~17 MB per step
+// per rank at C4) change that is unmeasured here (no multi-GPU box) -> off by default.
+// (read per engine at sph_engine_create)
+static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
 
 namespace {
 
@@ -154,6 +163,14 @@ struct sph_engine {
   // data path (slab selection, packing, RCCL groups, unpacking) on one GPU
   bool loopback = false;
   bool multi() const { return pg[0] * pg[1] * pg[2] > 1 || loopback; }
+  // halo/compute overlap (multi only): interior and boundary rows of the current list
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  DBuf<int> rows_in, rows_bd;
+  DBuf<unsigned char> fl_in, fl_bd;
+  int n_in = 0, n_bd = 0;
+  bool ov_ready = false;  // rows_in / rows_bd describe the current list
+  bool overlap = false;   // SPH_OVERLAP at creation
   int64_t step = 0;
   bool setup_done = false;
   bool global_tags = false;
@@ -1234,6 +1251,74 @@ struct sph_engine {
       }
     }
     if (want_tiles() && nlocal > 0) tiled = build_tiles();
+    ov_ready = false;
+    if (overlap_on()) classify_rows();
+  }
+
+  bool overlap_on() const {
+    return multi() && overlap && !staged && !tiled && !clustered && use_row2() &&
+           !tight_on() && (force_mode & M_TAIT) != 0 && cfg.rhosum_nstep > 0;
+  }
+  // interior rows (no ghost in the list) and boundary rows, each in row order
+  void classify_rows() {
+    const int n = nlocal;
+    if (!s2) {
+      // (a lowest-priority s2 was measured: the interior rows starve, 1.31 -> 2.17 ms per
+      // step on the loopback bench)
+      SPH_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      SPH_HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+      SPH_HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    fl_in.reserve(n > 0 ? n : 1);
+    fl_bd.reserve(n > 0 ? n : 1);
+    if (n)
+      hipLaunchKernelGGL(k_row_ghost_flags, dim3((unsigned)(((long)n * 8 + 255) / 256)),
+                         dim3(256), 0, s, n, nlocal, strided ? nullptr : off.p,
+                         strided ? list_stride : 0, ccnt.p, nbr.p, list_perm_g, list_perm_pi,
+                         fl_in.p, fl_bd.p);
+    n_in = select_flagged(fl_in.p, n, rows_in);
+    n_bd = select_flagged(fl_bd.p, n, rows_bd);
+    SPH_REQUIRE(n_in + n_bd == n, SPH_HIP_ERUNTIME, "row classification lost rows");
+    ov_ready = true;
+  }
+  void fork() {  // s2 continues after everything queued on s so far
+    SPH_HIP_TRY(hipEventRecord(ev_fork, s));
+    SPH_HIP_TRY(hipStreamWaitEvent(s2, ev_fork, 0));
+  }
+  void join() {  // s continues after everything queued on s2 so far
+    SPH_HIP_TRY(hipEventRecord(ev_join, s2));
+    SPH_HIP_TRY(hipStreamWaitEvent(s, ev_join, 0));
+  }
+
+  // Forward comm + rhosum + forward rho + taitwater(+heat) of a non-rebuild step with the
+  // halos overlapped: interior rows read no ghost, so their rhosum runs (on s2) while the
+  // x/vest/rho/e halo moves, and their force pass while the rho halo moves; boundary rows
+  // follow each exchange on s.  Same per-row arithmetic as pair_compute (bit-identical).
+  // The forward pack may read an interior row's rho/EOS term before or after this
+  // step's rhosum wrote it: ghost rho and P/rho^2 are only read after the rho halo has
+  // overwritten them, so either value is harmless.
+  void pair_compute_overlap() {
+    Row2Args b = row2_args(), bi = b, bb = b;
+    bi.a.n = n_in;
+    bi.rows = rows_in.p;
+    bb.a.n = n_bd;
+    bb.rows = rows_bd.p;
+    {
+      Scope t(this, T_RHO);  // (this class then includes the forward halo)
+      fork();
+      row2_rhosum(nt1(), s2, bi);
+      forward_multi();
+      row2_rhosum(nt1(), s, bb);
+      join();
+    }
+    {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);  // (includes the rho halo)
+      fork();
+      row2_force(nt1(), cfg.tait_visc, force_mode, s2, bi);
+      forward_rho_multi();
+      row2_force(nt1(), cfg.tait_visc, force_mode, s, bb);
+      join();
+    }
   }
 
   void rebuild() {
@@ -1488,10 +1573,13 @@ struct sph_engine {
       if ((step - last_build) % every == 0) {
         rebuild();
         last_build = (int)step;
+        pair_compute(rhosum_due());
+      } else if (ov_ready && rhosum_due() && overlap_on()) {
+        pair_compute_overlap();
       } else {
         forward();
+        pair_compute(rhosum_due());
       }
-      pair_compute(rhosum_due());
       if (timing && pending.size() > 4096) harvest();
     }
     if (nsteps > 0) {
@@ -1613,6 +1701,7 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     delete e;
     throw;
   }
+  e->overlap = overlap_env();
   *out = e;
   SPH_API_END
 }
@@ -1661,6 +1750,14 @@ int sph_engine_destroy(sph_engine *e) {
   e->nbr32.release();
   e->nbr16.release();
   if (e->dc) (void)hipFree(e->dc);
+  e->rows_in.release();
+  e->rows_bd.release();
+  e->fl_in.release();
+  e->fl_bd.release();
+  if (e->s2) (void)hipStreamSynchronize(e->s2);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->s2) (void)hipStreamDestroy(e->s2);
   if (e->s) (void)hipStreamDestroy(e->s);
   delete e;
   return SPH_HIP_OK;

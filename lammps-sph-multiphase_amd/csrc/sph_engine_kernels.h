@@ -687,4 +687,35 @@ static __global__ void k_add_gravity(int n, StepConst sc, double gx, double gy, 
   fo[i].z += m * gz;
 }
 
+// Rows whose list holds a ghost (index >= nlocal): bd[i] = 1, in[i] = !bd[i].  One
+// 64-lane wave per 8 rows (8 lanes per row walk its entries); strided rows stored
+// chunk-transposed (perm_g > 0) are read through tpos.  Interior rows (no ghost) can run
+// their pair passes while a halo exchange is in flight.
+static __global__ void __launch_bounds__(256)
+k_row_ghost_flags(int n, int nlocal, const int *__restrict__ off, int stride,
+                  const int *__restrict__ rcnt, const int *__restrict__ nbr, int perm_g,
+                  int perm_pi, unsigned char *__restrict__ in, unsigned char *__restrict__ bd) {
+  constexpr int G = 8;
+  const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  const bool live = i < n;
+  int beg = 0, cnt = 0;
+  if (live) {
+    beg = stride > 0 ? i * stride : off[i];
+    cnt = stride > 0 ? rcnt[i] : off[i + 1] - beg;
+  }
+  bool ghost = false;
+  for (int e = lane; e < cnt; e += G) {
+    const int q = (stride > 0 && perm_g > 0) ? tpos(e, perm_g, perm_pi) : e;
+    ghost |= nbr[beg + q] >= nlocal;
+  }
+  const unsigned long long m = __ballot(ghost);
+  const int gbase = (threadIdx.x & 63) & ~(G - 1);
+  const bool any = ((m >> gbase) & 0xffull) != 0;
+  if (live && lane == 0) {
+    bd[i] = any ? 1 : 0;
+    in[i] = any ? 0 : 1;
+  }
+}
+
 }  // namespace sph

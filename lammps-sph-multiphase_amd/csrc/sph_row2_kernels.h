@@ -151,7 +151,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
               const int *__restrict__ nbr, double4 *__restrict__ xf,
               const int *__restrict__ ty, double4 *__restrict__ vr,
               const Coefs *__restrict__ cf, int *__restrict__ tnbr, int *__restrict__ tcnt,
-              int pi) {
+              int pi, const int *__restrict__ rows) {
   static_assert(!TIGHT || LP, "the tight-list compaction needs wave-uniform trip counts");
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   __shared__ double s_fc[(NT1 || !TIGHT) ? 1 : NT2];
@@ -164,17 +164,20 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
     }
     __syncthreads();
   }
-  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  // rows != nullptr: the launch covers the n rows rows[0..n) (an interior / boundary
+  // subset, see sph_engine overlap), else rows 0..n-1
+  const int idx = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   const int el = entry_slot<G>(lane, pi);
   // LP: lanes of rows past n stay in the loop (masked) so every DPP partner is active
-  if (!LP && row >= n) return;
-  const bool live = row < n;
+  if (!LP && idx >= n) return;
+  const bool live = idx < n;
   const bool odd = (threadIdx.x & 1) != 0;
   const Rsrc rn = make_rsrc(nbr, nbytes<int>(ntot));
   const Rsrc rx = make_rsrc(xf, nbytes<double4>(nall));
   const Rsrc rt = make_rsrc(ty, nbytes<int>(nall));
-  const int rr = live ? row : n - 1;
+  const int rr = rows ? rows[live ? idx : n - 1] : (live ? idx : n - 1);
+  const int row = rr;
   const double4 xi = xf[rr];
   const int it = NT1 ? 1 : ty[rr];
   const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
@@ -259,7 +262,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
              const double4 *__restrict__ vr, const int *__restrict__ ty,
              const double *__restrict__ en, const Coefs *__restrict__ cf,
              double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-             double gz, int pi) {
+             double gz, int pi, const int *__restrict__ rows) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   __shared__ TaitPair s_t[(TAIT && !NT1) ? NT2 : 1];
@@ -272,18 +275,19 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
     }
     __syncthreads();
   }
-  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int idx = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   const int el = entry_slot<G>(lane, pi);
-  if (!LP && row >= n) return;
-  const bool live = row < n;
+  if (!LP && idx >= n) return;
+  const bool live = idx < n;
   const bool odd = (threadIdx.x & 1) != 0;
   const Rsrc rn = make_rsrc(nbr, nbytes<int>(ntot));
   const Rsrc rx = make_rsrc(xf, nbytes<double4>(nall));
   const Rsrc rv = make_rsrc(vr, nbytes<double4>(nall));
   const Rsrc rt = make_rsrc(ty, nbytes<int>(nall));
   const Rsrc re = make_rsrc(en, HEAT ? nbytes<double>(nall) : 0u);
-  const int rr = live ? row : n - 1;
+  const int rr = rows ? rows[live ? idx : n - 1] : (live ? idx : n - 1);
+  const int row = rr;
   const double4 xi = xf[rr];
   const double4 vi = vr[rr];
   const double ei = HEAT ? en[rr] : 0.0;
@@ -408,6 +412,7 @@ struct Row2Args {
   int stride = 0;                 // > 0: fixed-stride rows with counts rcnt (else a.off CSR)
   const int *rcnt = nullptr;
   int *tnbr = nullptr, *tcnt = nullptr;  // rhosum: write the tight list here (strided, LP)
+  const int *rows = nullptr;             // a.n rows listed here instead of rows 0..a.n-1
 };
 
 // 32-bit byte offsets of every array the row2 kernels read
@@ -423,11 +428,11 @@ inline void row2_rhosum_kt(bool nt1, hipStream_t s, const Row2Args &b) {
   if (nt1)
     hipLaunchKernelGGL((k_row2_rhosum<G, U, true, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows);
   else
     hipLaunchKernelGGL((k_row2_rhosum<G, U, false, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows);
 }
 template <int G, int U, bool LP, bool IV>
 inline void row2_rhosum_k(bool nt1, hipStream_t s, const Row2Args &b) {
@@ -454,7 +459,7 @@ inline void row2_force_t(hipStream_t s, const Row2Args &b) {
   if (grid == 0) return;
   hipLaunchKernelGGL((k_row2_force<G, U, VISC, MODE, NT1, LP, IV, EXP>), dim3(grid), dim3(256),
                      0, s, a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.vr,
-                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz, b.pi ? 1 : 0);
+                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz, b.pi ? 1 : 0, b.rows);
 }
 
 template <int G, int U, bool NT1, bool LP, bool IV>

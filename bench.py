@@ -183,6 +183,152 @@ def cpu_baseline(n_cpu, steps=2):
             "pair_only_particle_steps_per_s": s.n / (t_rho + t_tait)}
 
 
+# ---- C3: two-phase Morris + heat conduction on the engine ----------
+C3_MASS, C3_RHO0, C3_E = (1.0, 0.5), (1.0, 0.5), (1.0, 2.0)
+
+
+def c3_system(n, seed=12345, tseed=87287):
+    """C2's lattice with type 2 by Bernoulli(0.5) (seed 87287), m = (1, 0.5), rho = rho0 =
+    (1, 0.5), e = (1, 2) by type, cv = 1 -- as oracle/pyoracle.cubic_lattice(ntypes=2)."""
+    x, v, t, rho, e, cv, _ = brick_lattice(n, (1, 1, 1), 0, seed)
+    t[np.random.default_rng(tseed).random(t.shape[0]) < 0.5] = 2
+    rho = np.where(t == 1, C3_RHO0[0], C3_RHO0[1])
+    e = np.where(t == 1, C3_E[0], C3_E[1])
+    return x, v, t, rho, e, cv
+
+
+def c3_tables(h=3.0):
+    cut = np.zeros((3, 3))
+    cut[1:, 1:] = h
+    visc = np.zeros((3, 3))
+    visc[1:, 1:] = 0.01
+    alpha = np.zeros((3, 3))
+    alpha[1:, 1:] = 0.1
+    return cut, visc, alpha
+
+
+def c3_config(sph, n):
+    cut, visc, alpha = c3_tables()
+    return sph.make_config(3, 2, [0.0, 0.0, 0.0], [float(n)] * 3, [1, 1, 1],
+                           [0.0, C3_MASS[0], C3_MASS[1]], 0.3, 1e-3, neigh_every=10,
+                           tait=dict(rho0=np.array([0.0, *C3_RHO0]),
+                                     c0=np.array([0.0, 10.0, 10.0]), visc=visc, cut=cut,
+                                     morris=True),
+                           heat=dict(alpha=alpha, cut=cut))
+
+
+def c3_cpu_baseline(n_cpu, steps=2):
+    """The reference's own PairSPHTaitwaterMorris::compute + PairSPHHeatConduction::compute
+    (oracle/_ref, 1 core) on the C3 input at n_cpu^3 particles, half list, plus one
+    Neighbor::full_bin + half_from_full_newton amortised over neigh_every = 10."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    if not po.ref_available():
+        return None
+    R = po.ref()
+    x, v, t, rho, e, cv = c3_system(n_cpu)
+    s = po.cubic_lattice(n_cpu, ntypes=2, type2_frac=0.5, mass=C3_MASS, rho=C3_RHO0, e=C3_E)
+    assert np.array_equal(s.type, t) and np.array_equal(s.x, x)
+    cut, visc, alpha = c3_tables()
+    cns, cmax = po.cutneighsq(2, cut, 0.3)
+    g = po.borders(s, cmax)
+    args = (3, 2, g.nlocal, g.nghost, np.ascontiguousarray(g.x), g.type, s.boxlo, s.boxhi,
+            s.boxlo, s.boxhi, cmax, np.ascontiguousarray(cns))
+    t0 = time.perf_counter()
+    foff = np.zeros(g.nlocal + 1, dtype=np.int64)
+    tot = R.ref_neigh_full(*args, foff, None, 0)
+    fnb = np.zeros(tot, dtype=np.int32)
+    R.ref_neigh_full(*args, foff, fnb.ctypes.data, tot)
+    hoff = np.zeros(g.nlocal + 1, dtype=np.int64)
+    htot = R.ref_neigh_half_from_full(g.nlocal, g.nghost, g.x, foff, fnb, hoff, None)
+    hnb = np.zeros(htot, dtype=np.int32)
+    R.ref_neigh_half_from_full(g.nlocal, g.nghost, g.x, foff, fnb, hoff, hnb.ctypes.data)
+    t_build = (time.perf_counter() - t0) / 2.0
+    rho_all, e_all, vest = g.gather(s.rho), g.gather(s.e), g.gather(s.v)
+    f = np.zeros((g.nall, 3))
+    drho = np.zeros(g.nall)
+    de = np.zeros(g.nall)
+    rho0 = np.array([0.0, *C3_RHO0])
+    c0 = np.array([0.0, 10.0, 10.0])
+    t_m = t_h = 0.0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        R.ref_taitwater_morris(3, 2, g.nlocal, g.nghost, 1, g.x, vest, rho_all, g.type, s.mass,
+                               rho0, c0, visc, cut, hoff, hnb, f, drho, de)
+        t1 = time.perf_counter()
+        R.ref_heatconduction(3, 2, g.nlocal, g.nghost, 1, g.x, e_all, rho_all, g.type, s.mass,
+                             alpha, cut, hoff, hnb, de)
+        t2 = time.perf_counter()
+        t_m += (t1 - t0) / steps
+        t_h += (t2 - t1) / steps
+    per_step = t_m + t_h + t_build / 10.0
+    return {"value": s.n / per_step, "unit": "particle-steps/s", "cores": 1,
+            "kind": "reference",
+            "sample": f"reference USER-SPH compute code (oracle/_ref, g++ -O3) on {s.n} "
+                      f"particles, same C3 inputs: PairSPHTaitwaterMorris::compute {t_m:.3f} s "
+                      f"+ PairSPHHeatConduction::compute {t_h:.3f} s per step (mean of {steps}) "
+                      f"+ Neighbor::full_bin + half_from_full_newton {t_build:.2f} s amortised "
+                      f"over neigh_every=10; comm/integrate not included"}
+
+
+def c3_main(args, sph):
+    """Config 3 (BASELINE.json configs[2]): 1M particles, two types, sph/taitwater/morris +
+    sph/heatconduction, the device-resident engine step on one GPU."""
+    n = args.edge
+    x, v, t, rho, e, cv = c3_system(n)
+    eng = sph.Engine(c3_config(sph, n))
+    eng.set_atoms(x, v, t, rho, e, cv)
+    eng.setup()
+    eng.run(args.warmup)
+    eng.sync()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    eng.run(args.steps)
+    eng.sync()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    nloc = st["nlocal"]
+    n_half = st["nbr_full"] / max(nloc, 1) / 2.0
+    # SURVEY.md 8(d) C3: morris 104 + 4 N_h, heat 56 + 4 N_h (fused here into one pass)
+    bytes_pass = 160.0 + 8.0 * n_half
+    ms_pass = st["ms_tait"] / max(st["n_tait"], 1)
+    ach = bytes_pass * nloc / (ms_pass * 1e-3) / 1e9
+    out = {
+        "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
+        "value": n ** 3 * args.steps / elapsed,
+        "unit": "particle-steps/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (jittered sc lattice, Bernoulli(0.5) types, gaussian velocities, seeded)",
+        "config": {"workload": f"C3: {n ** 3} particles cubic lattice, two types, "
+                               "sph/taitwater/morris + sph/heatconduction, periodic, skin 0.3, "
+                               "rebuild every 10",
+                   "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
+                   "n_half_per_particle": n_half, "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm",
+                     "kernel": "k_row2_force<MORRIS, TAIT|HEAT> (taitwater/morris + "
+                               "heatconduction, one fused pass)",
+                     "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": ach / PEAK_HBM_GBS, "traffic": None,
+                     "bytes_per_particle": bytes_pass, "ms_per_launch": ms_pass},
+        "kernels": {"neighbor_build_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
+                    "integrate_ms_per_step": st["ms_integrate"] / args.steps,
+                    "comm_ms_per_step": st["ms_comm"] / args.steps},
+    }
+    if not args.no_cpu:
+        cb = c3_cpu_baseline(args.cpu_n)
+        if cb is not None:
+            out["cpu_baseline"] = cb
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
 # ---- C5 multiphase pair passes (SURVEY.md 8(d) C5 physics, 8(a) rows a6-a8 + 8(f) rank 2) --
 def kd_lists(x, rc):
     """Full and half (i < j) CSR lists of all pairs within rc (k-d tree; open boundaries)."""
@@ -447,8 +593,9 @@ def main():
                          "C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
-    ap.add_argument("--workload", choices=["c2", "c2pair", "c5pair"], default="c2",
-                    help="c2: the headline engine step (default); c2pair: rhosum + taitwater "
+    ap.add_argument("--workload", choices=["c2", "c3", "c2pair", "c5pair"], default="c2",
+                    help="c2: the headline engine step (default); c3: two-phase Morris + "
+                         "heat conduction engine step (config 3); c2pair: rhosum + taitwater "
                          "through the pair-style layer; c5pair: the multiphase pair passes "
                          "through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
@@ -475,6 +622,9 @@ def main():
         args.edge = args.edge or 80
         return (c2_pair_main if args.workload == "c2pair" else c5_pair_main)(args, sph)
     args.edge = args.edge or 100
+    if args.workload == "c3":
+        assert world == 1, "the C3 workload runs on one GPU"
+        return c3_main(args, sph)
     dev = local % ndev
 
     pg = procgrid_for(world)

@@ -119,6 +119,12 @@ static int row2_exp() {
 // loopback it measured 1.29 (serial) -> 1.35 ms per step at C2 1M: the split launches
 // cost more than the loopback halo they hide.  Whether xGMI transfers (~17 MB per step
 // per rank at C4) change that is unmeasured here (no multi-GPU box) -> off by default.
+// SPH_TBITS (default 1): with several types, strided list entries carry the neighbour's
+// type in their top bits, so the row2 passes skip the per-neighbour type gather
+static bool tbits_env() {
+  static bool v = env_int("SPH_TBITS", 1) != 0;
+  return v;
+}
 // (read per engine at sph_engine_create)
 static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
 
@@ -210,6 +216,7 @@ struct sph_engine {
   int list_stride = 0;
   int list_perm_g = 0;     // strided rows stored chunk-transposed for G-lane rows (tpos)
   int list_perm_pi = 0;    // ... with pair-interleaved entry slots
+  bool list_tbits = false; // strided entries carry the neighbour's type (SPH_TBIT_SHIFT)
   // this step's in-cut ("tight") list, written by the rhosum pass for the force pass
   DBuf<int> tnbr, tcnt;
   // cluster-pair path (kernel_path 3): rows of CL_CI consecutive owned atoms, fixed
@@ -824,7 +831,7 @@ struct sph_engine {
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,   \
-                     list_perm_pi)
+                     list_perm_pi, (stride > 0 && list_tbits) ? 1 : 0)
         if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
         else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
@@ -846,6 +853,7 @@ struct sph_engine {
       // rows stored chunk-transposed for the row2 kernels' 16-B index loads (k_neigh3 only)
       list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3()) ? row2_iv_g() : 0;
       list_perm_pi = row2_pi() ? 1 : 0;
+      list_tbits = !nt1() && tbits_env() && neigh_q() == 2 && neigh3();
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -857,6 +865,7 @@ struct sph_engine {
       }
     }
     strided = false;
+    list_tbits = false;
     launch(false, 0);
     hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
     size_t tb2 = 0;
@@ -1275,7 +1284,7 @@ struct sph_engine {
       hipLaunchKernelGGL(k_row_ghost_flags, dim3((unsigned)(((long)n * 8 + 255) / 256)),
                          dim3(256), 0, s, n, nlocal, strided ? nullptr : off.p,
                          strided ? list_stride : 0, ccnt.p, nbr.p, list_perm_g, list_perm_pi,
-                         fl_in.p, fl_bd.p);
+                         (strided && list_tbits) ? 1 : 0, fl_in.p, fl_bd.p);
     n_in = select_flagged(fl_in.p, n, rows_in);
     n_bd = select_flagged(fl_bd.p, n, rows_bd);
     SPH_REQUIRE(n_in + n_bd == n, SPH_HIP_ERUNTIME, "row classification lost rows");
@@ -1385,6 +1394,7 @@ struct sph_engine {
     b.iv = strided && list_perm_g > 0 && list_perm_g == row2_iv_g() &&
            list_perm_pi == (b.pi ? 1 : 0);
     b.exp = row2_exp();
+    b.tbits = strided && list_tbits;
     return b;
   }
   bool use_row2() const {

@@ -509,7 +509,8 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
          const int *__restrict__ tb, const int *__restrict__ beg,
          const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-         int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g, int perm_pi) {
+         int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g, int perm_pi,
+         int tbits) {
   constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
   __shared__ double s_cns[NT2];
   __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
@@ -593,7 +594,11 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
-        if (hit && qq < cap) row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] = (int)xj[u].w;
+        // tbits (strided rows, several types): the neighbour's type rides in the entry's
+        // bits 28-30 (SPH_TBIT_SHIFT), so the pair passes need no type gather
+        if (hit && qq < cap)
+          row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] =
+              (int)xj[u].w | (tbits ? (tj[u] - 1) << SPH_TBIT_SHIFT : 0);
         pos += __popcll(m);
       } else {
         n += hit ? 1 : 0;
@@ -694,7 +699,8 @@ static __global__ void k_add_gravity(int n, StepConst sc, double gx, double gy, 
 static __global__ void __launch_bounds__(256)
 k_row_ghost_flags(int n, int nlocal, const int *__restrict__ off, int stride,
                   const int *__restrict__ rcnt, const int *__restrict__ nbr, int perm_g,
-                  int perm_pi, unsigned char *__restrict__ in, unsigned char *__restrict__ bd) {
+                  int perm_pi, int tbits, unsigned char *__restrict__ in,
+                  unsigned char *__restrict__ bd) {
   constexpr int G = 8;
   const int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
@@ -707,7 +713,8 @@ k_row_ghost_flags(int n, int nlocal, const int *__restrict__ off, int stride,
   bool ghost = false;
   for (int e = lane; e < cnt; e += G) {
     const int q = (stride > 0 && perm_g > 0) ? tpos(e, perm_g, perm_pi) : e;
-    ghost |= nbr[beg + q] >= nlocal;
+    const int j = nbr[beg + q];
+    ghost |= (tbits ? (j & SPH_TBIT_MASK) : j) >= nlocal;
   }
   const unsigned long long m = __ballot(ghost);
   const int gbase = (threadIdx.x & 63) & ~(G - 1);

@@ -27,6 +27,11 @@ namespace sph {
 
 constexpr int MAXT = SPH_MAXTYPES;
 constexpr int NT2 = (MAXT + 1) * (MAXT + 1);
+// typed neighbour-list entries: atom index below bit 28, type-1 in bits 28-30 (row2_fits
+// bounds nall by 2^26; SPH_MAXTYPES = 8 needs 3 bits)
+#define SPH_TBIT_SHIFT 28
+#define SPH_TBIT_MASK 0x0FFFFFFF
+static_assert(MAXT - 1 < 8, "type bits hold 3 bits");
 
 // per type-pair coefficient records (index it*(ntypes+1)+jt)
 struct RhoPair {   // sph/rhosum, quadric kernel (pair_sph_rhosum.cpp:172-192)

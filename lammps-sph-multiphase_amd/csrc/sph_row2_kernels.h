@@ -40,6 +40,16 @@
 namespace sph {
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+// Typed list entries (k_neigh3 tbits): atom index in bits 0-27, type-1 in bits 28-30.
+// Slots past a row's end may hold anything: the decoded type is clamped to ntypes so the
+// coefficient lookup of a masked slot stays inside the loaded table.
+__device__ __forceinline__ unsigned ent_atom(unsigned e, bool tb) {
+  return tb ? (e & (unsigned)SPH_TBIT_MASK) : e;
+}
+__device__ __forceinline__ int ent_type(unsigned e, int ntypes) {
+  return min((int)(e >> SPH_TBIT_SHIFT) + 1, ntypes);
+}
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
@@ -151,7 +161,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
               const int *__restrict__ nbr, double4 *__restrict__ xf,
               const int *__restrict__ ty, double4 *__restrict__ vr,
               const Coefs *__restrict__ cf, int *__restrict__ tnbr, int *__restrict__ tcnt,
-              int pi, const int *__restrict__ rows) {
+              int pi, const int *__restrict__ rows, int tbits) {
   static_assert(!TIGHT || LP, "the tight-list compaction needs wave-uniform trip counts");
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   __shared__ double s_fc[(NT1 || !TIGHT) ? 1 : NT2];
@@ -178,6 +188,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
   const Rsrc rt = make_rsrc(ty, nbytes<int>(nall));
   const int rr = rows ? rows[live ? idx : n - 1] : (live ? idx : n - 1);
   const int row = rr;
+  const bool tb = !NT1 && tbits != 0;
   const double4 xi = xf[rr];
   const int it = NT1 ? 1 : ty[rr];
   const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
@@ -201,15 +212,16 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
 #pragma unroll
     for (int u = 0; u < U; u++) {
       jc[u] = jn[u];
+      const unsigned o = ent_atom((unsigned)jn[u], tb);
       if (LP) {
-        const unsigned jo = swap1((unsigned)jn[u]);
-        const unsigned ja = odd ? jo : (unsigned)jn[u], jb = odd ? (unsigned)jn[u] : jo;
+        const unsigned jo = swap1(o);
+        const unsigned ja = odd ? jo : o, jb = odd ? o : jo;
         const double4 x4 = lp_d4(rx, ja, jb, odd);
         xj[u] = make_double3(x4.x, x4.y, x4.z);
       } else {
-        xj[u] = ld_d3(rx, (unsigned)jn[u] * 32u);
+        xj[u] = ld_d3(rx, o * 32u);
       }
-      tj[u] = NT1 ? 1 : ld_i32(rt, (unsigned)jn[u] * 4u);
+      tj[u] = NT1 ? 1 : (tb ? ent_type((unsigned)jn[u], nt1 - 1) : ld_i32(rt, o * 4u));
     }
     chunk_idx<G, U, IV>(rn, k0 + G * U, lane, el, jn);
 #pragma unroll
@@ -262,7 +274,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
              const double4 *__restrict__ vr, const int *__restrict__ ty,
              const double *__restrict__ en, const Coefs *__restrict__ cf,
              double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-             double gz, int pi, const int *__restrict__ rows) {
+             double gz, int pi, const int *__restrict__ rows, int tbits) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   __shared__ TaitPair s_t[(TAIT && !NT1) ? NT2 : 1];
@@ -288,6 +300,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
   const Rsrc re = make_rsrc(en, HEAT ? nbytes<double>(nall) : 0u);
   const int rr = rows ? rows[live ? idx : n - 1] : (live ? idx : n - 1);
   const int row = rr;
+  const bool tb = !NT1 && tbits != 0;
   const double4 xi = xf[rr];
   const double4 vi = vr[rr];
   const double ei = HEAT ? en[rr] : 0.0;
@@ -312,7 +325,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
     int tj[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const unsigned o = (unsigned)jn[u];
+      const unsigned o = ent_atom((unsigned)jn[u], tb);
       if (EXP == 2) {
         xj[u] = make_double4(xi.x + 0.25 * (double)(o & 7u), xi.y + 0.5,
                              xi.z - 0.125 * (double)(o & 3u), xi.w);
@@ -327,7 +340,7 @@ k_row2_force(int n, int nall, int ntot, const int *__restrict__ off, int stride,
         vj[u] = ld_d4(rv, o * 32u);
       }
       ej[u] = HEAT ? ld_d1(re, o * 8u) : 0.0;
-      tj[u] = NT1 ? 1 : ld_i32(rt, o * 4u);
+      tj[u] = NT1 ? 1 : (tb ? ent_type((unsigned)jn[u], nt1 - 1) : ld_i32(rt, o * 4u));
     }
     chunk_idx<G, U, IV>(rn, k0 + G * U, lane, el, jn);
 #pragma unroll
@@ -413,6 +426,7 @@ struct Row2Args {
   const int *rcnt = nullptr;
   int *tnbr = nullptr, *tcnt = nullptr;  // rhosum: write the tight list here (strided, LP)
   const int *rows = nullptr;             // a.n rows listed here instead of rows 0..a.n-1
+  bool tbits = false;                    // typed list entries (k_neigh3 tbits)
 };
 
 // 32-bit byte offsets of every array the row2 kernels read
@@ -428,11 +442,11 @@ inline void row2_rhosum_kt(bool nt1, hipStream_t s, const Row2Args &b) {
   if (nt1)
     hipLaunchKernelGGL((k_row2_rhosum<G, U, true, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows, b.tbits ? 1 : 0);
   else
     hipLaunchKernelGGL((k_row2_rhosum<G, U, false, LP, IV, TIGHT>), dim3(grid), dim3(256), 0, s,
                        a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.ty, a.vr,
-                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows);
+                       a.cf, b.tnbr, b.tcnt, b.pi ? 1 : 0, b.rows, b.tbits ? 1 : 0);
 }
 template <int G, int U, bool LP, bool IV>
 inline void row2_rhosum_k(bool nt1, hipStream_t s, const Row2Args &b) {
@@ -459,7 +473,8 @@ inline void row2_force_t(hipStream_t s, const Row2Args &b) {
   if (grid == 0) return;
   hipLaunchKernelGGL((k_row2_force<G, U, VISC, MODE, NT1, LP, IV, EXP>), dim3(grid), dim3(256),
                      0, s, a.n, b.nall, b.ntot, a.off, b.stride, b.rcnt, a.nbr, a.xf, a.vr,
-                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz, b.pi ? 1 : 0, b.rows);
+                     a.ty, a.en, a.cf, a.fo, a.de, a.gx, a.gy, a.gz, b.pi ? 1 : 0, b.rows,
+                     b.tbits ? 1 : 0);
 }
 
 template <int G, int U, bool NT1, bool LP, bool IV>

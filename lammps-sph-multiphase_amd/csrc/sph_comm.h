@@ -33,6 +33,13 @@ struct Transport {
   virtual int size() const = 0;
   // exchange one int with two peers (send to dest, receive from src); host-synchronous
   virtual int exchange_count(int nsend, int dest, int src, hipStream_t s) = 0;
+  // the two directions of one dimension at once: send n0 to d0 and n1 to d1, receive from
+  // src0 into nrecv[0] and from src1 into nrecv[1]; host-synchronous
+  virtual void exchange_count2(int n0, int d0, int src0, int n1, int d1, int src1,
+                               hipStream_t s, int nrecv[2]) {
+    nrecv[0] = exchange_count(n0, d0, src0, s);
+    nrecv[1] = exchange_count(n1, d1, src1, s);
+  }
   // exchange device buffers (stream-ordered on s)
   virtual void exchange(const void *sbuf, size_t sbytes, int dest, void *rbuf, size_t rbytes,
                         int src, hipStream_t s) = 0;
@@ -56,7 +63,7 @@ class RcclTransport : public Transport {
  public:
   RcclTransport(const ncclUniqueId &id, int nranks, int rank) : n_(nranks), me_(rank) {
     SPH_NCCL_TRY(ncclCommInitRank(&comm_, nranks, id, rank));
-    SPH_HIP_TRY(hipMalloc(&dcnt_, 2 * sizeof(int)));
+    SPH_HIP_TRY(hipMalloc(&dcnt_, 4 * sizeof(int)));
   }
   ~RcclTransport() override {
     if (dcnt_) (void)hipFree(dcnt_);
@@ -81,6 +88,23 @@ class RcclTransport : public Transport {
     if (sbytes) SPH_NCCL_TRY(ncclSend(sbuf, sbytes, ncclUint8, dest, comm_, s));
     if (rbytes) SPH_NCCL_TRY(ncclRecv(rbuf, rbytes, ncclUint8, src, comm_, s));
     SPH_NCCL_TRY(ncclGroupEnd());
+  }
+  // one RCCL group and one host sync for both directions' counts (sends to the same peer
+  // are matched in posting order, so direction 0 meets direction 0)
+  void exchange_count2(int n0, int d0, int src0, int n1, int d1, int src1, hipStream_t s,
+                       int nrecv[2]) override {
+    int h[4] = {n0, n1, 0, 0};
+    SPH_HIP_TRY(hipMemcpyAsync(dcnt_, h, 2 * sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_NCCL_TRY(ncclGroupStart());
+    SPH_NCCL_TRY(ncclSend(dcnt_, 1, ncclInt32, d0, comm_, s));
+    SPH_NCCL_TRY(ncclRecv(dcnt_ + 2, 1, ncclInt32, src0, comm_, s));
+    SPH_NCCL_TRY(ncclSend(dcnt_ + 1, 1, ncclInt32, d1, comm_, s));
+    SPH_NCCL_TRY(ncclRecv(dcnt_ + 3, 1, ncclInt32, src1, comm_, s));
+    SPH_NCCL_TRY(ncclGroupEnd());
+    SPH_HIP_TRY(hipMemcpyAsync(&h[2], dcnt_ + 2, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    nrecv[0] = h[2];
+    nrecv[1] = h[3];
   }
   // one RCCL group for both directions of a dimension: one launch/sync round instead of two
   void exchange2(const void *s0, size_t sb0, int d0, void *r0, size_t rb0, int src0,

@@ -506,15 +506,20 @@ struct sph_engine {
     }
   }
 
-  // CommBrick::borders over a procgrid (comm_brick.cpp:690-880, maxneed = 1)
+  // CommBrick::borders over a procgrid (comm_brick.cpp:690-880, maxneed = 1).  Both swaps
+  // of a dimension select from the same atoms (owned + earlier dimensions' ghosts), so
+  // their counts travel in one exchange and their records in another; the ghosts of the
+  // lower swap are appended before those of the upper one, as in CommBrick.
   void borders_multi() {
     nghost = 0;
     int nall = nlocal;
     nswap = 0;
     for (int d = 0; d < cfg.dim; d++) {
-      const int nlast = nall;  // both swaps of a dimension scan owned + earlier ghosts
+      const int nlast = nall;
+      Swap *pair[2] = {&swaps[nswap], &swaps[nswap + 1]};
+      nswap += 2;
       for (int dir = 0; dir < 2; dir++) {
-        Swap &sw = swaps[nswap++];
+        Swap &sw = *pair[dir];
         sw.dim = d;
         sw.dir = dir;
         sw.sendproc = procneigh[d][dir];
@@ -536,23 +541,51 @@ struct sph_engine {
           ns = select_flagged(flags.p, nlast, sw.list);
         }
         sw.nsend = ns;
-        const int nr = sw.remote ? tr->exchange_count(ns, sw.sendproc, sw.recvproc, s) : ns;
-        sw.nrecv = nr;
-        sw.firstrecv = nall;
-        cbs.reserve((size_t)(ns > 0 ? ns : 1) * sizeof(BorderRec));
-        cbr.reserve((size_t)(nr > 0 ? nr : 1) * sizeof(BorderRec));
-        if (ns)
-          hipLaunchKernelGGL(k_pack_border, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sw.list.p, d,
-                             sw.shift, xf.p, vr.p, en.p, ty.p, (BorderRec *)cbs.p);
-        swap_move(sw.remote, (size_t)ns * sizeof(BorderRec), sw.sendproc,
-                  (size_t)nr * sizeof(BorderRec), sw.recvproc);
-        if (nr) {
-          ensure_atoms((size_t)nall + nr, true);
-          hipLaunchKernelGGL(k_unpack_border, dim3(blocks(nr)), dim3(BLK), 0, s, nr, nall,
-                             (const BorderRec *)cbr.p, xf.p, vr.p, en.p, ty.p);
-        }
-        nall += nr;
       }
+      Swap &a = *pair[0], &b = *pair[1];
+      if (a.remote) {
+        int nr[2];
+        tr->exchange_count2(a.nsend, a.sendproc, a.recvproc, b.nsend, b.sendproc, b.recvproc,
+                            s, nr);
+        a.nrecv = nr[0];
+        b.nrecv = nr[1];
+      } else {
+        a.nrecv = a.nsend;
+        b.nrecv = b.nsend;
+      }
+      a.firstrecv = nall;
+      b.firstrecv = nall + a.nrecv;
+      const size_t rec = sizeof(BorderRec);
+      const size_t sa = (size_t)a.nsend * rec, sb = (size_t)b.nsend * rec;
+      const size_t ra = (size_t)a.nrecv * rec, rb = (size_t)b.nrecv * rec;
+      const size_t so = (sa + 255) & ~(size_t)255, ro = (ra + 255) & ~(size_t)255;
+      cbs.reserve(std::max<size_t>(so + sb, 1), true, s);
+      cbr.reserve(std::max<size_t>(ro + rb, 1), true, s);
+      for (int dir = 0; dir < 2; dir++) {
+        Swap &sw = *pair[dir];
+        if (sw.nsend)
+          hipLaunchKernelGGL(k_pack_border, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                             sw.list.p, d, sw.shift, xf.p, vr.p, en.p, ty.p,
+                             (BorderRec *)(cbs.p + (dir ? so : 0)));
+      }
+      if (a.remote) {
+        tr->exchange2(cbs.p, sa, a.sendproc, cbr.p, ra, a.recvproc, cbs.p + so, sb, b.sendproc,
+                      cbr.p + ro, rb, b.recvproc, s);
+      } else {
+        if (ra) SPH_HIP_TRY(hipMemcpyAsync(cbr.p, cbs.p, ra, hipMemcpyDeviceToDevice, s));
+        if (rb) SPH_HIP_TRY(hipMemcpyAsync(cbr.p + ro, cbs.p + so, rb, hipMemcpyDeviceToDevice, s));
+      }
+      const int nr = a.nrecv + b.nrecv;
+      if (nr) ensure_atoms((size_t)nall + nr, true);
+      for (int dir = 0; dir < 2; dir++) {
+        Swap &sw = *pair[dir];
+        if (sw.nrecv)
+          hipLaunchKernelGGL(k_unpack_border, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s,
+                             sw.nrecv, sw.firstrecv,
+                             (const BorderRec *)(cbr.p + (dir ? ro : 0)), xf.p, vr.p, en.p,
+                             ty.p);
+      }
+      nall += nr;
     }
     nghost = nall - nlocal;
   }

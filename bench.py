@@ -742,7 +742,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_n)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
+    with stdout_to_stderr():  # communicator teardown
+        eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

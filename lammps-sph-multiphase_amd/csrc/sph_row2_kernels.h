@@ -41,6 +41,15 @@ namespace sph {
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
+// Cache policy of the neighbour-index stream loads: nt (bit 1, non-temporal), so the
+// ~620 MB/pass index stream, read once, does not push the gathered records out of L2.
+// Measured on C2 1M (kernel_sweep, 50 reps): rhosum 0.313 -> 0.302 ms, taitwater
+// 0.560 -> 0.548 ms; sc0|nt (3) 0.305 / 0.553; sc0 on the record gathers instead: 0.305 /
+// 0.561; nontemporal stores of f/drho/de: no gain (profiles/r01/kernels/sweep_cachepolicy.log)
+#ifndef SPH_IDX_AUX
+#define SPH_IDX_AUX 2
+#endif
+
 // Typed list entries (k_neigh3 tbits): atom index in bits 0-27, type-1 in bits 28-30.
 // Slots past a row's end may hold anything: the decoded type is clamped to ntypes so the
 // coefficient lookup of a masked slot stays inside the loaded table.
@@ -133,7 +142,8 @@ template <int G, int U, bool IV>
 __device__ __forceinline__ void chunk_idx(Rsrc rn, int k0, int lane, int el, int (&j)[U]) {
   if (IV) {
     static_assert(!IV || U == 4, "index vectors hold 4 entries");
-    const v4u v = ld_b128(rn, (unsigned)(k0 + 4 * lane) * 4u);
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rn, (unsigned)(k0 + 4 * lane) * 4u, 0,
+                                                        SPH_IDX_AUX);
     j[0] = (int)v.x;
     j[1] = (int)v.y;
     j[2] = (int)v.z;

@@ -1,6 +1,7 @@
 """Benchmark of the MI355X USER-SPH engine on BASELINE.json's headline workload.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 100] [--no-cpu]
+    python bench.py [--gpus N] [--scaling strong|weak] [--steps K] [--warmup W] [--edge 100]
+                    [--no-cpu] [--workload c2|c3|c2pair|c5pair]
 
 Workload (BASELINE.json configs[1]): 1M particles on a jittered 100^3 cubic lattice,
 periodic, hybrid/overlay sph/rhosum (nstep 1, h 3) + sph/taitwater (rho0 1, c0 10,
@@ -8,18 +9,24 @@ visc 0.1, h 3), skin 0.3, neighbor rebuild every 10 steps, dt 1e-3, fix meso.  A
 is one full Verlet step of the device-resident engine (integrate, forward comm or
 rebuild, rhosum, forward rho, taitwater, integrate) with everything already in HBM.
 
-N > 1 ranks (torch.distributed.run, one per GPU) run ONE box decomposed into N bricks
-(CommBrick-style spatial decomposition, halo exchange and migration over RCCL/xGMI): each
-brick holds a 100^3 share, the global box is 100*procgrid per side (weak scaling; N = 8 is
-BASELINE config C4, 200^3 = 8M particles on 2x2x2 GPUs).
+N > 1: one rank per GPU (LAMMPS' CommBrick spatial decomposition, halo exchange and
+migration over RCCL/xGMI).  Without WORLD_SIZE in the environment, `--gpus N` starts the N
+ranks itself (fresh child processes, before anything touches the GPU); under
+torch.distributed.run WORLD_SIZE must equal --gpus.
+  --scaling strong (default): the ONE 1M-particle C2 box split into N bricks (the
+      north star's "1M particles at 1/2/4/8 GPUs"; 125k particles per GPU at N = 8);
+  --scaling weak: every brick holds an edge^3 share of a box edge*procgrid per side
+      (N = 8 is BASELINE config C4: 200^3 = 8M particles on 2x2x2 GPUs).
 Rank 0 prints ONE JSON line.  `roofline` covers the dominant kernel (the taitwater force
 pass), timed live with HIP events recorded on the engine's stream; `cpu_baseline` is the
-oracle's C restatement timed on this host on a bounded sample (rank 0, N = 1 only).
+reference's own compute code timed on this host on a bounded sample (rank 0, N = 1 only).
 """
 import argparse
 import importlib.util
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -79,6 +86,51 @@ def brick_lattice(n, pg, rank, seed=12345):
     return x, v, np.ones(N, np.int32), np.ones(N), np.zeros(N), np.ones(N), tags
 
 
+def strong_lattice(n, pg, rank, seed=12345):
+    """Rank `rank`'s brick of the single-box C2 system (n^3 sites, box [0, n)^3): the atoms
+    whose position falls in the brick (uniform split, bricks numbered x fastest); the
+    union over ranks is exactly make_system(n).  Tags are the global site indices."""
+    x, v, t, rho, e, cv, tags = brick_lattice(n, (1, 1, 1), 0, seed)
+    loc = np.array((rank % pg[0], (rank // pg[0]) % pg[1], rank // (pg[0] * pg[1])))
+    w = np.array([n / p for p in pg])
+    b = np.clip(np.floor(x / w).astype(int), 0, np.array(pg) - 1)
+    sel = (b == loc).all(axis=1)
+    return x[sel], v[sel], t[sel], rho[sel], e[sel], cv[sel], tags[sel]
+
+
+def free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Start n ranks of this script as fresh processes (one per GPU, RANK/LOCAL_RANK/
+    WORLD_SIZE/MASTER_* set as torch.distributed.run would) and wait for them; if one fails
+    the others are stopped.  Returns the exit code.  Nothing here touches the GPU."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:          # exact PIDs we started, never a pattern
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def share_uid(dist, rank, make_uid):
     """RCCL unique id from rank 0 to every rank (torch.distributed object broadcast)."""
     obj = [make_uid() if rank == 0 else None]
@@ -101,13 +153,16 @@ class stdout_to_stderr:
         os.close(self.saved)
 
 
-def c2_config(sph, n, pg=(1, 1, 1), rank=0):
+def c2_config(sph, n, pg=(1, 1, 1), rank=0, strong=False):
+    """C2 physics; the box is n per side split into pg bricks (strong) or n*pg per side
+    (weak: an n^3 share per brick)."""
     h = 3.0
     cut = np.zeros((2, 2))
     cut[1, 1] = h
     visc = np.zeros((2, 2))
     visc[1, 1] = 0.1
-    return sph.make_config(3, 1, [0.0, 0.0, 0.0], [float(n * p) for p in pg], [1, 1, 1],
+    side = [float(n) for p in pg] if strong else [float(n * p) for p in pg]
+    return sph.make_config(3, 1, [0.0, 0.0, 0.0], side, [1, 1, 1],
                            [0.0, 1.0], 0.3, 1e-3, neigh_every=10, rhosum=dict(nstep=1, cut=cut),
                            tait=dict(rho0=np.array([0.0, 1.0]), c0=np.array([0.0, 10.0]),
                                      visc=visc, cut=cut), procgrid=pg, rank=rank)
@@ -586,11 +641,13 @@ def c5_pair_cpu(d):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="N > 1: strong = the one edge^3 box split into N bricks (default); "
+                         "weak = an edge^3 share per GPU (C4 at N = 8)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--edge", type=int, default=None,
-                    help="lattice edge (edge^3 particles per GPU; default 100, c5pair 80: "
-                         "C5's ~0.5M particles per GPU)")
+                    help="lattice edge (default 100; c5pair 80: C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
     ap.add_argument("--workload", choices=["c2", "c3", "c2pair", "c5pair"], default="c2",
@@ -599,14 +656,21 @@ def main():
                          "through the pair-style layer; c5pair: the multiphase pair passes "
                          "through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
-                    help="pair-kernel path: 0 = LDS-staged bins, 1 = CSR rows")
+                    help="pair-kernel path (sph_engine_config.kernel_path)")
     ap.add_argument("--comm-loopback", action="store_true",
                     help="one GPU: route the periodic self swaps through a one-rank RCCL "
                          "communicator (send/recv to itself) -- the multi-GPU halo path's cost "
                          "without the xGMI transfer")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="host path only (rank launch, decomposition, timing reduction), no "
+                         "HIP device: prints the JSON line with value null")
     args = ap.parse_args()
+    assert args.gpus >= 1
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == args.gpus, f"WORLD_SIZE={world} but --gpus {args.gpus}"
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -614,9 +678,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
-    sph = load_pkg()
-    ndev = sph.device_count()
-    assert ndev > 0, "bench.py needs a HIP device"
+    sph = None if args.dry_run else load_pkg()
+    ndev = 0 if args.dry_run else sph.device_count()
+    assert args.dry_run or ndev > 0, "bench.py needs a HIP device"
     if args.workload in ("c2pair", "c5pair"):
         assert world == 1, "the pair-layer workloads run on one GPU"
         args.edge = args.edge or 80
@@ -625,12 +689,77 @@ def main():
     if args.workload == "c3":
         assert world == 1, "the C3 workload runs on one GPU"
         return c3_main(args, sph)
-    dev = local % ndev
+    dev = local % max(ndev, 1)
 
+    strong = args.scaling == "strong" and world > 1
     pg = procgrid_for(world)
-    x, v, t, rho, e, cv, tags = brick_lattice(args.edge, pg, rank)
-    cfg = c2_config(sph, args.edge, pg, rank)
-    cfg.kernel_path = args.path if world == 1 else 1
+    if strong:
+        x, v, t, rho, e, cv, tags = strong_lattice(args.edge, pg, rank)
+        n_total = args.edge ** 3
+    else:
+        x, v, t, rho, e, cv, tags = brick_lattice(args.edge, pg, rank)
+        n_total = args.edge ** 3 * world
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(val):
+        if dist is None:
+            return val
+        import torch
+        tt = torch.tensor([val], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    if strong:
+        workload = (f"C2 strong scaling: one {args.edge}^3 = {n_total} particle cubic lattice "
+                    f"split into {pg[0]}x{pg[1]}x{pg[2]} bricks (~{n_total // world} per GPU), "
+                    "sph/rhosum + sph/taitwater, periodic, skin 0.3, rebuild every 10")
+    elif world > 1:
+        workload = (f"C2 weak scaling: {args.edge ** 3} particles/GPU, one "
+                    f"{args.edge * pg[0]}x{args.edge * pg[1]}x{args.edge * pg[2]} box in "
+                    f"{pg[0]}x{pg[1]}x{pg[2]} bricks (BASELINE C4 at 8 GPUs), sph/rhosum + "
+                    "sph/taitwater, periodic, skin 0.3, rebuild every 10")
+    else:
+        workload = (f"C2: {args.edge ** 3} particles cubic lattice, sph/rhosum + "
+                    "sph/taitwater, periodic, skin 0.3, rebuild every 10")
+    parallelism = (("single GPU, halos through RCCL loopback" if args.comm_loopback
+                    else "single GPU") if world == 1 else
+                   f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo exchange + "
+                   "migration, one rank per GPU")
+    base = {
+        "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
+        "unit": "particle-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (jittered sc lattice, gaussian velocities, seeded)",
+    }
+
+    if args.dry_run:
+        counts = [None] * world
+        if dist is not None:
+            dist.all_gather_object(counts, int(x.shape[0]))
+        else:
+            counts = [int(x.shape[0])]
+        barrier()
+        elapsed = max_over_ranks(0.0)
+        if rank == 0:
+            out = dict(base, value=None, ms_per_step=elapsed, dry_run=True,
+                       config={"workload": workload, "parallelism": parallelism,
+                               "particles_per_rank": counts, "particles_total": sum(counts)})
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    cfg = c2_config(sph, args.edge, pg, rank, strong=strong)
+    cfg.kernel_path = args.path
     eng = sph.Engine(cfg, device=dev)
     eng.set_atoms(x, v, t, rho, e, cv)
     if world > 1:
@@ -646,10 +775,6 @@ def main():
         eng.run(args.warmup)
     eng.sync()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     barrier()
     eng.sync()
     eng.set_timing(True)
@@ -658,16 +783,11 @@ def main():
     eng.sync()
     t1 = time.perf_counter()
     barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(t1 - t0)
     st = eng.stats()
 
     nloc = st["nlocal"]
-    total_ps = args.edge ** 3 * world * args.steps / elapsed
+    total_ps = n_total * args.steps / elapsed
     n_full = st["nbr_full"] / max(nloc, 1)
     n_half = n_full / 2.0
     # algorithmic bytes per particle per pass (half-list CSR, int32, fp64)
@@ -678,66 +798,30 @@ def main():
     ach_tait = bytes_tait * nloc / (ms_tait * 1e-3) / 1e9
     ach_rho = bytes_rho * nloc / (ms_rho * 1e-3) / 1e9
     ach_pair = (bytes_tait + bytes_rho) * nloc / ((ms_tait + ms_rho) * 1e-3) / 1e9
-
-    out = {
-        "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
-        "value": total_ps,
-        "unit": "particle-steps/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (jittered sc lattice, gaussian velocities, seeded)",
-        "config": {"workload": (f"C2: {args.edge ** 3} particles/GPU cubic lattice, sph/rhosum + "
-                                "sph/taitwater, periodic, skin 0.3, rebuild every 10")
-                               + ("" if world == 1 else
-                                  f"; one {args.edge * pg[0]}x{args.edge * pg[1]}x{args.edge * pg[2]} box "
-                                  f"in {pg[0]}x{pg[1]}x{pg[2]} bricks (C4 at 8 GPUs)"),
-                   "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
-                   "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "parallelism": (("single GPU, halos through RCCL loopback"
-                                    if args.comm_loopback else "single GPU") if world == 1 else
-                                   f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo "
-                                   "exchange + migration, one rank per GPU"),
-                   "kernel_path": {1: "lds-staged bins", 2: "lds tiles"}.get(st["staged"],
-                                                                             "csr rows")},
-        "roofline": {"bound": "hbm",
-                     "kernel": {1: "k_bin_force", 2: "k_tile_force"}.get(st["staged"], "k_row2_force")
-                     + "<TAIT> (sph/taitwater pass)",
-                     "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,
-                     "bytes_per_particle": bytes_tait, "ms_per_launch": ms_tait},
-        "kernels": {"rhosum": {"ms_per_launch": ms_rho, "achieved_GBs": ach_rho,
-                               "bytes_per_particle": bytes_rho},
-                    "rhosum+taitwater": {"achieved_GBs": ach_pair,
-                                         "frac": ach_pair / PEAK_HBM_GBS,
-                                         "kernel_particle_steps_per_s":
-                                             nloc / ((ms_tait + ms_rho) * 1e-3)},
-                    "neighbor_build_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
-                    "integrate_ms_per_step": st["ms_integrate"] / args.steps,
-                    "comm_ms_per_step": st["ms_comm"] / args.steps},
-    }
-    # HBM traffic per launch of the roofline kernel from PMC counters (tools/pmc_traffic.sh
-    # on this same command; FETCH_SIZE x2 + WRITE_SIZE), if a summary for it is committed
-    tj = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    if os.path.exists(tj):
-        # the instantiation of the roofline kernel with the most profiled launches (the
-        # steady-state one: strided list after the first rebuild)
-        kname = out["roofline"]["kernel"].split(" ")[0].split("<")[0]
-        best = None
-        for k, v in json.load(open(tj)).items():
-            if k.split("<")[0].split("::")[-1] == kname and v.get("traffic_bytes"):
-                if best is None or v["launches"][0] > best["launches"][0]:
-                    best = v
-        if best is not None:
-            out["roofline"]["traffic"] = best["traffic_bytes"] / 1e9
-            out["roofline"]["traffic_unit"] = ("GB per launch (PMC: 2*FETCH_SIZE + WRITE_SIZE, "
-                                               "tools/pmc_traffic.sh)")
-            out["roofline"]["algorithmic_GB_per_launch"] = bytes_tait * nloc / 1e9
+    kname = {1: "k_bin_force", 2: "k_tile_force", 5: "k_blk_force"}.get(st["staged"],
+                                                                      "k_row2_force")
+    out = dict(base, value=total_ps, ms_per_step=elapsed / args.steps * 1e3)
+    out["config"] = {"workload": workload,
+                     "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
+                     "n_full_per_particle": n_full, "n_half_per_particle": n_half,
+                     "parallelism": parallelism,
+                     "kernel_path": {1: "lds-staged bins", 2: "lds tiles",
+                                     5: "block-staged unions (LDS)"}.get(st["staged"],
+                                                                         "csr rows")}
+    out["roofline"] = {"bound": "hbm", "kernel": kname + "<TAIT> (sph/taitwater pass)",
+                       "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                       "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,
+                       "bytes_per_particle": bytes_tait, "ms_per_launch": ms_tait}
+    out["kernels"] = {"rhosum": {"ms_per_launch": ms_rho, "achieved_GBs": ach_rho,
+                                 "bytes_per_particle": bytes_rho},
+                      "rhosum+taitwater": {"achieved_GBs": ach_pair,
+                                           "frac": ach_pair / PEAK_HBM_GBS,
+                                           "kernel_particle_steps_per_s":
+                                               nloc / ((ms_tait + ms_rho) * 1e-3)},
+                      "neighbor_build_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
+                      "integrate_ms_per_step": st["ms_integrate"] / args.steps,
+                      "comm_ms_per_step": st["ms_comm"] / args.steps}
+    attach_pmc_traffic(out, kname, bytes_tait * nloc, world, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n)
     if rank == 0:
@@ -746,6 +830,33 @@ def main():
         eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def attach_pmc_traffic(out, kname, alg_bytes, world, args):
+    """HBM traffic per launch of the roofline kernel from PMC counters, measured on THIS
+    workload by tools/pmc_traffic.sh and committed as profiles/<round>/pmc_traffic.json with
+    the kernel, config and commit it was taken on.  Attached as `traffic` only when that
+    record matches this run (same kernel family, single GPU, same lattice edge and steps);
+    otherwise it is omitted (traffic null) rather than reported from another configuration."""
+    for rnd in ("r02",):
+        tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        if not os.path.exists(tj):
+            continue
+        rec = json.load(open(tj))
+        meta = rec.get("_meta", {})
+        if (meta.get("world") != world or meta.get("edge") != args.edge
+                or meta.get("path") != args.path):
+            continue
+        for k, v in rec.items():
+            if k.startswith("_"):
+                continue
+            if k.split("<")[0].split("::")[-1] == kname and v.get("traffic_bytes"):
+                out["roofline"]["traffic"] = v["traffic_bytes"] / 1e9
+                out["roofline"]["traffic_unit"] = (
+                    f"GB per launch (PMC 2*FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.sh, "
+                    f"profiles/{rnd}/pmc_traffic.json, commit {meta.get('commit', '?')})")
+                out["roofline"]["algorithmic_GB_per_launch"] = alg_bytes / 1e9
+                return
 
 
 if __name__ == "__main__":

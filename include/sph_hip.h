@@ -299,6 +299,9 @@ int sph_engine_sync(sph_engine *e);
 /* run only the pair passes (rhosum + forward comm + taitwater [+heat]) n times on the
    current state, no integration or rebuild: the kernel-roofline workload */
 int sph_engine_pair_passes(sph_engine *e, int n);
+/* run only the neighbour rebuild (pbc, spatial sort, borders, bins, list) n times on the
+   current positions: the list-build workload (timed under the neighbour class) */
+int sph_engine_rebuild_passes(sph_engine *e, int n);
 
 #ifdef __cplusplus
 }

@@ -128,6 +128,7 @@ EXPORTS = {
     "sph_engine_set_timing": (_i, [_vp, _i]),
     "sph_engine_sync": (_i, [_vp]),
     "sph_engine_pair_passes": (_i, [_vp, _i]),
+    "sph_engine_rebuild_passes": (_i, [_vp, _i]),
 }
 
 
@@ -427,6 +428,9 @@ class Engine:
 
     def pair_passes(self, n):
         _chk(self.L.sph_engine_pair_passes(self.h, n))
+
+    def rebuild_passes(self, n):
+        _chk(self.L.sph_engine_rebuild_passes(self.h, n))
 
     def sync(self):
         _chk(self.L.sph_engine_sync(self.h))

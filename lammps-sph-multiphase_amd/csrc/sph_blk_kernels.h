@@ -1,0 +1,759 @@
+// sph_blk_kernels.h -- block-staged pair passes of the engine (production path).
+//
+// What bounds a gather-per-pair walk of the full list on gfx950 is the texture addresser
+// (TA): every pair fetches its neighbour's 32-B records from L2 and the TA prices each
+// wave instruction by the distinct 128-B lines it touches (round-1 row2
+// kernels: TA_BUSY 93 %, 338 TA cycles per particle per taitwater pass).  Here the gathers
+// move into LDS:
+//
+//  * a BLOCK is R consecutive owned rows (Morton order, so a compact region of space);
+//    its UNION is the sorted set of atoms (owned or ghost) that appear in any of its rows'
+//    full-list entries -- at C2 (R = 64, h = 3 dx) about 950 atoms against 64 x 155
+//    entries, so each record is loaded ~10x less often than by per-pair gathers;
+//  * at every rebuild k_blk_build turns the block's rows into 16-bit SLOTS (positions in
+//    the union), each row's slots sorted ascending (atom order: lanes of a row read
+//    mostly consecutive LDS records) and stored chunk-transposed like the row2 list, so a
+//    lane's four slots of a chunk are one 8-byte load.  The index stream of a pass halves
+//    (2 B per entry instead of 4);
+//  * each pass stages its block's union records into LDS with coalesced loads (the union
+//    is sorted by atom index, so a wave's loads hit consecutive records), then the rows'
+//    G lanes walk their slot lists reading neighbour records from LDS (ds_read_b128).
+//
+// Pair arithmetic is the row2 kernels' (sph_row2_kernels.h: v_rcp/v_rsq seeds with one
+// Newton step, masked slots get a zero kernel weight), so results agree with the row
+// path to rounding of the summation order.  Reference semantics: rhosum
+// pair_sph_rhosum.cpp:116-195 (full list, strict rsq < cutsq), taitwater
+// pair_sph_taitwater.cpp:117-191, morris pair_sph_taitwater_morris.cpp:156-191,
+// heatconduction pair_sph_heatconduction.cpp:106-129 -- each pair evaluated from both
+// sides of the full list (Newton's third law by symmetry, no scatter, no atomics).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "sph_engine_kernels.h"
+#include "sph_row2_kernels.h"
+#include "sph_util.h"
+
+namespace sph {
+
+constexpr int BLK_TPR = 16;     // lanes per row of k_blk_neigh
+
+// exclusive prefix sum over the BT threads of a workgroup (BT/64 waves); *total = sum
+template <int BT>
+__device__ __forceinline__ int blk_scan(int v, int *s_w, int *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < BT / 64; k++) {
+    const int t = s_w[k];
+    base += (k < w) ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// Chunk-transposed slot rows: entry u*G + l of a U*G-entry chunk (taken by lane l of the
+// row's G lanes) is stored at U*l + u, so a lane's U slots of a chunk are one load.
+template <int G, int U>
+__host__ __device__ __forceinline__ int blk_tpos(int q) {
+  const int c = q % (U * G);
+  return q - c + U * (c % G) + c / G;
+}
+
+// ---- block neighbour build from the bins ------------------------------------------------
+// One 256-thread workgroup per block of R rows builds the block's rows DIRECTLY in slot
+// form, without a global-index list: Neighbor::full_bin membership (neigh_full.cpp:241-344:
+// every j != i with rsq <= cutneighsq[it][jt]) over the half-size bins of k_neigh3.
+//  1. each row trims its 5x5 (dz, dy) bin-rows to the x-range that can hold a point within
+//     cutneighmax (k_neigh3's conservative slab test); the block's CANDIDATES are, per
+//     bin-row, the union of its rows' x-ranges -- one contiguous range of the bin-sorted
+//     copy xb per bin-row, numbered in bin order;
+//  2. the candidates are staged in LDS BLK_WIN at a time (coalesced loads from xb); each
+//     row's lanes walk only the row's OWN trimmed ranges (sub-ranges of the block's, so the
+//     same ~N_f/0.7 tests per row as k_neigh3) and set a hit bit per candidate;
+//  3. the union is the candidates some row hit, numbered in candidate order (slot = rank
+//     among used candidates); each row's slots come out of its bitmap in ascending order.
+// Candidate ORDER differs from full_bin's (bins are scanned per block), which changes only
+// the summation order of the pair passes.  Overflows (> BLK_MCAP candidates, or a block
+// whose bin box exceeds the bin-row table) raise *ovf; the host then takes the row path.
+constexpr int BLK_MCAP = 4096;  // candidates per block (hit bitmaps; 12-bit slots)
+constexpr int BLK_WIN = 512;    // candidates staged in LDS at a time
+constexpr int BLK_TBL = 256;    // bin-rows per block
+
+template <int R, int G, int U, bool NT1>
+__global__ void __launch_bounds__(R * BLK_TPR)
+k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *__restrict__ ty,
+            const double4 *__restrict__ xb, const int *__restrict__ tb,
+            const int *__restrict__ qbeg, const Coefs *__restrict__ cf, int ucap, int sstride,
+            int *__restrict__ ulist, int *__restrict__ ucnt, int *__restrict__ rcnt,
+            unsigned short *__restrict__ snbr, int *__restrict__ ovf, int *__restrict__ umax,
+            int bexp) {
+  // bexp (study, SPH_BEXP; outputs meaningless): 1 = no candidate loads, 2 = no row
+  // tests, 4 = no slot-row stores, 8 = no union stores
+  constexpr int TPR = BLK_TPR, BLK_BT = R * TPR;
+  constexpr int W = BLK_MCAP / 32;
+  constexpr int RB = 2, NB = (2 * RB + 1) * (2 * RB + 1);
+  static_assert(BLK_BT <= 1024 && BLK_BT >= BLK_TBL && (TPR & (TPR - 1)) == 0, "block shape");
+  __shared__ double2 s_cxy[BLK_WIN];
+  __shared__ double s_cz[BLK_WIN];
+  __shared__ int s_cid[BLK_WIN];
+  __shared__ unsigned char s_ct[NT1 ? 1 : BLK_WIN];
+  __shared__ unsigned s_bm[R][W];
+  __shared__ unsigned s_used[W];
+  __shared__ int s_upre[W + 1];
+  __shared__ int s_x0[BLK_TBL], s_x1[BLK_TBL], s_pre[BLK_TBL + 1], s_st[BLK_TBL];
+  __shared__ int s_rc[R][NB];       // first candidate of each of the row's bin-row ranges
+  __shared__ int s_rl[R][NB];       // its length
+  __shared__ int s_lim[6];          // min/max bin y, z of the rows
+  __shared__ double s_cns[NT1 ? 1 : NT2];
+  __shared__ int s_w[BLK_BT / 64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int r = tid / TPR, sub = tid % TPR;
+  const int row = b * R + r;
+  const bool live = row < n;
+  const int nt1 = cf->ntypes + 1;
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += BLK_BT) s_cns[t] = cf->cutneighsq[t];
+  if (tid < 6) s_lim[tid] = (tid & 1) ? -0x7fffffff : 0x7fffffff;
+  for (int t = tid; t < BLK_TBL; t += BLK_BT) {
+    s_x0[t] = 0x7fffffff;
+    s_x1[t] = -1;
+  }
+  __syncthreads();
+  const double4 xi = xf[live ? row : 0];
+  const int it = NT1 ? 1 : ty[live ? row : 0];
+  const int cx = bin_coord(xi.x, q.lo[0], q.inv[0], q.nb[0]);
+  const int cy = bin_coord(xi.y, q.lo[1], q.inv[1], q.nb[1]);
+  const int cz = bin_coord(xi.z, q.lo[2], q.inv[2], q.nb[2]);
+  (void)cx;
+  if (live && sub == 0) {
+    atomicMin(&s_lim[0], cy);
+    atomicMax(&s_lim[1], cy);
+    atomicMin(&s_lim[2], cz);
+    atomicMax(&s_lim[3], cz);
+  }
+  __syncthreads();
+  const int y0 = s_lim[0] - RB, z0 = (dim == 3) ? s_lim[2] - RB : cz;
+  const int ny = s_lim[1] - s_lim[0] + 2 * RB + 1;
+  const int nz = (dim == 3) ? s_lim[3] - s_lim[2] + 2 * RB + 1 : 1;
+  if (ny * nz > BLK_TBL) {  // workgroup-uniform
+    if (tid == 0) atomicMax(ovf, 1 << 20);
+    return;
+  }
+  // 1) per-row trimmed bin-row x-ranges (kept per row: table entry, bx0, bx1), merged per
+  // block bin-row
+  const int nbr_rows = (dim == 3) ? NB : (2 * RB + 1);
+  int myt[(NB + TPR - 1) / TPR], mx0[(NB + TPR - 1) / TPR], mx1[(NB + TPR - 1) / TPR];
+#pragma unroll
+  for (int k = 0; k < (NB + TPR - 1) / TPR; k++) {
+    const int br = sub + k * TPR;
+    myt[k] = -1;
+    mx0[k] = 0;
+    mx1[k] = -1;
+    if (!live || br >= nbr_rows) continue;
+    const int bz = (dim == 3) ? cz - RB + br / (2 * RB + 1) : cz;
+    const int by = cy - RB + br % (2 * RB + 1);
+    if (bz < 0 || bz >= q.nb[2] || by < 0 || by >= q.nb[1]) continue;
+    const double gz = (dim == 3) ? slab_gap(xi.z, bz, cz, q.lo[2], q.size[2]) : 0.0;
+    const double gy = slab_gap(xi.y, by, cy, q.lo[1], q.size[1]);
+    const double d2 = gy * gy + gz * gz;
+    if (d2 > q.cutmaxsq) continue;
+    const double ext = sqrt(q.cutmaxsq - d2) * (1.0 + 1e-9) + 1e-9 * q.size[0];
+    const int bx0 = bin_coord(xi.x - ext, q.lo[0], q.inv[0], q.nb[0]);
+    const int bx1 = bin_coord(xi.x + ext, q.lo[0], q.inv[0], q.nb[0]);
+    const int t = (bz - z0) * ny + (by - y0);
+    myt[k] = t;
+    mx0[k] = bx0;
+    mx1[k] = bx1;
+    atomicMin(&s_x0[t], bx0);
+    atomicMax(&s_x1[t], bx1);
+  }
+  __syncthreads();
+  // 2) candidate ranges (one per table entry, in linear bin order) and their prefix
+  int len = 0, st = 0;
+  if (tid < ny * nz && s_x1[tid] >= s_x0[tid]) {
+    const int bz = z0 + tid / ny, by = y0 + tid % ny;
+    const int brow = (bz * q.nb[1] + by) * q.nb[0];
+    st = qbeg[brow + s_x0[tid]];
+    len = qbeg[brow + s_x1[tid] + 1] - st;
+  }
+  int M = 0;
+  const int pre = blk_scan<BLK_BT>(len, s_w, &M);
+  if (M > BLK_MCAP) {
+    if (tid == 0) atomicMax(ovf, M);
+    return;
+  }
+  if (tid < BLK_TBL) {
+    s_pre[tid] = pre;
+    s_st[tid] = st;
+  }
+  if (tid == 0) s_pre[BLK_TBL] = M;
+  for (int t = tid; t < R * W; t += BLK_BT) (&s_bm[0][0])[t] = 0u;
+  __syncthreads();
+  // the row's ranges in candidate numbering: xb positions [qbeg(bx0), qbeg(bx1 + 1)) of
+  // bin-row t sit at candidates s_pre[t] + (pos - s_st[t])
+#pragma unroll
+  for (int k = 0; k < (NB + TPR - 1) / TPR; k++) {
+    const int br = sub + k * TPR;
+    if (br >= NB) continue;
+    int c0 = 0, ln = 0;
+    if (myt[k] >= 0) {
+      const int t = myt[k];
+      const int bz = z0 + t / ny, by = y0 + t % ny;
+      const int brow = (bz * q.nb[1] + by) * q.nb[0];
+      const int a = qbeg[brow + mx0[k]];
+      c0 = s_pre[t] + (a - s_st[t]);
+      ln = qbeg[brow + mx1[k] + 1] - a;
+    }
+    s_rc[r][br] = c0;
+    s_rl[r][br] = ln;
+  }
+  int cntr = 0;  // the row's hits (this lane's share)
+  // 3) candidates staged BLK_WIN at a time; the row's lanes walk each of the row's ranges
+  // (a contiguous run of candidates, clipped to the window) and set a bit per hit
+  const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
+  const double *const crow = s_cns + (NT1 ? 0 : it * nt1);
+  for (int p0 = 0; p0 < M; p0 += BLK_WIN) {
+    const int pn = min(M - p0, BLK_WIN);
+    __syncthreads();  // (the previous window's tests are done; s_rc/s_rl are visible)
+#pragma unroll 2
+    for (int pw = tid; pw < pn; pw += BLK_BT) {
+      const int p = p0 + pw;
+      int lo = 0, hi = BLK_TBL - 1;  // last table entry with s_pre <= p (a non-empty range)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= p) lo = mid;
+        else hi = mid - 1;
+      }
+      const int pos = s_st[lo] + (p - s_pre[lo]);
+      if (bexp & 1) continue;
+      const double4 c = xb[pos];
+      s_cxy[pw] = make_double2(c.x, c.y);
+      s_cz[pw] = c.z;
+      s_cid[pw] = (int)c.w;
+      if (!NT1) s_ct[pw] = (unsigned char)tb[pos];
+    }
+    __syncthreads();
+    if (!live || (bexp & 2)) continue;
+    for (int br = 0; br < nbr_rows; br++) {
+      const int c0 = s_rc[r][br], c1 = c0 + s_rl[r][br];
+      const int lo = max(c0, p0), hi = min(c1, p0 + pn);
+      for (int p = lo + sub; p < hi; p += TPR) {
+        const int pw = p - p0;
+        const double2 cxy = s_cxy[pw];
+        const double dx = xi.x - cxy.x, dy = xi.y - cxy.y, dz = xi.z - s_cz[pw];
+        const double rsq = dx * dx + dy * dy + dz * dz;
+        if (rsq <= (NT1 ? cns1 : crow[s_ct[pw]]) && s_cid[pw] != row) {
+          atomicOr(&s_bm[r][p >> 5], 1u << (p & 31));
+          cntr++;
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int d = TPR >> 1; d > 0; d >>= 1) cntr += __shfl_xor(cntr, d, TPR);
+  const int Mw = (M + 31) >> 5;
+  // 4) used candidates -> slots (rank in candidate order); the union list
+  for (int w = tid; w < Mw; w += BLK_BT) s_used[w] = 0u;
+  __syncthreads();
+  {  // the OR over rows: (word, row group) per thread, then one LDS atomic per pair
+    constexpr int RG = 8;  // rows per thread
+    for (int t = tid; t < Mw * (R / RG); t += BLK_BT) {
+      const int w = t % Mw, r0 = (t / Mw) * RG;
+      unsigned o = 0u;
+#pragma unroll
+      for (int rr = 0; rr < RG; rr++) o |= s_bm[r0 + rr][w];
+      if (o) atomicOr(&s_used[w], o);
+    }
+  }
+  __syncthreads();
+  int u = 0;
+  {
+    const int v = tid < Mw ? __popc(s_used[tid]) : 0;
+    const int ex = blk_scan<BLK_BT>(v, s_w, &u);
+    if (tid < Mw) s_upre[tid] = ex;
+  }
+  __syncthreads();
+  for (int p = tid; p < M; p += BLK_BT) {  // (atom ids of used candidates from xb)
+    const unsigned wbits = s_used[p >> 5];
+    if (((wbits >> (p & 31)) & 1u) && !(bexp & 8)) {
+      int lo = 0, hi = BLK_TBL - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pre[mid] <= p) lo = mid;
+        else hi = mid - 1;
+      }
+      ulist[(size_t)b * ucap + s_upre[p >> 5] + __popc(wbits & ((1u << (p & 31)) - 1u))] =
+          (int)xb[s_st[lo] + (p - s_pre[lo])].w;
+    }
+  }
+  if (tid == 0) {
+    ucnt[b] = u;
+    atomicMax(umax, u);
+    atomicMax(umax + 1, M);   // (stats: largest candidate set, sums of candidates / unions)
+    atomicAdd(umax + 2, M);
+    atomicAdd(umax + 3, u);
+  }
+  if (!live) return;
+  // 5) the row's slots in ascending order (its TPR lanes take consecutive word ranges)
+  const int wp = (Mw + TPR - 1) / TPR;
+  const int w0 = min(sub * wp, Mw), w1 = min(w0 + wp, Mw);
+  int pc = 0;
+  for (int w = w0; w < w1; w++) pc += __popc(s_bm[r][w]);
+  int x = pc;
+#pragma unroll
+  for (int d = 1; d < TPR; d <<= 1) {
+    const int y = __shfl_up(x, d, TPR);
+    if (sub >= d) x += y;
+  }
+  int qq = x - pc;
+  unsigned short *const out = snbr + (size_t)row * sstride;
+  for (int w = w0; w < w1; w++) {
+    unsigned m = s_bm[r][w];
+    const unsigned used = s_used[w];
+    const int base = s_upre[w];
+    while (m) {
+      const int bit = __ffs(m) - 1;
+      m &= m - 1;
+      if (qq < sstride && !(bexp & 4))
+        out[blk_tpos<G, U>(qq)] = (unsigned short)(base + __popc(used & ((1u << bit) - 1u)));
+      qq++;
+    }
+  }
+  if (sub == 0) {
+    rcnt[row] = cntr;
+    if (cntr > sstride) atomicMax(ovf, 1 << 21);
+  }
+  const int cend = min((cntr + U * G - 1) / (U * G) * (U * G), sstride);
+  for (int k = cntr + sub; k < cend; k += TPR) out[blk_tpos<G, U>(k)] = 0;
+}
+
+// LDS images of a block's union (dynamic shared memory, um = largest union of the build)
+struct BlkRhoLds {
+  double2 *xy;
+  double *z;
+  unsigned char *t;
+};
+__host__ __device__ inline size_t blk_rho_lds(int um, bool nt1) {
+  return (size_t)um * (16 + 8) + (nt1 ? 0 : ((size_t)um + 15) / 16 * 16);
+}
+__host__ __device__ inline size_t blk_force_lds(int um, bool heat, bool nt1) {
+  return (size_t)um * 64 + (heat ? (size_t)um * 8 : 0) + (nt1 ? 0 : ((size_t)um + 15) / 16 * 16);
+}
+
+// A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.
+template <int U>
+struct SlotWord;
+template <>
+struct SlotWord<2> {
+  typedef unsigned T;
+  __device__ static int get(const T &w, int q) { return (int)((w >> (16 * q)) & 0xffffu); }
+};
+template <>
+struct SlotWord<4> {
+  typedef v2u T;
+  __device__ static int get(const T &w, int q) {
+    return (int)(((q < 2 ? w.x : w.y) >> (16 * (q & 1))) & 0xffffu);
+  }
+};
+
+// Walk a row's c slots (chunk-transposed, blk_tpos) with the row's G lanes, U slots per
+// lane per chunk: body(slot, in) for every slot position of the lane (in = position < c;
+// padded positions hold slot 0).  NCH > 0: all of the row's chunks (at most NCH, the
+// host guarantees c <= NCH*U*G) are loaded into registers before the first pair, so the
+// index stream's latency is paid once per row; NCH = 0: the next chunk is prefetched
+// while the current one is evaluated (the slot array is padded by two chunks).
+template <int G, int U, int NCH, class Body>
+__device__ __forceinline__ void blk_walk(const unsigned short *sl, int c, int lane,
+                                         Body body) {
+  typedef typename SlotWord<U>::T SW;
+  if (NCH > 0) {
+    SW w[NCH > 0 ? NCH : 1];
+#pragma unroll
+    for (int k = 0; k < NCH; k++)
+      w[k] = k * U * G < c ? *reinterpret_cast<const SW *>(sl + k * U * G + U * lane) : SW{};
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+      if (k * U * G >= c) break;
+#pragma unroll
+      for (int q = 0; q < U; q++) body(SlotWord<U>::get(w[k], q), k * U * G + q * G + lane < c);
+    }
+  } else {
+    SW wn = *reinterpret_cast<const SW *>(sl + U * lane);
+    for (int k0 = 0; k0 < c; k0 += U * G) {
+      const SW w = wn;
+      wn = *reinterpret_cast<const SW *>(sl + k0 + U * G + U * lane);
+#pragma unroll
+      for (int q = 0; q < U; q++) body(SlotWord<U>::get(w, q), k0 + q * G + lane < c);
+    }
+  }
+}
+
+// sph/rhosum over the block union (+ the Tait EOS epilogue: P/rho^2 into xf[i].w, rho into
+// vr[i].w), pair_sph_rhosum.cpp:116-195
+template <int R, int G, int U, int NCH, bool NT1>
+__global__ void __launch_bounds__(R * G)
+k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
+             const unsigned short *__restrict__ snbr, int sstride,
+             const int *__restrict__ rcnt, double4 *__restrict__ xf,
+             const int *__restrict__ ty, double4 *__restrict__ vr,
+             const Coefs *__restrict__ cf, int um) {
+  constexpr int NTH = R * G;
+  extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
+  __shared__ RhoPair s_c[NT1 ? 1 : NT2];
+  double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
+  double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)um * 16);
+  unsigned char *const s_t = blk_smem + (size_t)um * 24;
+  const int nt1 = cf->ntypes + 1;
+  const int b = (int)xcd_block(), tid = threadIdx.x;
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += NTH) s_c[t] = cf->rho[t];
+  const int u = ucnt[b];
+  const int *const ul = ulist + (size_t)b * ucap;
+  for (int p = tid; p < u; p += NTH) {
+    const int j = ul[p];
+    const double4 x = xf[j];
+    s_xy[p] = make_double2(x.x, x.y);
+    s_z[p] = x.z;
+    if (!NT1) s_t[p] = (unsigned char)ty[j];
+  }
+  __syncthreads();
+  const int row = b * R + tid / G, lane = tid & (G - 1);
+  const bool live = row < n;
+  const int rr = live ? row : n - 1;
+  const double4 xi = xf[rr];
+  const int it = NT1 ? 1 : ty[rr];
+  const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
+  const int c = live ? rcnt[rr] : 0;
+  double acc = 0.0;
+  blk_walk<G, U, NCH>(snbr + (size_t)rr * sstride, c, lane, [&](int sj, bool in) {
+    const double2 xy = s_xy[sj];
+    const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    const RhoPair cc = NT1 ? c1 : s_c[it * nt1 + s_t[sj]];
+    double wf = 1.0 - rsq * cc.ihsq;
+    wf = wf * wf;
+    wf = wf * wf;
+    acc += (in && rsq < cc.cutsq) ? cc.mK * wf : 0.0;
+  });
+  acc = group_sum<G>(acc);
+  if (lane == 0 && live) {
+    const double rho = cf->self_rho[it] + acc;
+    vr[row].w = rho;
+    xf[row].w = tait_p_over_rho2(rho, cf->rho0[it], cf->B[it]);
+  }
+}
+
+// sph/taitwater[/morris] [+ sph/heatconduction] over the block union (full list, i side
+// only), row2 pair body (k_row2_force).  blist == nullptr: every block whose union fits the
+// um-record LDS image (larger ones return at once); else the blocks listed in blist (the
+// second launch, with an image as large as the largest union).
+// EXP (study builds, SPH_EXP): 1 = neighbour records synthesised from the slot (no LDS
+// reads), 2 = LDS reads with a trivial body, 3 = no staging loads (LDS image left as is).
+// Outputs meaningless.
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+__global__ void __launch_bounds__(R * G)
+k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
+            const unsigned short *__restrict__ snbr, int sstride,
+            const int *__restrict__ rcnt, const double4 *__restrict__ xf,
+            const double4 *__restrict__ vr, const int *__restrict__ ty,
+            const double *__restrict__ en, const Coefs *__restrict__ cf,
+            double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
+            double gz, int um, const int *__restrict__ blist) {
+  constexpr bool TAIT = (MODE & M_TAIT) != 0;
+  constexpr bool HEAT = (MODE & M_HEAT) != 0;
+  constexpr int NTH = R * G;
+  extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
+  __shared__ TaitPair s_tp[(TAIT && !NT1) ? NT2 : 1];
+  __shared__ HeatPair s_hp[(HEAT && !NT1) ? NT2 : 1];
+  double2 *const s_a0 = reinterpret_cast<double2 *>(blk_smem);              // x, y
+  double2 *const s_a1 = s_a0 + um;                                          // z, P/rho^2
+  double2 *const s_a2 = s_a0 + 2 * (size_t)um;                              // vx, vy
+  double2 *const s_a3 = s_a0 + 3 * (size_t)um;                              // vz, rho
+  double *const s_e = reinterpret_cast<double *>(blk_smem + (size_t)um * 64);  // e (HEAT)
+  unsigned char *const s_t = blk_smem + (size_t)um * (HEAT ? 72 : 64);
+  const int nt1 = cf->ntypes + 1;
+  const int b = blist ? blist[blockIdx.x] : (int)xcd_block();
+  const int tid = threadIdx.x;
+  const int u = EXP == 3 ? 0 : ucnt[b];
+  if (!blist && u > um) return;  // (workgroup-uniform) left to the large-union launch
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += NTH) {
+      if (TAIT) s_tp[t] = cf->tait[t];
+      if (HEAT) s_hp[t] = cf->heat[t];
+    }
+  const int *const ul = ulist + (size_t)b * ucap;
+  for (int p = tid; p < u; p += NTH) {
+    const int j = ul[p];
+    const double4 x = xf[j], v = vr[j];
+    s_a0[p] = make_double2(x.x, x.y);
+    s_a1[p] = make_double2(x.z, x.w);
+    s_a2[p] = make_double2(v.x, v.y);
+    s_a3[p] = make_double2(v.z, v.w);
+    if (HEAT) s_e[p] = en[j];
+    if (!NT1) s_t[p] = (unsigned char)ty[j];
+  }
+  __syncthreads();
+  const int row = b * R + tid / G, lane = tid & (G - 1);
+  const bool live = row < n;
+  const int rr = live ? row : n - 1;
+  const double4 xi = xf[rr];
+  const double4 vi = vr[rr];
+  const double ei = HEAT ? en[rr] : 0.0;
+  const int it = NT1 ? 1 : ty[rr];
+  TaitPair t1{};
+  HeatPair h1{};
+  if (NT1) {
+    if (TAIT) t1 = cf->tait[3];
+    if (HEAT) h1 = cf->heat[3];
+  }
+  const int c = live ? rcnt[rr] : 0;
+  double fx = 0.0, fy = 0.0, fz = 0.0, drho = 0.0, dE = 0.0;
+  blk_walk<G, U, NCH>(snbr + (size_t)rr * sstride, c, lane, [&](int sj, bool ok) {
+    double2 a0, a1, a2, a3;
+    if (EXP == 1) {
+      const double o = (double)(sj & 7);
+      a0 = make_double2(xi.x + 0.25 * o, xi.y + 0.5);
+      a1 = make_double2(xi.z - 0.125 * o, xi.w);
+      a2 = make_double2(vi.x, vi.y - 0.01 * o);
+      a3 = make_double2(vi.z, vi.w);
+    } else {
+      a0 = s_a0[sj];
+      a1 = s_a1[sj];
+      a2 = s_a2[sj];
+      a3 = s_a3[sj];
+    }
+    if (EXP == 2) {
+      fx += a0.x + a2.x;
+      fy += a0.y + a2.y;
+      fz += a1.x + a3.x;
+      drho += a1.y + a3.y;
+      return;
+    }
+    const double dx = xi.x - a0.x, dy = xi.y - a0.y, dz = xi.z - a1.x;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    const int pidx = NT1 ? 3 : it * nt1 + s_t[sj];
+    const double r = sqrt1(rsq);
+    if (TAIT) {
+      const TaitPair cc = NT1 ? t1 : s_tp[pidx];
+      const bool hit = ok && rsq < cc.cutsq;
+      double wfd = cc.h - r;
+      wfd = cc.wK * (wfd * wfd);
+      wfd = hit ? wfd : 0.0;
+      const double velx = vi.x - a2.x, vely = vi.y - a2.y, velz = vi.z - a3.x;
+      const double dvdr = dx * velx + dy * vely + dz * velz;
+      if (VISC == SPH_VISC_MONAGHAN) {
+        const double qv = (cc.viscC * dvdr) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
+        const double fvisc = dvdr < 0. ? qv : 0.0;
+        const double fpair = cc.mm * (xi.w + a1.y + fvisc) * wfd;
+        fx += dx * fpair;
+        fy += dy * fpair;
+        fz += dz * fpair;
+        dE += -0.5 * fpair * dvdr;
+      } else {
+        double fvisc = cc.viscC * rcp1(vi.w * a3.y);
+        fvisc = hit ? fvisc * ((-cc.mm) * wfd) : 0.0;
+        const double fpair = cc.mm * (xi.w + a1.y) * wfd;
+        fx += dx * fpair + velx * fvisc;
+        fy += dy * fpair + vely * fvisc;
+        fz += dz * fpair + velz * fvisc;
+        dE += -0.5 * (fpair * dvdr + fvisc * (velx * velx + vely * vely + velz * velz));
+      }
+      drho += cc.mj * dvdr * wfd;
+    }
+    if (HEAT) {
+      const HeatPair cc = NT1 ? h1 : s_hp[pidx];
+      const bool hit = ok && rsq < cc.cutsq;
+      double wfd = cc.h - r;
+      wfd = cc.wK * (wfd * wfd);
+      wfd = hit ? wfd : 0.0;
+      double deltaE = cc.hmD;
+      deltaE *= (vi.w + a3.y) * rcp1(vi.w * a3.y);
+      deltaE = hit ? deltaE * ((ei - s_e[sj]) * wfd) : 0.0;
+      dE += deltaE;
+    }
+  });
+  if (TAIT) {
+    fx = group_sum<G>(fx);
+    fy = group_sum<G>(fy);
+    fz = group_sum<G>(fz);
+    drho = group_sum<G>(drho);
+  }
+  dE = group_sum<G>(dE);
+  if (lane == 0 && live) {
+    if (TAIT) {
+      const double m = cf->mass[it];
+      fo[row] = make_double4(fx + m * gx, fy + m * gy, fz + m * gz, drho);
+    }
+    de[row] = dE;
+  }
+}
+
+// blocks whose union exceeds the force pass's LDS image (um): their list for the second
+// launch
+static __global__ void k_blk_large(int nb, const int *__restrict__ ucnt, int um,
+                                   int *__restrict__ blist, int *__restrict__ nbig) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nb && ucnt[b] > um) blist[atomicAdd(nbig, 1)] = b;
+}
+
+// ---- host-side launch helpers ----------------------------------------------------------
+// Block shapes (rows per block R, lanes per row G, slots per lane and chunk U); SPH_BLK
+// picks one (tuning).  R*G threads per pair-pass workgroup.
+#define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4) X(2, 32, 16, 2)
+constexpr int BLK_NCH = 8;  // slot chunks preloaded per row (rows up to BLK_NCH*U*G entries)
+struct BlkShape {
+  int R, G, U;
+};
+inline BlkShape blk_shape(int k) {
+  switch (k) {
+#define SPH_CASE(k, R, G, U) \
+  case k: return BlkShape{R, G, U};
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+    default: return BlkShape{32, 16, 2};
+  }
+}
+
+struct BlkArgs {
+  int n = 0;            // owned rows
+  int shape = 2;        // index into SPH_BLK_SHAPES
+  int ucap = 0;         // union stride of ulist
+  int um = 0;           // largest union of the build
+  int umf = 0;          // force pass's LDS image (records); larger unions: second launch
+  int nbig = 0;         // blocks with a union larger than umf (listed in blist)
+  int sstride = 0;      // slot-row stride (entries)
+  int exp = 0;          // study variants (SPH_EXP), 0 in production
+  const int *ulist = nullptr, *ucnt = nullptr, *rcnt = nullptr, *blist = nullptr;
+  const unsigned short *snbr = nullptr;
+  bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
+};
+
+inline int blk_blocks(int n, int R) { return (n + R - 1) / R; }
+
+inline void blk_neigh(int shape, bool nt1, hipStream_t s, int n, const QBins &q, int dim,
+                      const double4 *xf, const int *ty, const double4 *xb, const int *tb,
+                      const int *qbeg, const Coefs *cf, int ucap, int sstride, int *ulist,
+                      int *ucnt, int *rcnt, unsigned short *snbr, int *ovf, int *umax,
+                      int bexp = 0) {
+  switch (shape) {
+#define SPH_CASE(k, R, G, U)                                                                  \
+  case k:                                                                                   \
+    if (nt1)                                                                                \
+      hipLaunchKernelGGL((k_blk_neigh<R, G, U, true>), dim3(blk_blocks(n, R)), dim3(R * BLK_TPR), 0, \
+                         s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt,  \
+                         rcnt, snbr, ovf, umax, bexp);                                        \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_blk_neigh<R, G, U, false>), dim3(blk_blocks(n, R)), dim3(R * BLK_TPR), 0,\
+                         s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt,  \
+                         rcnt, snbr, ovf, umax, bexp);                                        \
+    break;
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+  }
+}
+
+template <int R, int G, int U, int NCH, bool NT1>
+inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
+                         double4 *vr, const Coefs *cf) {
+  const size_t lds = blk_rho_lds(k.um, NT1);
+  auto fn = k_blk_rhosum<R, G, U, NCH, NT1>;
+  SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
+                     k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um);
+}
+template <int R, int G, int U>
+inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
+                         double4 *vr, const Coefs *cf) {
+  const bool pre = k.pre(BlkShape{R, G, U});
+  if (nt1) {
+    if (pre) blk_rhosum_t<R, G, U, BLK_NCH, true>(s, k, xf, ty, vr, cf);
+    else blk_rhosum_t<R, G, U, 0, true>(s, k, xf, ty, vr, cf);
+  } else {
+    if (pre) blk_rhosum_t<R, G, U, BLK_NCH, false>(s, k, xf, ty, vr, cf);
+    else blk_rhosum_t<R, G, U, 0, false>(s, k, xf, ty, vr, cf);
+  }
+}
+inline void blk_rhosum(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
+                       double4 *vr, const Coefs *cf) {
+  if (k.n == 0) return;
+  switch (k.shape) {
+#define SPH_CASE(q, R, G, U) \
+  case q: blk_rhosum_s<R, G, U>(nt1, s, k, xf, ty, vr, cf); break;
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+  }
+}
+
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
+  auto fn = k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;
+  const bool heat = (MODE & M_HEAT) != 0;
+  // main launch: every block whose union fits umf records; then the large-union blocks
+  const size_t lds = blk_force_lds(k.umf, heat, NT1);
+  const size_t ldsb = blk_force_lds(k.um, heat, NT1);
+  SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)std::max(lds, ldsb)));
+  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
+                     k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
+                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr);
+  if (k.nbig > 0)
+    hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
+                       k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
+                       a.gx, a.gy, a.gz, k.um, k.blist);
+}
+template <int R, int G, int U, int NCH, bool NT1>
+inline void blk_force_n(int visc, int mode, hipStream_t s, const BlkArgs &k, const RowArgs &a) {
+  const bool mor = visc == SPH_VISC_MORRIS;
+  switch (mode) {
+    case M_TAIT:
+      if (mor) blk_force_t<R, G, U, NCH, 1, M_TAIT, NT1>(s, k, a);
+      else if (NT1 && k.exp == 1) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 1>(s, k, a);
+      else if (NT1 && k.exp == 2) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 2>(s, k, a);
+      else if (NT1 && k.exp == 3) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 3>(s, k, a);
+      else blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1>(s, k, a);
+      break;
+    case M_TAIT | M_HEAT:
+      if (mor) blk_force_t<R, G, U, NCH, 1, M_TAIT | M_HEAT, NT1>(s, k, a);
+      else blk_force_t<R, G, U, NCH, 0, M_TAIT | M_HEAT, NT1>(s, k, a);
+      break;
+    default: blk_force_t<R, G, U, NCH, 0, M_HEAT, NT1>(s, k, a); break;
+  }
+}
+template <int R, int G, int U>
+inline void blk_force_s(bool nt1, int visc, int mode, hipStream_t s, const BlkArgs &k,
+                        const RowArgs &a) {
+  const bool pre = k.pre(BlkShape{R, G, U});
+  if (nt1) {
+    if (pre) blk_force_n<R, G, U, BLK_NCH, true>(visc, mode, s, k, a);
+    else blk_force_n<R, G, U, 0, true>(visc, mode, s, k, a);
+  } else {
+    if (pre) blk_force_n<R, G, U, BLK_NCH, false>(visc, mode, s, k, a);
+    else blk_force_n<R, G, U, 0, false>(visc, mode, s, k, a);
+  }
+}
+inline void blk_force(bool nt1, int visc, int mode, hipStream_t s, const BlkArgs &k,
+                      const RowArgs &a) {
+  if (k.n == 0) return;
+  switch (k.shape) {
+#define SPH_CASE(q, R, G, U) \
+  case q: blk_force_s<R, G, U>(nt1, visc, mode, s, k, a); break;
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+  }
+}
+
+}  // namespace sph

@@ -19,6 +19,7 @@
 #include "sph_comm.h"
 #include "sph_dispatch.h"
 #include "sph_bin_kernels.h"
+#include "sph_blk_kernels.h"
 #include "sph_cluster_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_row_kernels.h"
@@ -108,9 +109,8 @@ static bool row2_iv() {
   static bool v = env_int("SPH_IV", 1) != 0;
   return v;
 }
-static int row2_exp() {
-  static int v = env_int("SPH_EXP", 0);
-  return v;
+static int row2_exp() {  // read per launch: tools/kernel_sweep.py sets it for the timed passes only
+  return env_int("SPH_EXP", 0);
 }
 // SPH_OVERLAP (default 0): with a brick decomposition, run the pair passes of interior
 // rows (no ghost in the list) on a second stream while the forward / rho halos are in
@@ -123,6 +123,11 @@ static int row2_exp() {
 // type in their top bits, so the row2 passes skip the per-neighbour type gather
 static bool tbits_env() {
   static bool v = env_int("SPH_TBITS", 1) != 0;
+  return v;
+}
+// SPH_BLK (default 2): block shape of the block-staged path (SPH_BLK_SHAPES)
+static int blk_shape_env() {
+  static int v = env_int("SPH_BLK", 2);
   return v;
 }
 // (read per engine at sph_engine_create)
@@ -219,6 +224,12 @@ struct sph_engine {
   bool list_tbits = false; // strided entries carry the neighbour's type (SPH_TBIT_SHIFT)
   // this step's in-cut ("tight") list, written by the rhosum pass for the force pass
   DBuf<int> tnbr, tcnt;
+  // block-staged path (sph_blk_kernels.h): per block of blk_R rows its union of neighbour
+  // atoms (ulist, ucnt) and the rows' 16-bit slot lists (snbr, stride blk_sstride)
+  bool blk = false;
+  int blk_sh = 2, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
+  DBuf<int> ulist, ucnt, bl;
+  DBuf<unsigned short> snbr;
   // cluster-pair path (kernel_path 3): rows of CL_CI consecutive owned atoms, fixed
   // stride cl_stride, counts ccl; rhosum accumulator racc
   bool clustered = false;
@@ -328,14 +339,19 @@ struct sph_engine {
     const bool mort = !want_staged() && !want_tiles() && kbn.nb[0] <= 1024 &&
                       kbn.nb[1] <= 1024 && kbn.nb[2] <= 1024;
     if (!mort) kbn = bn;
+    // the block path orders rows along a Hilbert curve (its blocks of consecutive rows stay
+    // compact), the row path along a Morton curve
+    int cb = 1;
+    const int mx3 = std::max(kbn.nb[0], std::max(kbn.nb[1], kbn.nb[2]));
+    while ((1 << cb) < mx3) cb++;
+    const bool hil = mort && want_blk() && cb >= 2;
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks(n)), dim3(BLK), 0, s, n, 0, kbn, xf.p, bkey.p,
-                       bidx.p, mort ? 1 : 0);
-    // key bits: 3 x (bits of the largest cell dimension) for Morton codes, else bits(nbins)
+                       bidx.p, hil ? cb + 1 : (mort ? 1 : 0), cfg.dim);
+    // key bits: dim (Hilbert) or 3 (Morton) x bits of the largest cell dimension, else
+    // bits(nbins)
     int kb = 1;
     if (mort) {
-      const int mx3 = std::max(kbn.nb[0], std::max(kbn.nb[1], kbn.nb[2]));
-      while ((1 << kb) < mx3) kb++;
-      kb *= 3;
+      kb = cb * (hil ? cfg.dim : 3);
     } else {
       while ((1u << kb) < (unsigned)nbins && kb < 32) kb++;
     }
@@ -364,6 +380,7 @@ struct sph_engine {
   }
 
   bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2 && !multi(); }
+  bool want_blk() const { return cfg.kernel_path == 5; }
   bool want_tiles() const { return cfg.kernel_path == 2; }
   // cluster-pair path: kernel_path 3 = full cluster lists (gather only), 4 = half lists
   // (Newton-3 updates by atomics); SPH_CLUSTER = atoms per cluster (4 or 8)
@@ -884,9 +901,10 @@ struct sph_engine {
     // needs the CSR form (the setup half list, the tile/staged paths, row kernels gen < 2)
     if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
       // rows stored chunk-transposed for the row2 kernels' 16-B index loads (k_neigh3 only)
-      list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3()) ? row2_iv_g() : 0;
+      // (the block path reads plain entries: no transposition, no type bits)
+      list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3() && !want_blk()) ? row2_iv_g() : 0;
       list_perm_pi = row2_pi() ? 1 : 0;
-      list_tbits = !nt1() && tbits_env() && neigh_q() == 2 && neigh3();
+      list_tbits = !nt1() && tbits_env() && neigh_q() == 2 && neigh3() && !want_blk();
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -1265,6 +1283,79 @@ struct sph_engine {
     if (nt1()) tile_force_n<true>(); else tile_force_n<false>();
   }
 
+  // Block unions + slot rows straight from the bins (k_blk_neigh; bin_q() must have run) in
+  // the SPH_BLK shape.  The row stride is the last CSR build's (list_stride), doubled if a
+  // row outgrows it; false (the row path takes over) if a block overflows its LDS image.
+  bool build_blk() {
+    const int n = nlocal;
+    if (n == 0) return false;
+    mx.reserve(8);
+    ccnt.reserve(n + 1);
+    const int shape = blk_shape_env();
+    const BlkShape sh = blk_shape(shape);
+    const int chunk = sh.G * sh.U;
+    if (blk_rowcap == 0) blk_rowcap = std::max(list_stride, nbr_maxrow + nbr_maxrow / 4 + 16);
+    for (int attempt = 0; attempt < 2; attempt++) {
+      blk_sstride = (std::max(blk_rowcap, 1) + chunk - 1) / chunk * chunk;
+      snbr.reserve((size_t)n * blk_sstride + 2 * chunk);  // + the pair passes' prefetch pad
+      const int nb = blk_blocks(n, sh.R);
+      ulist.reserve((size_t)nb * BLK_MCAP);
+      ucnt.reserve(nb);
+      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
+      blk_neigh(shape, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, BLK_MCAP,
+                blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
+                env_int("SPH_BEXP", 0));
+      int hm[5];
+      SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipStreamSynchronize(s));
+      if (env_int("SPH_DEBUG", 0))
+        fprintf(stderr,
+                "[sph] k_blk_neigh shape %d n %d rowcap %d: ovf %d union max %d mean %.1f, "
+                "candidates max %d mean %.1f\n",
+                shape, n, blk_rowcap, hm[0], hm[1], (double)hm[4] / nb, hm[2],
+                (double)hm[3] / nb);
+      if (env_int("SPH_DEBUG", 0) && hm[0] == 0) fprintf(stderr, "[sph] (stats above)\n");
+      if (hm[0] == 0) {
+        blk_sh = shape;
+        blk_um = std::max(hm[1], 1);
+        // the force pass's LDS image: ~1.25x the mean union (64-record steps), the blocks
+        // above it in a second launch (k_blk_large)
+        const double mean = (double)hm[4] / nb;
+        blk_umf = std::min(blk_um, ((int)(1.25 * mean) + 63) / 64 * 64);
+        if (env_int("SPH_BLKUMF", 0) > 0) blk_umf = std::min(blk_um, env_int("SPH_BLKUMF", 0));
+        blk_nbig = 0;
+        if (blk_umf < blk_um) {
+          bl.reserve(nb);
+          SPH_HIP_TRY(hipMemsetAsync(mx.p + 5, 0, sizeof(int), s));
+          hipLaunchKernelGGL(k_blk_large, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p, blk_umf,
+                             bl.p, mx.p + 5);
+          blk_nbig = read_scalar(mx.p + 5);
+        }
+        return true;
+      }
+      if (hm[0] != (1 << 21)) return false;  // a block overflowed its LDS image
+      blk_rowcap *= 2;                        // a row outgrew the slot-row stride
+    }
+    return false;
+  }
+  BlkArgs blk_args() const {
+    BlkArgs k;
+    k.n = nlocal;
+    k.shape = blk_sh;
+    k.exp = row2_exp();
+    k.ucap = BLK_MCAP;
+    k.um = blk_um;
+    k.umf = blk_umf;
+    k.nbig = blk_nbig;
+    k.blist = bl.p;
+    k.sstride = blk_sstride;
+    k.ulist = ulist.p;
+    k.ucnt = ucnt.p;
+    k.rcnt = ccnt.p;
+    k.snbr = snbr.p;
+    return k;
+  }
+
   // pbc + sort + borders + list(s); `need_csr` also builds the global-index CSR list
   void build_all(bool need_csr) {
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
@@ -1274,6 +1365,7 @@ struct sph_engine {
     borders();
     staged = false;
     tiled = false;
+    blk = false;
     if (st) {
       sort_ghosts();
       staged = build_staged();
@@ -1284,6 +1376,23 @@ struct sph_engine {
       bin_q();
       clustered = build_clusters();
       if (need_csr || !clustered) build_list_q(true, /*rebin=*/false);
+    } else if (want_blk() && !staged && neigh_q() == 2) {
+      // block path: bins, the global-index CSR list only where the setup's half-list pass
+      // needs it, then the block unions + slot rows from the bins; the row path's strided
+      // list if a block overflows
+      bin_q();
+      if (need_csr) list_q(true);
+      blk = build_blk();
+      if (blk) {
+        if (!need_csr) {
+          strided = true;  // (ccnt holds the full-list counts; list_entries sums them)
+          nbr_total = -1;
+          full_counts = true;
+          nbr_builds++;
+        }
+      } else if (!need_csr) {
+        list_q(false);
+      }
     } else if (!staged || need_csr) {
       if (neigh_q()) {
         build_list_q(need_csr || st || want_tiles() || row_gen() != 2);
@@ -1298,7 +1407,7 @@ struct sph_engine {
   }
 
   bool overlap_on() const {
-    return multi() && overlap && !staged && !tiled && !clustered && use_row2() &&
+    return multi() && overlap && !staged && !tiled && !clustered && !blk && use_row2() &&
            !tight_on() && (force_mode & M_TAIT) != 0 && cfg.rhosum_nstep > 0;
   }
   // interior rows (no ghost in the list) and boundary rows, each in row order
@@ -1442,6 +1551,8 @@ struct sph_engine {
         Scope t(this, T_RHO);
         if (clustered && !setup) {
           cl_rhosum();
+        } else if (blk) {
+          blk_rhosum(nt1(), s, blk_args(), xf.p, ty.p, vr.p, dc);
         } else if (staged) {
           launch_bin_rhosum();
         } else if (tiled) {
@@ -1481,6 +1592,9 @@ struct sph_engine {
     } else if (force_mode && clustered) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       cl_force();
+    } else if (force_mode && blk) {
+      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
+      blk_force(nt1(), cfg.tait_visc, force_mode, s, blk_args(), row_args());
     } else if (force_mode && staged) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       launch_bin_force();
@@ -1792,6 +1906,10 @@ int sph_engine_destroy(sph_engine *e) {
   e->tcnt.release();
   e->nbr32.release();
   e->nbr16.release();
+  e->ulist.release();
+  e->ucnt.release();
+  e->bl.release();
+  e->snbr.release();
   if (e->dc) (void)hipFree(e->dc);
   e->rows_in.release();
   e->rows_bd.release();
@@ -1881,6 +1999,16 @@ int sph_engine_pair_passes(sph_engine *e, int n) {
   SPH_API_END
 }
 
+int sph_engine_rebuild_passes(sph_engine *e, int n) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && n >= 0, SPH_HIP_EINVAL, "sph_engine_rebuild_passes: bad argument");
+  SPH_REQUIRE(e->setup_done, SPH_HIP_EINVAL, "sph_engine_rebuild_passes: call setup first");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  for (int k = 0; k < n; k++) e->rebuild();
+  SPH_HIP_TRY(hipGetLastError());
+  SPH_API_END
+}
+
 int sph_engine_nlocal(sph_engine *e) { return e ? e->nlocal : 0; }
 
 int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, double *en,
@@ -1960,7 +2088,7 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->nbr_full = e->list_entries();
   st->nbr_builds = e->nbr_builds;
   st->nbr_maxrow = e->nbr_maxrow;
-  st->staged = e->staged ? 1 : (e->tiled ? 2 : (e->clustered ? 3 : 0));
+  st->staged = e->staged ? 1 : (e->tiled ? 2 : (e->clustered ? 3 : (e->blk ? 5 : 0)));
   st->stage_max = e->stage_max;
   st->ms_rhosum = e->ms[T_RHO];
   st->ms_tait = e->ms[T_TAIT];

@@ -257,21 +257,64 @@ __device__ __forceinline__ unsigned spread3(unsigned v) {
   return v;
 }
 
+// Hilbert index of cell (x, y[, z]), b bits per axis (Skilling, "Programming the Hilbert
+// curve", AIP Conf. Proc. 707, 2004: axes -> transpose, then bit interleave).  Consecutive
+// indices are face-adjacent cells, so a run of consecutive atoms in this order is a
+// connected, compact region (Morton order jumps at every level boundary).
+__device__ __forceinline__ unsigned spread2(unsigned v) {
+  v &= 0xffffu;
+  v = (v | (v << 8)) & 0x00ff00ffu;
+  v = (v | (v << 4)) & 0x0f0f0f0fu;
+  v = (v | (v << 2)) & 0x33333333u;
+  v = (v | (v << 1)) & 0x55555555u;
+  return v;
+}
+__device__ __forceinline__ unsigned hilbert_key(int dim, unsigned x, unsigned y, unsigned z,
+                                                int b) {
+  unsigned X[3] = {x, y, z};
+  const int n = dim;
+  const unsigned M = 1u << (b - 1);
+  for (unsigned Q = M; Q > 1; Q >>= 1) {
+    const unsigned P = Q - 1;
+    for (int i = 0; i < n; i++) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      } else {
+        const unsigned t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  for (int i = 1; i < n; i++) X[i] ^= X[i - 1];
+  unsigned t = 0;
+  for (unsigned Q = M; Q > 1; Q >>= 1)
+    if (X[n - 1] & Q) t ^= Q - 1;
+  for (int i = 0; i < n; i++) X[i] ^= t;
+  return n == 3 ? (spread3(X[0]) << 2) | (spread3(X[1]) << 1) | spread3(X[2])
+                : (spread2(X[0]) << 1) | spread2(X[1]);
+}
+
 // Sort keys: linear bin index (x fastest; the staged path needs each x-row of bins
 // contiguous), or the bins' Morton code (morton != 0; the CSR path's row order: a run
 // of consecutive rows then covers a compact block of space, so the neighbor records a
 // wave of rows gathers stay within one XCD's L2).
+// morton: 0 = linear bins, 1 = Morton code, > 1 = Hilbert index with (morton - 1) bits
+// per axis of dimension `hdim`
 static __global__ void k_bin_keys(int n, int first, Bins bn, const double4 *__restrict__ xf,
                                   unsigned *__restrict__ key, int *__restrict__ idx,
-                                  int morton = 0) {
+                                  int morton = 0, int hdim = 3) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const double4 x = xf[first + k];
   const int cx = bin_coord(x.x, bn.lo[0], bn.inv[0], bn.nb[0]);
   const int cy = bin_coord(x.y, bn.lo[1], bn.inv[1], bn.nb[1]);
   const int cz = bin_coord(x.z, bn.lo[2], bn.inv[2], bn.nb[2]);
-  key[k] = morton ? (spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2))
-                  : (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
+  if (morton > 1)
+    key[k] = hilbert_key(hdim, (unsigned)cx, (unsigned)cy, (unsigned)cz, morton - 1);
+  else
+    key[k] = morton ? (spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2))
+                    : (unsigned)((cz * bn.nb[1] + cy) * bn.nb[0] + cx);
   idx[k] = first + k;
 }
 

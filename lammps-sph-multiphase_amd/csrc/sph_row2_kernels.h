@@ -175,7 +175,11 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
   static_assert(!TIGHT || LP, "the tight-list compaction needs wave-uniform trip counts");
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   __shared__ double s_fc[(NT1 || !TIGHT) ? 1 : NT2];
-  __shared__ __attribute__((aligned(16))) int s_tq[TIGHT ? 256 / G : 1][TIGHT ? 64 : 4];
+  // a group's buffer holds up to 3 carried entries + one chunk's G*U hits, rounded up to
+  // whole 16-B stores (G*U = 64 at tile 2 would overflow a 64-entry row)
+  constexpr int TQ = TIGHT ? (G * U + 3 + 3) / 4 * 4 : 4;
+  static_assert(!TIGHT || TQ >= G * U + 3, "tight-list buffer too small");
+  __shared__ __attribute__((aligned(16))) int s_tq[TIGHT ? 256 / G : 1][TQ];
   const int nt1 = cf->ntypes + 1;
   if (!NT1) {
     for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) {

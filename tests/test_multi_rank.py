@@ -71,3 +71,58 @@ def test_two_rank_bricks_gloo():
     # the sites are exactly those of the global lattice, tag = (z*NY + y)*NX + x
     site = np.rint(xs).astype(int)
     assert np.array_equal((site[:, 2] * n + site[:, 1]) * NX + site[:, 0], tags)
+
+
+def _bench_json(args):
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout            # ONE JSON line, from rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_launches_ranks_strong():
+    """`bench.py --gpus 2` without WORLD_SIZE starts its own two ranks (fresh processes);
+    the rank-0 line says n_gpus 2 and the strong split partitions the one 1M box."""
+    out = _bench_json(["--gpus", "2", "--dry-run", "--steps", "1", "--warmup", "0"])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert "strong" in out["config"]["workload"] and "2x1x1" in out["config"]["workload"]
+    assert out["config"]["particles_total"] == 100 ** 3
+    assert len(out["config"]["particles_per_rank"]) == 2
+
+
+def test_bench_launches_ranks_weak():
+    out = _bench_json(["--gpus", "4", "--dry-run", "--scaling", "weak", "--edge", "10"])
+    assert out["n_gpus"] == 4 and out["scaling"] == "weak"
+    assert "weak" in out["config"]["workload"]
+    assert out["config"]["particles_per_rank"] == [1000] * 4
+
+
+def test_strong_lattice_partition():
+    """The strong split's bricks partition make_system(n) exactly (same sites, jitter,
+    velocities), so N = 1 and N > 1 run the same physical system."""
+    import bench
+    n = 12
+    x0, v0, *_ = bench.make_system(n, 12345)
+    pg = bench.procgrid_for(8)
+    parts = [bench.strong_lattice(n, pg, r) for r in range(8)]
+    tags = np.concatenate([p[6] for p in parts])
+    assert np.array_equal(np.sort(tags), np.arange(n ** 3))
+    order = np.argsort(tags)
+    xs = np.concatenate([p[0] for p in parts])[order]
+    vs = np.concatenate([p[1] for p in parts])[order]
+    assert np.array_equal(xs, x0) and np.array_equal(vs, v0)
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dry-run"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -16,10 +16,13 @@ def main():
     x, v, t, rho, e, cv = bench.make_system(n, 12345)
     cfg = bench.c2_config(sph, n)
     cfg.kernel_path = int(os.environ.get("SPH_PATH", "0"))
+    exp = os.environ.pop("SPH_EXP", None)   # study variants: the timed passes only
     eng = sph.Engine(cfg)
     eng.set_atoms(x, v, t, rho, e, cv)
     eng.setup()
     eng.run(12)                 # past the first rebuild: the steady-state (strided) list
+    if exp is not None:
+        os.environ["SPH_EXP"] = exp
     eng.pair_passes(3)
     eng.sync()
     eng.set_timing(True)

@@ -6,8 +6,12 @@ import json
 import sys
 
 
+FAMILIES = ["k_blk_force", "k_blk_rhosum", "k_blk_build", "k_row2_force", "k_row2_rhosum",
+            "k_bin_force", "k_bin_rhosum", "k_bin_neigh", "k_force", "k_rhosum", "k_neigh"]
+
+
 def family(name):
-    for k in ("k_bin_force", "k_bin_rhosum", "k_bin_neigh", "k_force", "k_rhosum", "k_neigh"):
+    for k in FAMILIES:
         if k in name:
             return k
     return None

@@ -655,8 +655,9 @@ def main():
                          "heat conduction engine step (config 3); c2pair: rhosum + taitwater "
                          "through the pair-style layer; c5pair: the multiphase pair passes "
                          "through the pair-style layer (--edge sets n^3)")
-    ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "1")),
-                    help="pair-kernel path (sph_engine_config.kernel_path)")
+    ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "0")),
+                    help="pair-kernel path (sph_engine_config.kernel_path): 0 = block-staged "
+                         "(production), 1 = row path")
     ap.add_argument("--comm-loopback", action="store_true",
                     help="one GPU: route the periodic self swaps through a one-rank RCCL "
                          "communicator (send/recv to itself) -- the multi-GPU halo path's cost "
@@ -798,16 +799,14 @@ def main():
     ach_tait = bytes_tait * nloc / (ms_tait * 1e-3) / 1e9
     ach_rho = bytes_rho * nloc / (ms_rho * 1e-3) / 1e9
     ach_pair = (bytes_tait + bytes_rho) * nloc / ((ms_tait + ms_rho) * 1e-3) / 1e9
-    kname = {1: "k_bin_force", 2: "k_tile_force", 5: "k_blk_force"}.get(st["staged"],
-                                                                      "k_row2_force")
+    kname = "k_blk_force" if st["staged"] == 1 else "k_row2_force"
     out = dict(base, value=total_ps, ms_per_step=elapsed / args.steps * 1e3)
     out["config"] = {"workload": workload,
                      "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                      "n_full_per_particle": n_full, "n_half_per_particle": n_half,
                      "parallelism": parallelism,
-                     "kernel_path": {1: "lds-staged bins", 2: "lds tiles",
-                                     5: "block-staged unions (LDS)"}.get(st["staged"],
-                                                                         "csr rows")}
+                     "kernel_path": ("block-staged LDS unions + 16-bit slot rows"
+                                     if st["staged"] == 1 else "row path (global gathers)")}
     out["roofline"] = {"bound": "hbm", "kernel": kname + "<TAIT> (sph/taitwater pass)",
                        "achieved": ach_tait, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": ach_tait / PEAK_HBM_GBS, "traffic": None,

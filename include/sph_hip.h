@@ -229,12 +229,12 @@ typedef struct {
   int rank;                    /* my rank in the brick, x fastest */
   /* spatially sort owned particles at every rebuild (atom->sort analogue) */
   int sort;
-  /* pair-pass kernels: 1 = full-list rows with global gathers (second-generation row
-     kernels over strided, chunk-transposed lists: the fastest, use this),
-     0 = LDS-staged bins + 16-bit slot lists (needs sort), 2 = LDS tiles,
-     3 = cluster pairs (a wave takes a cluster of 4 consecutive owned atoms and the union
-         of their neighbours, each neighbour record loaded once for the cluster; gather
-         only), 4 = as 3 over half lists with Newton-3 updates by fp64 atomics */
+  /* pair-pass kernels (full lists, gather only, no atomics):
+     0 = block-staged (production): blocks of consecutive owned rows stage the union of
+         their neighbours in LDS, rows walk 16-bit slot lists built from the bins at every
+         rebuild (falls back to 1 for a build whose blocks overflow the LDS image);
+     1 = row path: rows gather neighbour records from HBM through a strided global-index
+         list (the round-1 production path) */
   int kernel_path;
 } sph_engine_config;
 
@@ -243,9 +243,9 @@ typedef struct {
   int nlocal, nghost;
   int64_t nbr_full;            /* entries in the device full list (owned rows) */
   int nbr_builds;
-  int nbr_maxrow;              /* staged path: max owned atoms in one bin */
-  int staged;                  /* 1 if the last build produced LDS-staged lists */
-  int stage_max;               /* staged path: max atoms staged by one bin workgroup */
+  int nbr_maxrow;              /* longest full-list row of the last CSR build */
+  int staged;                  /* 1 if the last build produced block-staged lists */
+  int stage_max;               /* block path: largest block union (LDS records) */
   double ms_rhosum, ms_tait, ms_heat, ms_integrate, ms_comm, ms_neigh; /* event-timed */
   int64_t n_rhosum, n_tait, n_heat, n_neigh;  /* launches timed */
 } sph_engine_stats;

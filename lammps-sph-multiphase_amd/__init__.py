@@ -332,9 +332,9 @@ def _pair_table(dst, tab, ntypes):
 def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every=10,
                 rhosum=None, tait=None, heat=None, gravity=(0.0, 0.0, 0.0),
                 stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0,
-                kernel_path=1) -> EngineConfig:
-    """kernel_path: 1 = the production pair passes (row2 kernels over strided full lists;
-    bench.py's path), 0 = LDS-staged bins, 2 = LDS tiles, 3/4 = cluster pairs (study paths).
+                kernel_path=0) -> EngineConfig:
+    """kernel_path: 0 = the production pair passes (block-staged LDS unions + 16-bit slot
+    rows; bench.py's path), 1 = the row path (row2 gathers over strided global lists).
     rhosum = dict(nstep, cut); tait = dict(rho0, c0, visc, cut, morris[, B]);
     heat = dict(alpha, cut); per-type arrays (ntypes+1), per-pair (ntypes+1, ntypes+1)."""
     c = EngineConfig()

@@ -18,13 +18,9 @@
 #include "sph_coef.h"
 #include "sph_comm.h"
 #include "sph_dispatch.h"
-#include "sph_bin_kernels.h"
 #include "sph_blk_kernels.h"
-#include "sph_cluster_kernels.h"
 #include "sph_engine_kernels.h"
-#include "sph_row_kernels.h"
 #include "sph_row2_kernels.h"
-#include "sph_tile_kernels.h"
 #include "sph_util.h"
 
 using namespace sph;
@@ -34,12 +30,6 @@ static int env_int(const char *name, int dflt) {
   const char *s = getenv(name);
   return s ? atoi(s) : dflt;
 }
-// SPH_ROWTILE: tile shape index of SPH_ROW_TILES (tuning; default 3 = 16 lanes x 2 pairs,
-// the fastest measured on C2 1M: tools/sweep_rowtile.sh)
-int row_tile() {
-  static int t = env_int("SPH_ROWTILE", 3);
-  return t;
-}
 // SPH_ROW2TILE: shape index of SPH_ROW2_TILES (default 3 = 8 lanes x 4 pairs, the fastest
 // with lane-pair gathers on C2 1M: profiles/r01/sweep_row2.log)
 int row2_tile() {
@@ -47,46 +37,15 @@ int row2_tile() {
   return t;
 }
 }  // namespace sph
-// SPH_ROWK: 2 = second-generation row kernels (buffer loads, index prefetch, one-step
-// Newton rcp/sqrt; default), 1 = first-generation row kernels, 0 = the generic
-// pair-layer kernels (comparison only)
-// list builder (default 2, fastest end to end on C2 1M: tools/sweep_neigh.sh):
-// 3 = binned copy over full-size bins (27-bin stencil, rows in lockstep),
-// 2 = binned copy over half-size bins with per-row trimming, 1 = bidx-indirect (original)
-static int neigh_q() {
-  static int v = env_int("SPH_NEIGH", 2);
-  return v == 1 ? 0 : v;
-}
-// SPH_NEIGH3 (default 1): the half-size-bin builder walks its candidates as one flat
-// range (k_neigh3) instead of bin-row by bin-row (k_neigh2); same list
-static bool neigh3() {
-  static bool v = env_int("SPH_NEIGH3", 1) != 0;
-  return v;
-}
-// SPH_MORTON_DIV (default 4, the fastest of 1/2/4/8 on C2 1M): cells per bin edge of the
-// owned atoms' Morton sort key
+// SPH_MORTON_DIV (default 4, the fastest of 1/2/4/8 on C2 1M for the row path): cells per
+// bin edge of the owned atoms' sort key (Morton for the row path, Hilbert for the block path)
 static int morton_div() {
   static int v = std::max(1, env_int("SPH_MORTON_DIV", 4));
   return v;
 }
-// SPH_CLX: study variants of the cluster passes (ClArgs::exp); 0 in production
-// SPH_CLUSTER (default 4): atoms per cluster of the cluster-pair paths (4 or 8)
-static int cl_size() {
-  static int v = env_int("SPH_CLUSTER", 4) == 8 ? 8 : 4;
-  return v;
-}
-static int cl_exp() {
-  static int v = env_int("SPH_CLX", 0);
-  return v;
-}
-static int row_gen() {
-  static int g = env_int("SPH_ROWK", 2);
-  return g;
-}
-static bool row_kernels() { return row_gen() != 0; }
-// SPH_LP (default 1): lane-pair gathers in the row2 kernels; SPH_IV (default 1): the
-// strided list is stored chunk-transposed so each lane's four indices of a chunk are one
-// 16-B load (sph_row2_kernels.h); SPH_EXP: study variants (kernel_sweep)
+// Row path (kernel_path 1) knobs.  SPH_LP (default 1): lane-pair gathers in the row2
+// kernels; SPH_IV (default 1): the strided list is stored chunk-transposed so each lane's
+// four indices of a chunk are one 16-B load (sph_row2_kernels.h).
 static bool row2_lp() {
   static bool v = env_int("SPH_LP", 1) != 0;
   return v;
@@ -109,9 +68,9 @@ static bool row2_iv() {
   static bool v = env_int("SPH_IV", 1) != 0;
   return v;
 }
-static int row2_exp() {  // read per launch: tools/kernel_sweep.py sets it for the timed passes only
-  return env_int("SPH_EXP", 0);
-}
+// SPH_EXP: study variants of the pair passes (tools/kernel_sweep.py sets it for the timed
+// passes only, so it is read per launch); 0 in production
+static int row2_exp() { return env_int("SPH_EXP", 0); }
 // SPH_OVERLAP (default 0): with a brick decomposition, run the pair passes of interior
 // rows (no ghost in the list) on a second stream while the forward / rho halos are in
 // flight, then the boundary rows after them (sph_engine::pair_compute_overlap).  Parity
@@ -125,9 +84,10 @@ static bool tbits_env() {
   static bool v = env_int("SPH_TBITS", 1) != 0;
   return v;
 }
-// SPH_BLK (default 2): block shape of the block-staged path (SPH_BLK_SHAPES)
+// SPH_BLK (default 0 = 64-row blocks, 8 lanes x 4 slots; the fastest pair passes on C2 1M):
+// block shape of the block-staged path (SPH_BLK_SHAPES)
 static int blk_shape_env() {
-  static int v = env_int("SPH_BLK", 2);
+  static int v = env_int("SPH_BLK", 0);
   return v;
 }
 // (read per engine at sph_engine_create)
@@ -212,7 +172,7 @@ struct sph_engine {
   DBuf<int> qbeg, tb;
   DBuf<double4> xb;
   DBuf<unsigned> bkey, bkey2;
-  DBuf<int> bidx, bidx2, bstart, bend;
+  DBuf<int> bidx, bidx2;
   // neighbor list
   DBuf<int> cnt, off, nbr;
   int64_t nbr_total = 0;   // list entries (-1: strided list, counted on demand)
@@ -224,33 +184,14 @@ struct sph_engine {
   bool list_tbits = false; // strided entries carry the neighbour's type (SPH_TBIT_SHIFT)
   // this step's in-cut ("tight") list, written by the rhosum pass for the force pass
   DBuf<int> tnbr, tcnt;
-  // block-staged path (sph_blk_kernels.h): per block of blk_R rows its union of neighbour
-  // atoms (ulist, ucnt) and the rows' 16-bit slot lists (snbr, stride blk_sstride)
+  // block-staged path (production, sph_blk_kernels.h): per block of consecutive rows its
+  // union of neighbour atoms (ulist, ucnt) and the rows' 16-bit slot rows (snbr)
   bool blk = false;
-  int blk_sh = 2, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
+  int blk_sh = 0, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
   DBuf<int> ulist, ucnt, bl;
   DBuf<unsigned short> snbr;
-  // cluster-pair path (kernel_path 3): rows of CL_CI consecutive owned atoms, fixed
-  // stride cl_stride, counts ccl; rhosum accumulator racc
-  bool clustered = false;
-  DBuf<int> cnbr, ccl;
-  DBuf<double> racc;
-  int cl_stride = 0, cl_maxrow = 0;
-  bool full_counts = false;  // ccnt holds this build's full-list row counts
-  // LDS-tiled path: bin-sorted ghost index list and its inverse
-  bool tiled = false;
-  DBuf<int> gidx, gpos;
-  DBuf<unsigned> nbr32;   // packed thread-major slot pairs
-  // LDS-staged bin path
-  bool staged = false;
-  int stage_max = 0, rows_max = 0;
-  size_t lds_neigh = 0, lds_rho = 0, lds_force = 0;
-  DBuf<unsigned> okey, gkey;
-  DBuf<int> obeg, gbeg, binE, desc, roff, mx, ccnt;
-  DBuf<long long> blen, boff;
-  DBuf<unsigned short> nbr16;
-  DBuf<int> gowner2, gimg2;
-  long long *h_total = nullptr;
+  DBuf<int> mx, ccnt;  // scratch scalars; full-list row counts of the current build
+  DBuf<long long> blen;
   // cub scratch
   DBuf<unsigned char> tmp;
   // pinned host scalar
@@ -325,10 +266,9 @@ struct sph_engine {
     bkey2.reserve(n);
     bidx.reserve(n);
     bidx2.reserve(n);
-    // Morton order unless the staged path needs linear bins (and bins fit 10 bits/axis)
-    // Morton codes over cells of 1/div of a bin per axis (finer order inside a bin: a row's
-    // neighbors and the rows of one wave then occupy fewer, longer index runs, so the pair
-    // passes' gathers share more cache lines)
+    // Space-filling-curve order over cells of 1/div of a bin per axis (bins fit 10 bits per
+    // axis; else linear bins): consecutive rows are a compact region, so a block's union
+    // (block path) or a wave's gathers (row path) stay small and within one XCD's L2
     const int div = morton_div();
     Bins kbn = bn;
     for (int k = 0; k < 3; k++)
@@ -336,8 +276,7 @@ struct sph_engine {
         kbn.nb[k] = bn.nb[k] * div;
         kbn.inv[k] = bn.inv[k] * div;
       }
-    const bool mort = !want_staged() && !want_tiles() && kbn.nb[0] <= 1024 &&
-                      kbn.nb[1] <= 1024 && kbn.nb[2] <= 1024;
+    const bool mort = kbn.nb[0] <= 1024 && kbn.nb[1] <= 1024 && kbn.nb[2] <= 1024;
     if (!mort) kbn = bn;
     // the block path orders rows along a Hilbert curve (its blocks of consecutive rows stay
     // compact), the row path along a Morton curve
@@ -375,123 +314,11 @@ struct sph_engine {
     std::swap(ty, ty2);
     std::swap(vel, vel2);
     std::swap(tag, tag2);
-    okey.reserve(n);
-    SPH_HIP_TRY(hipMemcpyAsync(okey.p, bkey2.p, n * sizeof(unsigned), hipMemcpyDeviceToDevice, s));
   }
 
-  bool want_staged() const { return cfg.kernel_path == 0 && nlocal >= 2 && !multi(); }
-  bool want_blk() const { return cfg.kernel_path == 5; }
-  bool want_tiles() const { return cfg.kernel_path == 2; }
-  // cluster-pair path: kernel_path 3 = full cluster lists (gather only), 4 = half lists
-  // (Newton-3 updates by atomics); SPH_CLUSTER = atoms per cluster (4 or 8)
-  bool want_clusters() const {
-    return (cfg.kernel_path == 3 || cfg.kernel_path == 4) && neigh_q() == 2;
-  }
-  bool cl_half() const { return cfg.kernel_path == 4; }
-  int cl_ci() const { return cl_size(); }
-
-  // order the ghost segment by bin too (the staged ranges need it contiguous)
-  void sort_ghosts() {
-    const int ng = nghost;
-    if (ng == 0) return;
-    bkey.reserve(ng);
-    bkey2.reserve(ng);
-    bidx.reserve(ng);
-    bidx2.reserve(ng);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p, bkey.p, bidx.p, 0);
-    int endbit = 1;
-    while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, endbit, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, endbit, s));
-    xf2.reserve(ng);
-    vr2.reserve(ng);
-    en2.reserve(ng);
-    ty2.reserve(ng);
-    gowner2.reserve(ng);
-    gimg2.reserve(ng);
-    hipLaunchKernelGGL(k_permute_ghosts, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bidx2.p,
-                       xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p, xf2.p, vr2.p, en2.p, ty2.p,
-                       gowner2.p, gimg2.p);
-    SPH_HIP_TRY(hipMemcpyAsync(xf.p + nlocal, xf2.p, ng * sizeof(double4), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(vr.p + nlocal, vr2.p, ng * sizeof(double4), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(en.p + nlocal, en2.p, ng * sizeof(double), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(ty.p + nlocal, ty2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(gowner.p, gowner2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(gimg.p, gimg2.p, ng * sizeof(int), hipMemcpyDeviceToDevice, s));
-    gkey.reserve(ng);
-    SPH_HIP_TRY(hipMemcpyAsync(gkey.p, bkey2.p, ng * sizeof(unsigned), hipMemcpyDeviceToDevice, s));
-  }
-
-  BinCtx bin_ctx() const {
-    BinCtx c;
-    c.bn = bn;
-    c.dim = cfg.dim;
-    c.nbins = nbins;
-    c.nlocal = nlocal;
-    c.obeg = obeg.p;
-    c.gbeg = gbeg.p;
-    return c;
-  }
-
-  // LDS-staged full list (16-bit slots, thread-major per bin); false if it does not fit
-  bool build_staged() {
-    const int n = nlocal, ng = nghost;
-    obeg.reserve(nbins + 1);
-    gbeg.reserve(nbins + 1);
-    binE.reserve(nbins + 1);
-    desc.reserve((size_t)nbins * kDescInts);
-    roff.reserve(n + 1);
-    blen.reserve(nbins + 1);
-    boff.reserve(nbins + 1);
-    mx.reserve(2);
-    cnt.reserve(n + 1);
-    gkey.reserve(ng > 0 ? ng : 1);
-    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, n, 0, okey.p, obeg.p);
-    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, ng, n, gkey.p, gbeg.p);
-    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 2 * sizeof(int), s));
-    const BinCtx c = bin_ctx();
-    hipLaunchKernelGGL(k_bin_desc, dim3(blocks(nbins)), dim3(BLK), 0, s, c, desc.p, mx.p);
-    int hm[2];
-    SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    stage_max = hm[0];
-    rows_max = hm[1];
-    const bool nt = nt1(), heat = (force_mode & M_HEAT) != 0;
-    lds_neigh = kFixedNeigh + kNeighCoefBytes + (size_t)stage_max * neigh_atom_bytes();
-    lds_rho = kFixedRho + (nt ? 0 : kRhoCoefBytes) + (size_t)stage_max * rho_atom_bytes(nt);
-    lds_force = kFixedForce + (nt ? 0 : kForceCoefBytes) + (size_t)stage_max * force_atom_bytes(heat, nt);
-    const size_t lds_cap = 160 * 1024;
-    if (rows_max > MAXROWS || stage_max >= 65535 || lds_neigh > lds_cap || lds_rho > lds_cap ||
-        lds_force > lds_cap)
-      return false;
-    for (const void *k : {(const void *)k_bin_neigh<false>, (const void *)k_bin_neigh<true>})
-      SPH_HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_neigh));
-    hipLaunchKernelGGL((k_bin_neigh<false>), dim3(nbins), dim3(BT), lds_neigh, s, nbins, desc.p, xf.p,
-                       ty.p, dc, cnt.p, roff.p, binE.p, (const long long *)nullptr,
-                       (unsigned short *)nullptr);
-    hipLaunchKernelGGL(k_bin_listlen, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, binE.p, blen.p);
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, blen.p, boff.p, nbins + 1, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, blen.p, boff.p, nbins + 1, s));
-    SPH_HIP_TRY(hipMemcpyAsync(h_total, boff.p + nbins, sizeof(long long), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    const long long tot = *h_total;
-    nbr16.reserve(tot > 0 ? (size_t)tot : 1);
-    hipLaunchKernelGGL((k_bin_neigh<true>), dim3(nbins), dim3(BT), lds_neigh, s, nbins, desc.p, xf.p,
-                       ty.p, dc, cnt.p, roff.p, binE.p, boff.p, nbr16.p);
-    // entries proper (without padding) = sum of row counts
-    size_t tb2 = 0;
-    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tb2, binE.p, mx.p, nbins, s));
-    tmp_reserve(tb2);
-    SPH_HIP_TRY(hipcub::DeviceReduce::Sum(tmp.p, tb2, binE.p, mx.p, nbins, s));
-    nbr_total = read_scalar(mx.p);
-    nbr_maxrow = rows_max;
-    nbr_builds++;
-    return true;
-  }
+  // kernel_path 0: block-staged passes (production; the row path takes over for a build
+  // whose blocks overflow); 1: the row path (row2 gathers over the strided global list)
+  bool want_blk() const { return cfg.kernel_path == 0; }
 
   int read_scalar(const int *dptr) {
     SPH_HIP_TRY(hipMemcpyAsync(h_scalar, dptr, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -803,12 +630,12 @@ struct sph_engine {
       }
     }
     nbins = bn.nb[0] * bn.nb[1] * bn.nb[2];
-    // half-size bins of the CSR list builder (k_neigh2, reach 2)
+    // half-size bins of the list builders (k_neigh3, k_blk_neigh: reach 2)
     for (int k = 0; k < 3; k++) {
       const double ext = bn.nb[k] > 0 && bn.inv[k] > 0.0 ? bn.nb[k] / bn.inv[k] : 0.0;
       int nb = 1;
       if (k < cfg.dim) {
-        nb = (int)(ext / (neigh_q() == 2 ? 0.5 * cutneighmax : cutneighmax));
+        nb = (int)(ext / (0.5 * cutneighmax));
         if (nb < 1) nb = 1;
         if (nb > 8192) nb = 8192;
       }
@@ -821,13 +648,6 @@ struct sph_engine {
     nqbins = qb.nb[0] * qb.nb[1] * qb.nb[2];
   }
 
-  // Full list over half-size bins and a bin-ordered copy of all atoms: CSR (count pass,
-  // scan, fill pass) or, when `csr` is false and an earlier build sized the rows, one
-  // fill pass into fixed-stride rows (ccnt = row counts; `strided` records which).
-  void build_list_q(bool csr, bool rebin = true) {
-    if (rebin) bin_q();
-    list_q(csr);
-  }
   // bin-ordered copy of all atoms over the half-size bins (xb, tb, qbeg)
   void bin_q() {
     const int nall = nlocal + nghost;
@@ -857,54 +677,40 @@ struct sph_engine {
     hipLaunchKernelGGL(k_bin_copy, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bidx2.p, xf.p,
                        ty.p, xb.p, tb.p);
   }
-  // xi: positions of the owned rows (default: the current ones, as binned by bin_q)
+  // Global-index full list (k_neigh3, Neighbor::full_bin membership) of the owned rows at
+  // positions xi (default: the current ones, as binned by bin_q): CSR (count pass, scan,
+  // fill pass) or, when `csr` is false and an earlier build sized the rows, one fill pass
+  // into fixed-stride rows (ccnt = row counts; `strided` records which).
   void list_q(bool csr, const double4 *xi = nullptr) {
     const int n = nlocal, nall = nlocal + nghost;
     const double4 *const xi_src = xi ? xi : xf.p;
-    full_counts = true;
     ccnt.reserve(n + 1);
     off.reserve(n + 1);
-    constexpr int G = 8, U = 2;
+    constexpr int G = 8;
     dim3 grid(grid_for_rows(n, G)), block(BLK);
     auto launch = [&](bool fill, int stride) {
       if (n == 0) return;
-      const bool t = nt1(), q2 = neigh_q() == 2;
+      const bool t = nt1();
       int *const cnt_out = (!fill || stride > 0) ? ccnt.p : (int *)nullptr;
-#define SPH_NQ(F, T, R, TR)                                                                  \
-  hipLaunchKernelGGL((k_neigh2<G, U, F, T, R, TR>), grid, block, 0, s, n, qb, cfg.dim, xi_src, \
-                     ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
-                     (F && stride == 0) ? off.p : (const int *)nullptr,                        \
-                     F ? nbr.p : (int *)nullptr, stride, mx.p)
-      if (q2 && neigh3()) {
 #define SPH_N3(F, T)                                                                           \
   hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xi_src, ty.p, \
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,   \
                      list_perm_pi, (stride > 0 && list_tbits) ? 1 : 0)
-        if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
-        else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
+      if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
+      else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
-        return;
-      }
-      if (fill) {
-        if (q2) { if (t) SPH_NQ(true, true, 2, true); else SPH_NQ(true, false, 2, true); }
-        else { if (t) SPH_NQ(true, true, 1, false); else SPH_NQ(true, false, 1, false); }
-      } else {
-        if (q2) { if (t) SPH_NQ(false, true, 2, true); else SPH_NQ(false, false, 2, true); }
-        else { if (t) SPH_NQ(false, true, 1, false); else SPH_NQ(false, false, 1, false); }
-      }
-#undef SPH_NQ
     };
-    mx.reserve(4);
+    mx.reserve(8);
     // single pass into fixed-stride rows when a previous build sized them and nothing
-    // needs the CSR form (the setup half list, the tile/staged paths, row kernels gen < 2)
+    // needs the CSR form (the setup's half-list pass)
     if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
-      // rows stored chunk-transposed for the row2 kernels' 16-B index loads (k_neigh3 only)
-      // (the block path reads plain entries: no transposition, no type bits)
-      list_perm_g = (row2_iv() && neigh_q() == 2 && neigh3() && !want_blk()) ? row2_iv_g() : 0;
+      // rows stored chunk-transposed for the row2 kernels' 16-B index loads; with several
+      // types the neighbour's type rides in the entry's top bits
+      list_perm_g = row2_iv() ? row2_iv_g() : 0;
       list_perm_pi = row2_pi() ? 1 : 0;
-      list_tbits = !nt1() && tbits_env() && neigh_q() == 2 && neigh3() && !want_blk();
+      list_tbits = !nt1() && tbits_env();
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -940,347 +746,8 @@ struct sph_engine {
     // (whole chunks of the transposed layout, 16-B aligned rows)
     list_stride = ((hm[1] + hm[1] / 4 + 16) + 63) & ~63;
     nbr_maxrow = hm[1];
-    if (!staged) {
-      nbr_total = tot;
-      nbr_builds++;
-    }
-  }
-
-  // Cluster-pair list (sph_cluster_kernels.h) over the half-size bins: one pass into
-  // fixed-stride rows when an earlier build sized them (and no row overflows), else a
-  // count pass sizes the rows first.  False if the list would not fit 32-bit offsets.
-  template <int CI, bool HALF>
-  void cl_neigh_launch(int *nbrp, int stride) {
-    const int nc = (nlocal + CI - 1) / CI;
-    const dim3 grid((nc + 3) / 4), block(256);
-    if (nt1())
-      hipLaunchKernelGGL((k_cl_neigh<CI, HALF, true>), grid, block, 0, s, nlocal, qb, cfg.dim,
-                         xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, ccl.p, nbrp, stride, mx.p);
-    else
-      hipLaunchKernelGGL((k_cl_neigh<CI, HALF, false>), grid, block, 0, s, nlocal, qb, cfg.dim,
-                         xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, ccl.p, nbrp, stride, mx.p);
-  }
-  void cl_neigh(int *nbrp, int stride) {
-    const bool h = cl_half();
-    if (cl_ci() == 8) { if (h) cl_neigh_launch<8, true>(nbrp, stride); else cl_neigh_launch<8, false>(nbrp, stride); }
-    else { if (h) cl_neigh_launch<4, true>(nbrp, stride); else cl_neigh_launch<4, false>(nbrp, stride); }
-  }
-  int cl_count() const { return (nlocal + cl_ci() - 1) / cl_ci(); }
-  bool build_clusters() {
-    const int n = nlocal, nall = nlocal + nghost;
-    const int nc = cl_count();
-    ccl.reserve(nc + 1);
-    mx.reserve(4);
-    if (n == 0) return true;
-    for (int pass = 0; pass < 2; pass++) {
-      if (cl_stride > 0 && row2_fits((long)nall, (long)nc * cl_stride)) {
-        cnbr.reserve((size_t)nc * cl_stride);
-        SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
-        cl_neigh(cnbr.p, cl_stride);
-        if (read_scalar(mx.p) == 0) {
-          nbr_builds++;
-          return true;
-        }
-      }
-      cl_neigh(nullptr, 0);  // row counts only
-      size_t tb3 = 0;
-      SPH_HIP_TRY(hipcub::DeviceReduce::Max(nullptr, tb3, ccl.p, mx.p + 1, nc, s));
-      tmp_reserve(tb3);
-      SPH_HIP_TRY(hipcub::DeviceReduce::Max(tmp.p, tb3, ccl.p, mx.p + 1, nc, s));
-      cl_maxrow = read_scalar(mx.p + 1);
-      // longest row + 25% + 16 (a later build's rows may grow), whole 64-entry blocks
-      cl_stride = ((cl_maxrow + cl_maxrow / 4 + 16) + 63) & ~63;
-      if (!row2_fits((long)nall, (long)nc * cl_stride)) return false;
-    }
-    return false;
-  }
-  // the full list's row counts of the current build (stats, sph_engine_neighbor_counts):
-  // built on demand on the cluster path, which does not need the full list
-  // (the owned rows' positions as of the build are recovered from the binned copy xb)
-  void ensure_full_counts() {
-    if (full_counts || !clustered) return;
-    const int builds = nbr_builds, nall = nlocal + nghost;
-    DBuf<double4> xbuild;
-    xbuild.reserve(nall);
-    hipLaunchKernelGGL(k_unbin, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xb.p, xbuild.p);
-    list_q(true, xbuild.p);
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    xbuild.release();
-    nbr_builds = builds;
-  }
-  ClArgs cl_args() {
-    ClArgs a{};
-    a.n = nlocal;
-    a.nall = nlocal + nghost;
-    a.stride = cl_stride;
-    a.ntot = (int)((long)cl_count() * cl_stride);
-    a.cnt = ccl.p;
-    a.nbr = cnbr.p;
-    a.xf = xf.p;
-    a.vr = vr.p;
-    a.ty = ty.p;
-    a.en = en.p;
-    a.cf = dc;
-    a.fo = fo.p;
-    a.de = de.p;
-    a.racc = racc.p;
-    a.gx = cfg.gravity[0];
-    a.gy = cfg.gravity[1];
-    a.gz = cfg.gravity[2];
-    a.exp = cl_exp();
-    return a;
-  }
-  template <int CI, bool HALF>
-  void cl_rhosum_ci(const ClArgs &a) {
-    const dim3 grid((cl_count() + 3) / 4), block(256);
-    if (nt1()) hipLaunchKernelGGL((k_cl_rhosum<CI, HALF, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((k_cl_rhosum<CI, HALF, false>), grid, block, 0, s, a);
-  }
-  void cl_rhosum() {
-    const int n = nlocal;
-    if (n == 0) return;
-    const bool h = cl_half();
-    if (h) {
-      racc.reserve(n);
-      SPH_HIP_TRY(hipMemsetAsync(racc.p, 0, n * sizeof(double), s));
-    }
-    const ClArgs a = cl_args();
-    if (cl_ci() == 8) { if (h) cl_rhosum_ci<8, true>(a); else cl_rhosum_ci<8, false>(a); }
-    else { if (h) cl_rhosum_ci<4, true>(a); else cl_rhosum_ci<4, false>(a); }
-    if (h)
-      hipLaunchKernelGGL(k_cl_rho_final<true>, dim3(blocks(n)), dim3(BLK), 0, s, n, racc.p,
-                         ty.p, dc, xf.p, vr.p);
-  }
-  template <int CI, int V, int M>
-  void cl_force_t(const ClArgs &a) {
-    const dim3 grid((cl_count() + 3) / 4), block(256);
-    const bool h = cl_half();
-    if (nt1()) {
-      if (h) hipLaunchKernelGGL((k_cl_force<CI, V, M, true, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((k_cl_force<CI, V, M, true, false>), grid, block, 0, s, a);
-    } else {
-      if (h) hipLaunchKernelGGL((k_cl_force<CI, V, M, false, true>), grid, block, 0, s, a);
-      else hipLaunchKernelGGL((k_cl_force<CI, V, M, false, false>), grid, block, 0, s, a);
-    }
-  }
-  template <int CI>
-  void cl_force_ci(const ClArgs &a) {
-    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
-    switch (force_mode) {
-      case M_TAIT:
-        if (mor) cl_force_t<CI, 1, M_TAIT>(a);
-        else cl_force_t<CI, 0, M_TAIT>(a);
-        break;
-      case M_TAIT | M_HEAT:
-        if (mor) cl_force_t<CI, 1, M_TAIT | M_HEAT>(a);
-        else cl_force_t<CI, 0, M_TAIT | M_HEAT>(a);
-        break;
-      default: cl_force_t<CI, 0, M_HEAT>(a); break;
-    }
-  }
-  void cl_force() {
-    const int n = nlocal;
-    if (n == 0) return;
-    if (cl_half()) {
-      SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, n * sizeof(double4), s));
-      SPH_HIP_TRY(hipMemsetAsync(de.p, 0, n * sizeof(double), s));
-    }
-    const ClArgs a = cl_args();
-    if (cl_ci() == 8) cl_force_ci<8>(a);
-    else cl_force_ci<4>(a);
-  }
-
-  void build_bins() {
-    const int nall = nlocal + nghost;
-    bkey.reserve(nall);
-    bkey2.reserve(nall);
-    bidx.reserve(nall);
-    bidx2.reserve(nall);
-    bstart.reserve(nbins);
-    bend.reserve(nbins);
-    hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, bn, xf.p, bkey.p, bidx.p, 0);
-    int endbit = 1;
-    while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
-    SPH_HIP_TRY(hipMemsetAsync(bstart.p, 0, nbins * sizeof(int), s));
-    SPH_HIP_TRY(hipMemsetAsync(bend.p, 0, nbins * sizeof(int), s));
-    hipLaunchKernelGGL(k_bin_bounds, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bkey2.p, bstart.p, bend.p);
-  }
-
-  void build_list() {
-    constexpr int G = 8;
-    const int n = nlocal;
-    ccnt.reserve(n + 1);
-    off.reserve(n + 1);
-    dim3 grid(grid_for_rows(n, G)), block(BLK);
-    if (n > 0)
-      hipLaunchKernelGGL((k_neigh<G, false>), grid, block, 0, s, n, bn, cfg.dim, xf.p, ty.p, bidx2.p,
-                         bstart.p, bend.p, dc, ccnt.p, (const int *)nullptr, (int *)nullptr);
-    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, off.p, off.p, n + 1, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, off.p, off.p, n + 1, s));
-    // total (int32 offsets: SPH_HIP_EOVERFLOW beyond 2^31-1 entries)
-    const int tot = read_scalar(off.p + n);
-    SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
-    nbr.reserve(tot > 0 ? tot : 1);
-    if (n > 0)
-      hipLaunchKernelGGL((k_neigh<G, true>), grid, block, 0, s, n, bn, cfg.dim, xf.p, ty.p, bidx2.p,
-                         bstart.p, bend.p, dc, (int *)nullptr, off.p, nbr.p);
-    if (!staged) {
-      nbr_total = tot;
-      nbr_builds++;
-    }
-  }
-
-  template <int DIM, bool NT1>
-  void bin_rhosum_t() {
-    auto k = k_bin_rhosum<DIM, NT1>;
-    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rho));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_rho, s, nbins, desc.p, xf.p, ty.p, vr.p,
-                       roff.p, boff.p, nbr16.p, dc);
-  }
-  void launch_bin_rhosum() {
-    if (cfg.dim == 3) {
-      if (nt1()) bin_rhosum_t<3, true>(); else bin_rhosum_t<3, false>();
-    } else {
-      if (nt1()) bin_rhosum_t<2, true>(); else bin_rhosum_t<2, false>();
-    }
-  }
-  template <int DIM, int VISC, int MODE, bool NT1>
-  void bin_force_t() {
-    auto k = k_bin_force<DIM, VISC, MODE, NT1>;
-    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(BT), lds_force, s, nbins, desc.p, xf.p, vr.p, ty.p,
-                       en.p, roff.p, boff.p, nbr16.p, dc, fo.p, de.p, cfg.gravity[0],
-                       cfg.gravity[1], cfg.gravity[2]);
-  }
-  template <int DIM, bool NT1>
-  void bin_force_d() {
-    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
-    switch (force_mode) {
-      case M_TAIT:
-        if (mor) bin_force_t<DIM, 1, M_TAIT, NT1>(); else bin_force_t<DIM, 0, M_TAIT, NT1>();
-        break;
-      case M_TAIT | M_HEAT:
-        if (mor) bin_force_t<DIM, 1, M_TAIT | M_HEAT, NT1>();
-        else bin_force_t<DIM, 0, M_TAIT | M_HEAT, NT1>();
-        break;
-      case M_HEAT: bin_force_t<DIM, 0, M_HEAT, NT1>(); break;
-      default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", force_mode);
-    }
-  }
-  void launch_bin_force() {
-    if (cfg.dim == 3) {
-      if (nt1()) bin_force_d<3, true>(); else bin_force_d<3, false>();
-    } else {
-      if (nt1()) bin_force_d<2, true>(); else bin_force_d<2, false>();
-    }
-  }
-
-  // ---- LDS-tiled path (sph_tile_kernels.h) ---------------------------------------------
-  // Owned atoms are sorted by linear bin (sort_owned); ghosts stay where borders() put
-  // them and are reached through a bin-sorted index list (gidx, gbeg) and its inverse
-  // (gpos).  Bin descriptors (staged ranges) as for the staged path, then the CSR list is
-  // translated into thread-major 16-bit slot lists.  Returns false (CSR fallback) when a
-  // bin has too many rows or the LDS image does not fit.
-  bool build_tiles() {
-    const int n = nlocal, ng = nghost;
-    obeg.reserve(nbins + 1);
-    gbeg.reserve(nbins + 1);
-    desc.reserve((size_t)nbins * kDescInts);
-    mx.reserve(4);
-    gidx.reserve(ng > 0 ? ng : 1);
-    gpos.reserve(ng > 0 ? ng : 1);
-    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, n, 0,
-                       okey.p, obeg.p);
-    if (ng > 0) {
-      bkey.reserve(ng);
-      bkey2.reserve(ng);
-      bidx.reserve(ng);
-      hipLaunchKernelGGL(k_bin_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, bn, xf.p,
-                         bkey.p, bidx.p, 0);
-      int endbit = 1;
-      while ((1u << endbit) < (unsigned)nbins && endbit < 32) endbit++;
-      size_t tb = 0;
-      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, gidx.p, ng, 0, endbit, s));
-      tmp_reserve(tb);
-      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, gidx.p, ng, 0, endbit, s));
-      hipLaunchKernelGGL(k_inverse_perm, dim3(blocks(ng)), dim3(BLK), 0, s, ng, nlocal, gidx.p,
-                         gpos.p);
-    }
-    hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, ng, 0,
-                       bkey2.p, gbeg.p);
-    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 4 * sizeof(int), s));
-    BinCtx c = bin_ctx();
-    hipLaunchKernelGGL(k_bin_desc, dim3(blocks(nbins)), dim3(BLK), 0, s, c, desc.p, mx.p);
-    blen.reserve(nbins + 1);
-    boff.reserve(nbins + 1);
-    hipLaunchKernelGGL(k_tile_plan, dim3(blocks(nbins + 1)), dim3(BLK), 0, s, nbins, desc.p,
-                       off.p, blen.p, mx.p);
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, blen.p, boff.p, nbins + 1, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, blen.p, boff.p, nbins + 1, s));
-    int hm[4];
-    SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipMemcpyAsync(h_total, boff.p + nbins, sizeof(long long), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    stage_max = hm[0];
-    rows_max = hm[1];
-    if (hm[2] != 0 || hm[3] > TILE_LMAX || stage_max >= 65535 || rows_max < 1) return false;
-    const bool nt = nt1(), heat = (force_mode & M_HEAT) != 0;
-    lds_rho = tile_lds_bytes(false, false, nt, stage_max, rows_max);
-    lds_force = tile_lds_bytes(true, heat, nt, stage_max, rows_max);
-    if (lds_rho > 160 * 1024 || lds_force > 160 * 1024) return false;
-    const long long tot = *h_total;
-    nbr32.reserve(tot > 0 ? (size_t)tot : 1);
-    SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_tile_translate, dim3(nbins), dim3(TB), 0, s, nbins, nlocal, desc.p,
-                       off.p, nbr.p, gpos.p, boff.p, nbr32.p, mx.p);
-    if (read_scalar(mx.p) != 0) return false;  // a neighbor outside the staged bins
-    return true;
-  }
-
-  template <bool NT1>
-  void tile_rhosum_t() {
-    auto k = k_tile_rhosum<NT1>;
-    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_rho));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(TB), lds_rho, s, nbins, rows_max, desc.p, gidx.p,
-                       xf.p, ty.p, vr.p, off.p, boff.p, nbr32.p, dc);
-  }
-  template <int VISC, int MODE, bool NT1>
-  void tile_force_t() {
-    auto k = k_tile_force<VISC, MODE, NT1>;
-    SPH_HIP_TRY(hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
-    hipLaunchKernelGGL(k, dim3(nbins), dim3(TB), lds_force, s, nbins, rows_max, desc.p, gidx.p,
-                       xf.p, vr.p, ty.p, en.p, off.p, boff.p, nbr32.p, dc, fo.p, de.p,
-                       cfg.gravity[0], cfg.gravity[1], cfg.gravity[2]);
-  }
-  template <bool NT1>
-  void tile_force_n() {
-    const bool mor = cfg.tait_visc == SPH_VISC_MORRIS;
-    switch (force_mode) {
-      case M_TAIT:
-        if (mor) tile_force_t<1, M_TAIT, NT1>(); else tile_force_t<0, M_TAIT, NT1>();
-        break;
-      case M_TAIT | M_HEAT:
-        if (mor) tile_force_t<1, M_TAIT | M_HEAT, NT1>();
-        else tile_force_t<0, M_TAIT | M_HEAT, NT1>();
-        break;
-      case M_HEAT: tile_force_t<0, M_HEAT, NT1>(); break;
-      default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "unsupported force mode %d", force_mode);
-    }
-  }
-  void launch_tile_rhosum() {
-    if (nt1()) tile_rhosum_t<true>(); else tile_rhosum_t<false>();
-  }
-  void launch_tile_force() {
-    if (nt1()) tile_force_n<true>(); else tile_force_n<false>();
+    nbr_total = tot;
+    nbr_builds++;
   }
 
   // Block unions + slot rows straight from the bins (k_blk_neigh; bin_q() must have run) in
@@ -1291,10 +758,23 @@ struct sph_engine {
     if (n == 0) return false;
     mx.reserve(8);
     ccnt.reserve(n + 1);
-    const int shape = blk_shape_env();
+    if (blk_rowcap == 0) blk_rowcap = std::max(list_stride, nbr_maxrow + nbr_maxrow / 4 + 16);
+    // the SPH_BLK shape, then 32-row blocks (smaller unions) if its blocks do not fit
+    const int first = blk_shape_env();
+    for (int shape : {first, 1}) {
+      if (shape == 1 && first == 1) break;
+      const int r = build_blk_shape(shape);
+      if (r == 1) return true;
+      if (r == 2) continue;   // a union too large for the LDS image: smaller blocks
+      return false;
+    }
+    return false;
+  }
+  // 1 = built, 2 = a block overflowed (candidates, bin table or LDS image), 0 = failed
+  int build_blk_shape(int shape) {
+    const int n = nlocal;
     const BlkShape sh = blk_shape(shape);
     const int chunk = sh.G * sh.U;
-    if (blk_rowcap == 0) blk_rowcap = std::max(list_stride, nbr_maxrow + nbr_maxrow / 4 + 16);
     for (int attempt = 0; attempt < 2; attempt++) {
       blk_sstride = (std::max(blk_rowcap, 1) + chunk - 1) / chunk * chunk;
       snbr.reserve((size_t)n * blk_sstride + 2 * chunk);  // + the pair passes' prefetch pad
@@ -1314,29 +794,35 @@ struct sph_engine {
                 "candidates max %d mean %.1f\n",
                 shape, n, blk_rowcap, hm[0], hm[1], (double)hm[4] / nb, hm[2],
                 (double)hm[3] / nb);
-      if (env_int("SPH_DEBUG", 0) && hm[0] == 0) fprintf(stderr, "[sph] (stats above)\n");
-      if (hm[0] == 0) {
-        blk_sh = shape;
-        blk_um = std::max(hm[1], 1);
-        // the force pass's LDS image: ~1.25x the mean union (64-record steps), the blocks
-        // above it in a second launch (k_blk_large)
-        const double mean = (double)hm[4] / nb;
-        blk_umf = std::min(blk_um, ((int)(1.25 * mean) + 63) / 64 * 64);
-        if (env_int("SPH_BLKUMF", 0) > 0) blk_umf = std::min(blk_um, env_int("SPH_BLKUMF", 0));
-        blk_nbig = 0;
-        if (blk_umf < blk_um) {
-          bl.reserve(nb);
-          SPH_HIP_TRY(hipMemsetAsync(mx.p + 5, 0, sizeof(int), s));
-          hipLaunchKernelGGL(k_blk_large, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p, blk_umf,
-                             bl.p, mx.p + 5);
-          blk_nbig = read_scalar(mx.p + 5);
-        }
-        return true;
+      if (hm[0] == (1 << 21)) {  // a row outgrew the slot-row stride
+        blk_rowcap *= 2;
+        continue;
       }
-      if (hm[0] != (1 << 21)) return false;  // a block overflowed its LDS image
-      blk_rowcap *= 2;                        // a row outgrew the slot-row stride
+      if (hm[0] != 0) return 2;
+      // the largest union's force-pass LDS image (+ the static coefficient tables) must fit
+      // the CU's 160 KiB
+      const size_t lds_big = blk_force_lds(std::max(hm[1], 1), (force_mode & M_HEAT) != 0,
+                                           nt1()) +
+                             (nt1() ? 0 : (sizeof(TaitPair) + sizeof(HeatPair)) * NT2);
+      if (lds_big > 160 * 1024 - 1024) return 2;
+      blk_sh = shape;
+      blk_um = std::max(hm[1], 1);
+      // the force pass's LDS image: ~1.25x the mean union (64-record steps), the blocks
+      // above it in a second launch (k_blk_large)
+      const double mean = (double)hm[4] / nb;
+      blk_umf = std::min(blk_um, ((int)(1.25 * mean) + 63) / 64 * 64);
+      if (env_int("SPH_BLKUMF", 0) > 0) blk_umf = std::min(blk_um, env_int("SPH_BLKUMF", 0));
+      blk_nbig = 0;
+      if (blk_umf < blk_um) {
+        bl.reserve(nb);
+        SPH_HIP_TRY(hipMemsetAsync(mx.p + 5, 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_blk_large, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p, blk_umf,
+                           bl.p, mx.p + 5);
+        blk_nbig = read_scalar(mx.p + 5);
+      }
+      return 1;
     }
-    return false;
+    return 0;
   }
   BlkArgs blk_args() const {
     BlkArgs k;
@@ -1356,58 +842,34 @@ struct sph_engine {
     return k;
   }
 
-  // pbc + sort + borders + list(s); `need_csr` also builds the global-index CSR list
+  // pbc + sort + borders + bins + list(s); `need_csr` also builds the global-index CSR
+  // list (the setup's half-list pass walks it).  Block path: the block unions + slot rows
+  // from the bins (no global-index list on a plain rebuild); the row path's strided list
+  // if a block overflows its LDS image.
   void build_all(bool need_csr) {
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
     if (multi()) exchange_multi();
-    const bool st = want_staged();
-    if (st || cfg.sort || want_tiles() || want_clusters()) sort_owned();
+    if (cfg.sort) sort_owned();
     borders();
-    staged = false;
-    tiled = false;
+    bin_q();
     blk = false;
-    if (st) {
-      sort_ghosts();
-      staged = build_staged();
-    }
-    clustered = false;
-    full_counts = false;
-    if (want_clusters()) {
-      bin_q();
-      clustered = build_clusters();
-      if (need_csr || !clustered) build_list_q(true, /*rebin=*/false);
-    } else if (want_blk() && !staged && neigh_q() == 2) {
-      // block path: bins, the global-index CSR list only where the setup's half-list pass
-      // needs it, then the block unions + slot rows from the bins; the row path's strided
-      // list if a block overflows
-      bin_q();
-      if (need_csr) list_q(true);
+    if (need_csr || !want_blk()) list_q(need_csr);
+    if (want_blk()) {
       blk = build_blk();
-      if (blk) {
-        if (!need_csr) {
-          strided = true;  // (ccnt holds the full-list counts; list_entries sums them)
-          nbr_total = -1;
-          full_counts = true;
-          nbr_builds++;
-        }
-      } else if (!need_csr) {
+      if (blk && !need_csr) {
+        strided = true;  // (ccnt holds the full-list counts; list_entries sums them)
+        nbr_total = -1;
+        nbr_builds++;
+      } else if (!blk && !need_csr) {
         list_q(false);
       }
-    } else if (!staged || need_csr) {
-      if (neigh_q()) {
-        build_list_q(need_csr || st || want_tiles() || row_gen() != 2);
-      } else {
-        build_bins();
-        build_list();
-      }
     }
-    if (want_tiles() && nlocal > 0) tiled = build_tiles();
     ov_ready = false;
     if (overlap_on()) classify_rows();
   }
 
   bool overlap_on() const {
-    return multi() && overlap && !staged && !tiled && !clustered && !blk && use_row2() &&
+    return multi() && overlap && !blk && use_row2() &&
            !tight_on() && (force_mode & M_TAIT) != 0 && cfg.rhosum_nstep > 0;
   }
   // interior rows (no ghost in the list) and boundary rows, each in row order
@@ -1539,41 +1001,32 @@ struct sph_engine {
     b.tbits = strided && list_tbits;
     return b;
   }
-  bool use_row2() const {
-    return row_gen() == 2 && row2_fits((long)nlocal + nghost, (long)list_span());
-  }
+  bool use_row2() const { return row2_fits((long)nlocal + nghost, (long)list_span()); }
 
+  // rhosum (+ the EOS epilogue) -> forward rho -> taitwater[/morris][+heat] on the current
+  // list: block path, row path (row2 kernels), or the generic CSR kernels for a list past
+  // the row2 kernels' 32-bit offsets.  The setup step's force pass walks the half list.
   void pair_compute(bool do_rhosum, bool setup = false) {
     const int nall = nlocal + nghost;
     bool tight = false;
     if (do_rhosum) {
       {
         Scope t(this, T_RHO);
-        if (clustered && !setup) {
-          cl_rhosum();
-        } else if (blk) {
+        if (blk) {
           blk_rhosum(nt1(), s, blk_args(), xf.p, ty.p, vr.p, dc);
-        } else if (staged) {
-          launch_bin_rhosum();
-        } else if (tiled) {
-          launch_tile_rhosum();
-        } else {
-          if (use_row2()) {
-            Row2Args b = row2_args();
-            if (strided && row2_lp() && tight_on() && force_mode && !setup) {
-              tnbr.reserve((size_t)list_span());
-              tcnt.reserve(nlocal > 0 ? nlocal : 1);
-              b.tnbr = tnbr.p;
-              b.tcnt = tcnt.p;
-              tight = true;
-            }
-            row2_rhosum(nt1(), s, b);
-          } else if (row_kernels()) {
-            row_rhosum(nt1(), s, row_args());
-          } else {
-            RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
-            launch_rhosum(cfg.dim, true, nt1(), s, ra);
+        } else if (use_row2()) {
+          Row2Args b = row2_args();
+          if (strided && row2_lp() && tight_on() && force_mode && !setup) {
+            tnbr.reserve((size_t)list_span());
+            tcnt.reserve(nlocal > 0 ? nlocal : 1);
+            b.tnbr = tnbr.p;
+            b.tcnt = tcnt.p;
+            tight = true;
           }
+          row2_rhosum(nt1(), s, b);
+        } else {
+          RhoArgs ra{nlocal, nullptr, off.p, nbr.p, xf.p, ty.p, vr.p, nullptr, dc};
+          launch_rhosum(cfg.dim, true, nt1(), s, ra);
         }
       }
       if (multi()) {
@@ -1589,18 +1042,9 @@ struct sph_engine {
     }
     if (force_mode && setup) {
       setup_forces_half();
-    } else if (force_mode && clustered) {
-      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      cl_force();
     } else if (force_mode && blk) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       blk_force(nt1(), cfg.tait_visc, force_mode, s, blk_args(), row_args());
-    } else if (force_mode && staged) {
-      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      launch_bin_force();
-    } else if (force_mode && tiled) {
-      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      launch_tile_force();
     } else if (force_mode && use_row2()) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       Row2Args b = row2_args();
@@ -1610,9 +1054,6 @@ struct sph_engine {
         b.iv = false;
       }
       row2_force(nt1(), cfg.tait_visc, force_mode, s, b);
-    } else if (force_mode && row_kernels()) {
-      Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      row_force(nt1(), cfg.tait_visc, force_mode, s, row_args());
     } else if (force_mode) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       ForceArgs a{};
@@ -1853,7 +1294,6 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     SPH_HIP_TRY(hipMalloc(&e->dc, sizeof(Coefs)));
     SPH_HIP_TRY(hipMemcpy(e->dc, &e->hc, sizeof(Coefs), hipMemcpyHostToDevice));
     SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));
-    SPH_HIP_TRY(hipHostMalloc(&e->h_total, sizeof(long long)));
   } catch (...) {
     delete e;
     throw;
@@ -1867,55 +1307,27 @@ int sph_engine_destroy(sph_engine *e) {
   if (!e) return SPH_HIP_OK;
   (void)hipSetDevice(e->device);
   if (e->s) (void)hipStreamSynchronize(e->s);
-  for (auto *b : {&e->xf, &e->vr, &e->vel, &e->fo, &e->xf2, &e->vr2, &e->vel2}) b->release();
-  e->en.release();
-  e->en2.release();
-  e->de.release();
-  for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel, &e->bidx,
-                  &e->bidx2, &e->bstart, &e->bend, &e->cnt, &e->off, &e->nbr})
+  if (e->s2) (void)hipStreamSynchronize(e->s2);
+  for (auto *b : {&e->xf, &e->vr, &e->vel, &e->fo, &e->xf2, &e->vr2, &e->vel2, &e->xb}) b->release();
+  for (auto *b : {&e->en, &e->en2, &e->de}) b->release();
+  for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
+                  &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
+                  &e->ccnt, &e->qbeg, &e->tb, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
+                  &e->tcnt, &e->ulist, &e->ucnt, &e->bl})
     b->release();
-  e->bkey.release();
-  e->bkey2.release();
-  e->flags.release();
-  e->tmp.release();
+  for (auto *b : {&e->bkey, &e->bkey2}) b->release();
+  for (auto *b : {&e->flags, &e->tmp, &e->cbs, &e->cbr, &e->flag2, &e->fl_in, &e->fl_bd}) b->release();
+  e->snbr.release();
+  e->blen.release();
+  for (auto &sw : e->swaps) sw.list.release();
   for (auto &p : e->pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
   }
   for (auto ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->h_scalar) (void)hipHostFree(e->h_scalar);
-  if (e->h_total) (void)hipHostFree(e->h_total);
-  for (auto *b : {&e->obeg, &e->gbeg, &e->binE, &e->desc, &e->roff, &e->mx, &e->ccnt, &e->gowner2, &e->gimg2})
-    b->release();
-  e->okey.release();
-  e->gkey.release();
-  e->qbeg.release();
-  e->tb.release();
-  e->xb.release();
-  for (auto &sw : e->swaps) sw.list.release();
-  e->cbs.release();
-  e->cbr.release();
-  e->flag2.release();
-  e->sel2.release();
   delete e->tr;
-  e->blen.release();
-  e->boff.release();
-  e->gidx.release();
-  e->gpos.release();
-  e->tnbr.release();
-  e->tcnt.release();
-  e->nbr32.release();
-  e->nbr16.release();
-  e->ulist.release();
-  e->ucnt.release();
-  e->bl.release();
-  e->snbr.release();
   if (e->dc) (void)hipFree(e->dc);
-  e->rows_in.release();
-  e->rows_bd.release();
-  e->fl_in.release();
-  e->fl_bd.release();
-  if (e->s2) (void)hipStreamSynchronize(e->s2);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->s2) (void)hipStreamDestroy(e->s2);
@@ -2065,9 +1477,8 @@ int sph_engine_neighbor_counts(sph_engine *e, int *numneigh) {
   SPH_HIP_TRY(hipSetDevice(e->device));
   const int n = e->nlocal;
   if (n == 0) return SPH_HIP_OK;
-  e->ensure_full_counts();
   std::vector<int> hc(n), ht(n);
-  SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->staged ? e->cnt.p : e->ccnt.p, n * sizeof(int),
+  SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->ccnt.p, n * sizeof(int),
                              hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
@@ -2084,12 +1495,11 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->step = e->step;
   st->nlocal = e->nlocal;
   st->nghost = e->nghost;
-  e->ensure_full_counts();
   st->nbr_full = e->list_entries();
   st->nbr_builds = e->nbr_builds;
   st->nbr_maxrow = e->nbr_maxrow;
-  st->staged = e->staged ? 1 : (e->tiled ? 2 : (e->clustered ? 3 : (e->blk ? 5 : 0)));
-  st->stage_max = e->stage_max;
+  st->staged = e->blk ? 1 : 0;
+  st->stage_max = e->blk ? e->blk_um : 0;
   st->ms_rhosum = e->ms[T_RHO];
   st->ms_tait = e->ms[T_TAIT];
   st->ms_heat = e->ms[T_HEAT];

@@ -318,14 +318,18 @@ static __global__ void k_bin_keys(int n, int first, Bins bn, const double4 *__re
   idx[k] = first + k;
 }
 
-// bin start/end from sorted keys
-static __global__ void k_bin_bounds(int n, const unsigned *__restrict__ skey,
-                                    int *__restrict__ bstart, int *__restrict__ bend) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const unsigned k = skey[p];
-  if (p == 0 || skey[p - 1] != k) bstart[k] = p;
-  if (p == n - 1 || skey[p + 1] != k) bend[k] = p + 1;
+// per-bin lower bounds of sorted keys: beg[b] = first p with key[p] >= b (b in [0,nbins])
+static __global__ void k_lower_bound(int nbins, int n, int base, const unsigned *__restrict__ key,
+                                     int *__restrict__ beg) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nbins) return;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (key[mid] < (unsigned)b) lo = mid + 1;
+    else hi = mid;
+  }
+  beg[b] = base + lo;
 }
 
 // permutation gather for the spatial sort of owned atoms (atom->sort analogue)
@@ -345,79 +349,6 @@ static __global__ void k_permute(int n, const int *__restrict__ perm,
   ty2[i] = ty[s];
   vel2[i] = vel[s];
   tag2[i] = tag[s];
-}
-
-// ---- binned full list: count pass and fill pass (G lanes per owned atom) ----------------
-template <int G, bool FILL>
-__global__ void __launch_bounds__(256)
-k_neigh(int nlocal, Bins bn, int dim, const double4 *__restrict__ xf,
-        const int *__restrict__ ty, const int *__restrict__ bidx,
-        const int *__restrict__ bstart, const int *__restrict__ bend,
-        const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-        int *__restrict__ nbr) {
-  __shared__ double s_cns[NT2];
-  const int nt1 = cf->ntypes + 1;
-  for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
-  __syncthreads();
-  const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
-  const int lane = threadIdx.x & (G - 1);
-  if (i >= nlocal) return;
-  const double4 xi = xf[i];
-  const double *crow = s_cns + ty[i] * nt1;
-  const int cx = bin_coord(xi.x, bn.lo[0], bn.inv[0], bn.nb[0]);
-  const int cy = bin_coord(xi.y, bn.lo[1], bn.inv[1], bn.nb[1]);
-  const int cz = bin_coord(xi.z, bn.lo[2], bn.inv[2], bn.nb[2]);
-  const int zr = (dim == 3) ? 1 : 0;
-  int n = 0;
-  int pos = FILL ? off[i] : 0;
-  const int gbase = (threadIdx.x & 63) & ~(G - 1);
-  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
-  for (int oz = -zr; oz <= zr; oz++) {
-    const int bz = cz + oz;
-    if (bz < 0 || bz >= bn.nb[2]) continue;
-    for (int oy = -1; oy <= 1; oy++) {
-      const int by = cy + oy;
-      if (by < 0 || by >= bn.nb[1]) continue;
-      const int brow = (bz * bn.nb[1] + by) * bn.nb[0];
-      // the three x-bins of a row are contiguous in the sorted order
-      const int bx0 = cx > 0 ? cx - 1 : 0;
-      const int bx1 = cx < bn.nb[0] - 1 ? cx + 1 : bn.nb[0] - 1;
-      int s = 0x7fffffff, e = 0;
-      for (int bx = bx0; bx <= bx1; bx++) {
-        const int b = brow + bx;
-        const int bs = bstart[b], be = bend[b];
-        if (be > bs) {
-          s = min(s, bs);
-          e = max(e, be);
-        }
-      }
-      for (int base = s; base < e; base += G) {
-        const int p = base + lane;
-        bool hit = false;
-        int j = -1;
-        if (p < e) {
-          j = bidx[p];
-          if (j != i) {
-            const double4 xj = xf[j];
-            const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-            const double rsq = dx * dx + dy * dy + dz * dz;
-            hit = rsq <= crow[ty[j]];
-          }
-        }
-        if (FILL) {
-          const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
-          if (hit) nbr[pos + __popcll(m & ((1ull << lane) - 1ull))] = j;
-          pos += __popcll(m);
-        } else {
-          n += hit ? 1 : 0;
-        }
-      }
-    }
-  }
-  if (!FILL) {
-    n = group_sum_i<G>(n);
-    if (lane == 0) cnt[i] = n;
-  }
 }
 
 // ---- CSR full-list build over a binned copy ----------------------------------------
@@ -453,98 +384,13 @@ __device__ __forceinline__ double slab_gap(double v, int b, int c, double lo, do
   return fmax(g - 1e-6 * size, 0.0);
 }
 
-// FILL with stride > 0: single pass into fixed-stride rows (row i at nbr + i*stride), the
-// row's count into cnt[i]; a row longer than stride keeps its first stride entries and
-// raises *ovf (the host then rebuilds with the counted CSR passes).
-template <int G, int U, bool FILL, bool NT1, int R, bool TRIM>
-__global__ void __launch_bounds__(256)
-k_neigh2(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
-         const int *__restrict__ ty, const double4 *__restrict__ xb,
-         const int *__restrict__ tb, const int *__restrict__ beg,
-         const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
-         int *__restrict__ nbr, int stride = 0, int *__restrict__ ovf = nullptr) {
-  __shared__ double s_cns[NT2];
-  const int nt1 = cf->ntypes + 1;
-  if (!NT1) {
-    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
-    __syncthreads();
-  }
-  const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
-  const int lane = threadIdx.x & (G - 1);
-  if (i >= nlocal) return;
-  const double4 xi = xf[i];
-  const double *crow = s_cns + (NT1 ? 0 : ty[i] * nt1);
-  const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
-  const int cx = bin_coord(xi.x, q.lo[0], q.inv[0], q.nb[0]);
-  const int cy = bin_coord(xi.y, q.lo[1], q.inv[1], q.nb[1]);
-  const int cz = bin_coord(xi.z, q.lo[2], q.inv[2], q.nb[2]);
-  const int zr = (dim == 3) ? R : 0;
-  const double di = (double)i;
-  int n = 0;
-  int *const row = FILL ? nbr + (stride > 0 ? (size_t)i * stride : (size_t)off[i]) : nullptr;
-  const int cap = stride > 0 ? stride : 0x7fffffff;
-  int pos = 0;
-  const int gbase = (threadIdx.x & 63) & ~(G - 1);
-  const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
-  for (int bz = max(cz - zr, 0); bz <= min(cz + zr, q.nb[2] - 1); bz++) {
-    const double gz = (TRIM && dim == 3) ? slab_gap(xi.z, bz, cz, q.lo[2], q.size[2]) : 0.0;
-    for (int by = max(cy - R, 0); by <= min(cy + R, q.nb[1] - 1); by++) {
-      int bx0 = max(cx - R, 0), bx1 = min(cx + R, q.nb[0] - 1);
-      if (TRIM) {
-        const double gy = slab_gap(xi.y, by, cy, q.lo[1], q.size[1]);
-        const double d2 = gy * gy + gz * gz;
-        if (d2 > q.cutmaxsq) continue;
-        const double ext = sqrt(q.cutmaxsq - d2) * (1.0 + 1e-9) + 1e-9 * q.size[0];
-        bx0 = bin_coord(xi.x - ext, q.lo[0], q.inv[0], q.nb[0]);
-        bx1 = bin_coord(xi.x + ext, q.lo[0], q.inv[0], q.nb[0]);
-      }
-      const int brow = (bz * q.nb[1] + by) * q.nb[0];
-      const int s = beg[brow + bx0], e = beg[brow + bx1 + 1];
-      for (int base = s; base < e; base += G * U) {  // group-uniform trip count
-        const int b0 = base + lane;
-        double4 xj[U];
-        int tj[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int p = min(b0 + u * G, e - 1);
-          xj[u] = xb[p];
-          tj[u] = NT1 ? 1 : tb[p];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
-          const double rsq = dx * dx + dy * dy + dz * dz;
-          const bool hit = (b0 + u * G < e) && (xj[u].w != di) &&
-                           rsq <= (NT1 ? cns1 : crow[tj[u]]);
-          if (FILL) {
-            const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
-            const int q = pos + __popcll(m & ((1ull << lane) - 1ull));
-            if (hit && q < cap) row[q] = (int)xj[u].w;
-            pos += __popcll(m);
-          } else {
-            n += hit ? 1 : 0;
-          }
-        }
-      }
-    }
-  }
-  if (!FILL) {
-    n = group_sum_i<G>(n);
-    if (lane == 0) cnt[i] = n;
-  } else if (stride > 0 && lane == 0) {
-    cnt[i] = pos;
-    if (pos > stride) atomicOr(ovf, 1);
-  }
-}
-
 // ---- full-list build v3: flattened candidate ranges ---------------------------------------
-// Same half-size bins (reach 2), per-row trimming, membership and entry ORDER as k_neigh2,
-// but restructured for latency: k_neigh2 walks its <= 25 (dz, dy) bin-rows one after the
-// other, each paying a dependent bin-start load and then its candidate loads.  Here the
-// row's G lanes first resolve all bin-row ranges at once (independent loads, into LDS),
-// then walk the concatenated candidates as ONE flat range in chunks of G*U -- each chunk
-// one round of independent record loads.  Hits are compacted in candidate order, so the
-// list is identical to k_neigh2's.  Modes as k_neigh2 (count | CSR fill | strided fill);
+// Half-size bins (reach 2) with per-row trimming: a row's <= 25 (dz, dy) bin-rows are cut
+// to the x-range that can hold a point within cutneighmax.  The row's G lanes first resolve
+// all bin-row ranges at once (independent loads, into LDS), then walk the concatenated
+// candidates as ONE flat range in chunks of G*U -- each chunk one round of independent
+// record loads.  Hits are compacted in candidate order.  Modes: count | CSR fill | strided
+// fill (fixed-stride rows, the row's count in cnt, a row longer than stride raises *ovf);
 // perm_g > 0 stores a strided row chunk-transposed (tpos, stride a multiple of 4*perm_g).
 template <int G, int U, bool FILL, bool NT1>
 __global__ void __launch_bounds__(256)
@@ -569,7 +415,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   const int cy = bin_coord(xi.y, q.lo[1], q.inv[1], q.nb[1]);
   const int cz = bin_coord(xi.z, q.lo[2], q.inv[2], q.nb[2]);
   const int nbr_rows = (dim == 3) ? NB : (2 * R + 1);
-  // 1) this lane's bin-rows br = lane + k*G, in k_neigh2's (bz, by) loop order
+  // 1) this lane's bin-rows br = lane + k*G, in (bz, by) loop order
 #pragma unroll
   for (int k = 0; k < KB; k++) {
     const int br = lane + k * G;
@@ -655,14 +501,6 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
     cnt[i] = pos;
     if (pos > stride) atomicOr(ovf, 1);
   }
-}
-
-// positions as binned (xb[p].w = atom index) back in atom order
-static __global__ void k_unbin(int n, const double4 *__restrict__ xb, double4 *__restrict__ xo) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const double4 v = xb[p];
-  xo[(int)v.w] = v;
 }
 
 static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__restrict__ off) {

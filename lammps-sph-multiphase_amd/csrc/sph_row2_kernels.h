@@ -1,7 +1,8 @@
 // sph_row2_kernels.h -- second generation of the engine's CSR-row pair passes.
 //
-// Same pair arithmetic and list walk as sph_row_kernels.h (full list, gather only, G
-// lanes per row, U pairs in flight per lane, branch-free pair body).  What bounds these
+// The row path (engine kernel_path 1): full list, gather only, G lanes per row, U pairs in
+// flight per lane, branch-free pair body (a pair outside the cutoff, or a padding slot,
+// gets a zero kernel weight, which zeroes every term it feeds).  What bounds these
 // passes on gfx950 is the texture addresser (TA): rocprofv3 on C2 1M shows TA_TA_BUSY at
 // ~93% of the kernel's cycles, and a body-free variant (EXP=1) runs as long as the full
 // kernel.  tools/ta_bench.hip prices the TA: ~2.25 cycles per DISTINCT 128-B line a
@@ -35,9 +36,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "sph_row_kernels.h"
+#include "sph_kernels.h"
 
 namespace sph {
+
+// the engine's per-pass arguments (owned rows, layout of sph_kernels.h)
+struct RowArgs {
+  int n;
+  const int *off, *nbr;
+  double4 *xf, *vr;
+  const int *ty;
+  const double *en;
+  const Coefs *cf;
+  double4 *fo;
+  double *de;
+  double gx, gy, gz;
+};
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 

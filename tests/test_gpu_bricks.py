@@ -42,7 +42,7 @@ def at_rest(s):
     return s
 
 
-def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=1):
+def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0):
     nt = s.ntypes
     P = int(np.prod(pg))
     kw = {}
@@ -82,6 +82,8 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=1):
     assert not any(t.is_alive() for t in th), "brick threads hung"
     try:
         assert not errors, errors
+        for e in engines:  # the requested pair path really ran (no silent fallback)
+            assert e.stats()["staged"] == (1 if path == 0 else 0)
         return collect(engines, s)
     finally:
         for e in engines:
@@ -118,9 +120,11 @@ def compare(out, ref, tol=TOL):
     assert rel_err(out["v"], s.v) < tol
 
 
-@pytest.mark.parametrize("pg,path", [((2, 1, 1), 1), ((1, 2, 2), 1), ((2, 2, 2), 1),
-                                     ((2, 1, 1), 2), ((2, 2, 2), 2), ((2, 1, 1), 3),
-                                     ((2, 2, 2), 3), ((1, 2, 2), 4)])
+PATHS = [0, 1]   # 0 = block-staged LDS unions (production), 1 = row path (global gathers)
+
+
+@pytest.mark.parametrize("pg,path", [((2, 1, 1), 0), ((1, 2, 2), 0), ((2, 2, 2), 0),
+                                     ((2, 1, 1), 1), ((1, 2, 2), 1), ((2, 2, 2), 1)])
 def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     s = at_rest(c2_system(12))
     ph = po.c2_physics()
@@ -134,7 +138,7 @@ def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     compare(out, ref)
 
 
-@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("path", PATHS)
 def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     s = at_rest(c3_system(12))
     ph = po.c3_physics()
@@ -148,7 +152,7 @@ def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     assert rel_err(out["e"], ref.s.e) < TOL
 
 
-@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("path", PATHS)
 def test_bricks_migration(gpu, sph_amd, path):
     """Pressure-driven motion from rest with a larger step: atoms of the lattice plane that
     sits on the brick face (x = 6) cross it between rebuilds and migrate."""
@@ -168,7 +172,7 @@ def test_bricks_migration(gpu, sph_amd, path):
     compare(out, ref)
 
 
-@pytest.mark.parametrize("path", [1, 2, 3])
+@pytest.mark.parametrize("path", PATHS)
 def test_bricks_2d(gpu, sph_amd, path):
     s = at_rest(c2_system(30, dim=2))
     ph = po.c2_physics(2.5)
@@ -201,8 +205,8 @@ def test_rccl_communicator_single_rank(gpu, sph_amd):
     eng.close()
 
 
-@pytest.mark.parametrize("moving", [False, True])
-def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving):
+@pytest.mark.parametrize("moving,path", [(False, 0), (True, 0), (True, 1)])
+def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving, path):
     """The RCCL data path on one GPU: a one-rank communicator in loopback mode sends every
     periodic self swap (border records at rebuilds, the per-step forward x/vest/rho/e and
     rho/EOS halos, the setup reverse comm) through ncclSend/ncclRecv to itself, packed and
@@ -221,7 +225,7 @@ def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving):
                               neigh_every=ph.every,
                               rhosum=dict(nstep=1, cut=ph.rhosum_cut),
                               tait=dict(rho0=ph.rho0, c0=ph.c0, visc=ph.visc, cut=ph.tait_cut),
-                              kernel_path=1)
+                              kernel_path=path)
     eng = sph_amd.Engine(cfg)
     try:
         eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)
@@ -249,7 +253,7 @@ def test_bricks_halo_overlap(gpu, sph_amd, monkeypatch, pg):
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(9)
-    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9)
+    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=1)   # (overlap: row path)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
 

@@ -33,7 +33,9 @@ def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None, kernel_path=0):
     return eng
 
 
-def compare(eng, ref, tol=TOL):
+def compare(eng, ref, tol=TOL, path=None):
+    if path is not None:  # the requested pair path really ran (no silent fallback)
+        assert eng.stats()["staged"] == (1 if path == 0 else 0)
     got = eng.get_atoms()
     s = ref.s
     assert rel_err(got["rho"], s.rho) < tol
@@ -47,18 +49,25 @@ def compare(eng, ref, tol=TOL):
     return got
 
 
-@pytest.mark.parametrize("sort,path", [(1, 0), (0, 1), (1, 1), (1, 2), (0, 2), (1, 3), (0, 4), (1, 5), (0, 5)])
-def test_setup_c2(gpu, sph_amd, sort, path):
-    """path 0 = LDS-staged bins (16-bit slot lists), 1 = CSR rows with global gathers,
-    2 = LDS tiles (bin neighborhoods staged once, CSR list translated to slots),
-    3/4 = cluster pairs, full lists / half lists with Newton-3 atomics."""
+PATHS = [0, 1]   # 0 = block-staged LDS unions (production), 1 = row path (global gathers)
+
+
+@pytest.mark.parametrize("sort,path,umf", [(1, 0, 0), (1, 0, 64), (0, 0, 0), (1, 1, 0),
+                                           (0, 1, 0)])
+def test_setup_c2(gpu, sph_amd, monkeypatch, sort, path, umf):
+    """path 0 = block-staged passes (LDS unions, 16-bit slot rows built from the bins), 1 =
+    the row path.  umf = 64 caps the force pass's LDS image at 64 records, so nearly every
+    block runs in the large-union launch; unsorted rows (sort 0) make wide blocks whose
+    unions only fit the LDS image as 32-row blocks (the build's second shape)."""
+    if umf:
+        monkeypatch.setenv("SPH_BLKUMF", str(umf))
     s = c2_system(12)
     ph = po.c2_physics()
     ref = po.RefRun(s, ph)
     ref.setup()
     eng = engine_for(sph_amd, s, ph, sort=sort, kernel_path=path)
     eng.setup()
-    assert eng.stats()["staged"] == {0: 1, 1: 0, 2: 2, 3: 3, 4: 3, 5: 5}[path]
+    assert eng.stats()["staged"] == (1 if path == 0 else 0)
     # neighbor membership: bit-exact counts per particle
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     st = eng.stats()
@@ -68,7 +77,7 @@ def test_setup_c2(gpu, sph_amd, sort, path):
     assert elem_rel_err(got["rho"], ref.s.rho) < 1e-13
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     s = c2_system(12)
     ph = po.c2_physics()
@@ -79,11 +88,11 @@ def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     eng.setup()
     eng.run(25)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
-    compare(eng, ref)
+    compare(eng, ref, path=path)
     assert eng.stats()["step"] == 25
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_run_c3_morris_heat(gpu, sph_amd, path):
     s = c3_system(10)
     ph = po.c3_physics()
@@ -95,10 +104,10 @@ def test_run_c3_morris_heat(gpu, sph_amd, path):
     eng.setup()
     eng.run(12)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
-    compare(eng, ref)
+    compare(eng, ref, path=path)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_run_2d(gpu, sph_amd, path):
     s = c2_system(30, dim=2)
     ph = po.c2_physics(2.5)
@@ -110,10 +119,10 @@ def test_run_2d(gpu, sph_amd, path):
     eng.setup()
     eng.run(9)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
-    compare(eng, ref)
+    compare(eng, ref, path=path)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_every_step_rebuild_and_nstep(gpu, sph_amd, path):
     s = c2_system(9)
     ph = po.c2_physics()
@@ -125,10 +134,10 @@ def test_every_step_rebuild_and_nstep(gpu, sph_amd, path):
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
     eng.setup()
     eng.run(7)
-    compare(eng, ref)
+    compare(eng, ref, path=path)
 
 
-@pytest.mark.parametrize("path", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_nonperiodic_box(gpu, sph_amd, path):
     """No ghosts across non-periodic boundaries (sendneed = 0, comm_brick.cpp:226-274)."""
     s = c2_system(9)
@@ -143,10 +152,10 @@ def test_nonperiodic_box(gpu, sph_amd, path):
     eng.setup()
     eng.run(3)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
-    compare(eng, ref)
+    compare(eng, ref, path=path)
 
 
-@pytest.mark.parametrize("path", [1, 2, 3, 5])
+@pytest.mark.parametrize("path", PATHS)
 def test_full_size_properties(gpu, sph_amd, path):
     """BASELINE C2 size (1M particles): size-independent checks -- total neighbor count
     equals the oracle's full_bin count, momentum is conserved by the pair forces

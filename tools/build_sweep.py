@@ -15,7 +15,7 @@ def main():
     sph = bench.load_pkg()
     x, v, t, rho, e, cv = bench.make_system(n, 12345)
     cfg = bench.c2_config(sph, n)
-    cfg.kernel_path = int(os.environ.get("SPH_PATH", "5"))
+    cfg.kernel_path = int(os.environ.get("SPH_PATH", "0"))
     bexp = os.environ.pop("SPH_BEXP", None)
     eng = sph.Engine(cfg)
     eng.set_atoms(x, v, t, rho, e, cv)

@@ -13,7 +13,7 @@ if [ "$3" = "test" ]; then
 fi
 export TMPDIR=/tmp
 for b in $SHAPES; do
-  (cd /tmp && SPH_PATH=5 SPH_BLK=$b timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+  (cd /tmp && SPH_BLK=$b timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
      -d "$R/gpurun_out/prof_${TAG}_$b" -o run -- python3 "$R/tools/kernel_sweep.py" 100 20) > "$R/gpurun_out/sweep_${TAG}_$b.log" 2>&1 || exit 1
   echo "shape $b: $(tail -1 $R/gpurun_out/sweep_${TAG}_$b.log)"
   f=$(find "$R/gpurun_out/prof_${TAG}_$b" -name '*kernel_stats.csv' | head -1)

@@ -87,22 +87,25 @@ __host__ __device__ __forceinline__ int blk_tpos(int q) {
 // Candidate ORDER differs from full_bin's (bins are scanned per block), which changes only
 // the summation order of the pair passes.  Overflows (> BLK_MCAP candidates, or a block
 // whose bin box exceeds the bin-row table) raise *ovf; the host then takes the row path.
-constexpr int BLK_MCAP = 4096;  // candidates per block (hit bitmaps; 12-bit slots)
+constexpr int BLK_MCAP = 4096;  // candidates per block (hit bitmaps)
+constexpr int BLK_MBIG = 8192;  // ... in the large-image variant (wide blocks, small boxes)
+constexpr int BLK_UCAP = BLK_MBIG;  // union stride of ulist
 constexpr int BLK_WIN = 512;    // candidates staged in LDS at a time
 constexpr int BLK_TBL = 256;    // bin-rows per block
 
-template <int R, int G, int U, bool NT1>
+template <int R, int G, int U, bool NT1, int MC>
 __global__ void __launch_bounds__(R * BLK_TPR)
 k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *__restrict__ ty,
             const double4 *__restrict__ xb, const int *__restrict__ tb,
-            const int *__restrict__ qbeg, const Coefs *__restrict__ cf, int ucap, int sstride,
+            const int *__restrict__ qbeg, const int *__restrict__ xpos,
+            const Coefs *__restrict__ cf, int ucap, int sstride,
             int *__restrict__ ulist, int *__restrict__ ucnt, int *__restrict__ rcnt,
             unsigned short *__restrict__ snbr, int *__restrict__ ovf, int *__restrict__ umax,
             int bexp) {
   // bexp (study, SPH_BEXP; outputs meaningless): 1 = no candidate loads, 2 = no row
   // tests, 4 = no slot-row stores, 8 = no union stores
   constexpr int TPR = BLK_TPR, BLK_BT = R * TPR;
-  constexpr int W = BLK_MCAP / 32;
+  constexpr int W = MC / 32;
   constexpr int RB = 2, NB = (2 * RB + 1) * (2 * RB + 1);
   static_assert(BLK_BT <= 1024 && BLK_BT >= BLK_TBL && (TPR & (TPR - 1)) == 0, "block shape");
   __shared__ double2 s_cxy[BLK_WIN];
@@ -190,7 +193,7 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
   }
   int M = 0;
   const int pre = blk_scan<BLK_BT>(len, s_w, &M);
-  if (M > BLK_MCAP) {
+  if (M > MC) {
     if (tid == 0) atomicMax(ovf, M);
     return;
   }
@@ -643,22 +646,36 @@ struct BlkArgs {
 
 inline int blk_blocks(int n, int R) { return (n + R - 1) / R; }
 
-inline void blk_neigh(int shape, bool nt1, hipStream_t s, int n, const QBins &q, int dim,
-                      const double4 *xf, const int *ty, const double4 *xb, const int *tb,
-                      const int *qbeg, const Coefs *cf, int ucap, int sstride, int *ulist,
-                      int *ucnt, int *rcnt, unsigned short *snbr, int *ovf, int *umax,
-                      int bexp = 0) {
+template <int R, int G, int U, int MC>
+inline void blk_neigh_t(bool nt1, hipStream_t s, int n, const QBins &q, int dim,
+                        const double4 *xf, const int *ty, const double4 *xb, const int *tb,
+                        const int *qbeg, const int *xpos, const Coefs *cf, int ucap,
+                        int sstride, int *ulist, int *ucnt, int *rcnt, unsigned short *snbr,
+                        int *ovf, int *umax, int bexp) {
+  if (nt1)
+    hipLaunchKernelGGL((k_blk_neigh<R, G, U, true, MC>), dim3(blk_blocks(n, R)),
+                       dim3(R * BLK_TPR), 0, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf, ucap,
+                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp);
+  else
+    hipLaunchKernelGGL((k_blk_neigh<R, G, U, false, MC>), dim3(blk_blocks(n, R)),
+                       dim3(R * BLK_TPR), 0, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf, ucap,
+                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp);
+}
+// big: the large candidate image (BLK_MBIG; 32-row shapes only)
+inline void blk_neigh(int shape, bool big, bool nt1, hipStream_t s, int n, const QBins &q,
+                      int dim, const double4 *xf, const int *ty, const double4 *xb,
+                      const int *tb, const int *qbeg, const int *xpos, const Coefs *cf,
+                      int ucap, int sstride, int *ulist, int *ucnt, int *rcnt,
+                      unsigned short *snbr, int *ovf, int *umax, int bexp = 0) {
   switch (shape) {
-#define SPH_CASE(k, R, G, U)                                                                  \
-  case k:                                                                                   \
-    if (nt1)                                                                                \
-      hipLaunchKernelGGL((k_blk_neigh<R, G, U, true>), dim3(blk_blocks(n, R)), dim3(R * BLK_TPR), 0, \
-                         s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt,  \
-                         rcnt, snbr, ovf, umax, bexp);                                        \
-    else                                                                                    \
-      hipLaunchKernelGGL((k_blk_neigh<R, G, U, false>), dim3(blk_blocks(n, R)), dim3(R * BLK_TPR), 0,\
-                         s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt,  \
-                         rcnt, snbr, ovf, umax, bexp);                                        \
+#define SPH_CASE(k, R, G, U)                                                                \
+  case k:                                                                                 \
+    if (big && R == 32)                                                                   \
+      blk_neigh_t<R, G, U, BLK_MBIG>(nt1, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf,   \
+                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp); \
+    else                                                                                  \
+      blk_neigh_t<R, G, U, BLK_MCAP>(nt1, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf,   \
+                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp); \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE

@@ -169,7 +169,7 @@ struct sph_engine {
   int nbins = 0;
   QBins qb{};
   int nqbins = 0;
-  DBuf<int> qbeg, tb;
+  DBuf<int> qbeg, tb, xpos;
   DBuf<double4> xb;
   DBuf<unsigned> bkey, bkey2;
   DBuf<int> bidx, bidx2;
@@ -276,6 +276,25 @@ struct sph_engine {
         kbn.nb[k] = bn.nb[k] * div;
         kbn.inv[k] = bn.inv[k] * div;
       }
+    if (want_blk()) {
+      // block path: cells of ~1/div of a bin over the OWNED sub-box only, so the Hilbert
+      // curve (over the next power of two of cells) leaves the rows' region as rarely as
+      // possible -- a block of consecutive rows stays one compact piece of space
+      for (int k = 0; k < 3; k++) {
+        const double ext = subhi[k] - sublo[k];
+        if (k >= cfg.dim || ext <= 0.0) {
+          kbn.lo[k] = sublo[k];
+          kbn.nb[k] = 1;
+          kbn.inv[k] = 0.0;
+          continue;
+        }
+        int nc = std::max(1, (int)std::ceil(ext / (cutneighmax / div)));
+        nc = std::min(nc, 1024);
+        kbn.lo[k] = sublo[k];
+        kbn.nb[k] = nc;
+        kbn.inv[k] = nc / ext;
+      }
+    }
     const bool mort = kbn.nb[0] <= 1024 && kbn.nb[1] <= 1024 && kbn.nb[2] <= 1024;
     if (!mort) kbn = bn;
     // the block path orders rows along a Hilbert curve (its blocks of consecutive rows stay
@@ -674,8 +693,9 @@ struct sph_engine {
     SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tbytes, bkey.p, bkey2.p, bidx.p, bidx2.p, nall, 0, endbit, s));
     hipLaunchKernelGGL(k_lower_bound, dim3(blocks(nqbins + 1)), dim3(BLK), 0, s, nqbins, nall,
                        0, bkey2.p, qbeg.p);
+    xpos.reserve(nall);
     hipLaunchKernelGGL(k_bin_copy, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bidx2.p, xf.p,
-                       ty.p, xb.p, tb.p);
+                       ty.p, xb.p, tb.p, xpos.p);
   }
   // Global-index full list (k_neigh3, Neighbor::full_bin membership) of the owned rows at
   // positions xi (default: the current ones, as binned by bin_q): CSR (count pass, scan,
@@ -759,19 +779,20 @@ struct sph_engine {
     mx.reserve(8);
     ccnt.reserve(n + 1);
     if (blk_rowcap == 0) blk_rowcap = std::max(list_stride, nbr_maxrow + nbr_maxrow / 4 + 16);
-    // the SPH_BLK shape, then 32-row blocks (smaller unions) if its blocks do not fit
+    // the SPH_BLK shape, then 32-row blocks (smaller unions), then 32-row blocks with the
+    // build's large candidate image, if the blocks do not fit
     const int first = blk_shape_env();
-    for (int shape : {first, 1}) {
-      if (shape == 1 && first == 1) break;
-      const int r = build_blk_shape(shape);
+    const int chain[3][2] = {{first, 0}, {1, 0}, {1, 1}};
+    for (const auto &c : chain) {
+      if (c[0] == 1 && first == 1 && c[1] == 0 && &c != &chain[0]) continue;
+      const int r = build_blk_shape(c[0], c[1] != 0);
       if (r == 1) return true;
-      if (r == 2) continue;   // a union too large for the LDS image: smaller blocks
-      return false;
+      if (r != 2) return false;  // (2: a block overflowed: the next, roomier variant)
     }
     return false;
   }
   // 1 = built, 2 = a block overflowed (candidates, bin table or LDS image), 0 = failed
-  int build_blk_shape(int shape) {
+  int build_blk_shape(int shape, bool big) {
     const int n = nlocal;
     const BlkShape sh = blk_shape(shape);
     const int chunk = sh.G * sh.U;
@@ -779,20 +800,20 @@ struct sph_engine {
       blk_sstride = (std::max(blk_rowcap, 1) + chunk - 1) / chunk * chunk;
       snbr.reserve((size_t)n * blk_sstride + 2 * chunk);  // + the pair passes' prefetch pad
       const int nb = blk_blocks(n, sh.R);
-      ulist.reserve((size_t)nb * BLK_MCAP);
+      ulist.reserve((size_t)nb * BLK_UCAP);
       ucnt.reserve(nb);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
-      blk_neigh(shape, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, dc, BLK_MCAP,
-                blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
+      blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
+                dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
                 env_int("SPH_BEXP", 0));
       int hm[5];
       SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
       if (env_int("SPH_DEBUG", 0))
         fprintf(stderr,
-                "[sph] k_blk_neigh shape %d n %d rowcap %d: ovf %d union max %d mean %.1f, "
+                "[sph] k_blk_neigh shape %d%s n %d rowcap %d: ovf %d union max %d mean %.1f, "
                 "candidates max %d mean %.1f\n",
-                shape, n, blk_rowcap, hm[0], hm[1], (double)hm[4] / nb, hm[2],
+                shape, big ? " (large image)" : "", n, blk_rowcap, hm[0], hm[1], (double)hm[4] / nb, hm[2],
                 (double)hm[3] / nb);
       if (hm[0] == (1 << 21)) {  // a row outgrew the slot-row stride
         blk_rowcap *= 2;
@@ -829,7 +850,7 @@ struct sph_engine {
     k.n = nlocal;
     k.shape = blk_sh;
     k.exp = row2_exp();
-    k.ucap = BLK_MCAP;
+    k.ucap = BLK_UCAP;
     k.um = blk_um;
     k.umf = blk_umf;
     k.nbig = blk_nbig;
@@ -1312,7 +1333,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->en, &e->en2, &e->de}) b->release();
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
-                  &e->ccnt, &e->qbeg, &e->tb, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
+                  &e->ccnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
                   &e->tcnt, &e->ulist, &e->ucnt, &e->bl})
     b->release();
   for (auto *b : {&e->bkey, &e->bkey2}) b->release();

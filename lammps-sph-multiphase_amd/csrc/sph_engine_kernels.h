@@ -365,15 +365,18 @@ struct QBins {
   double cutmaxsq;
 };
 
+// (xpos, if given: the inverse, atom -> position in xb)
 static __global__ void k_bin_copy(int n, const int *__restrict__ perm,
                                   const double4 *__restrict__ xf, const int *__restrict__ ty,
-                                  double4 *__restrict__ xb, int *__restrict__ tb) {
+                                  double4 *__restrict__ xb, int *__restrict__ tb,
+                                  int *__restrict__ xpos = nullptr) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const int j = perm[p];
   const double4 x = xf[j];
   xb[p] = make_double4(x.x, x.y, x.z, (double)j);
   tb[p] = ty[j];
+  if (xpos) xpos[j] = p;
 }
 
 // distance from coordinate v to bin b's slab along one axis (0 inside), shrunk by a margin

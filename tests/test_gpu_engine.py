@@ -57,8 +57,8 @@ PATHS = [0, 1]   # 0 = block-staged LDS unions (production), 1 = row path (globa
 def test_setup_c2(gpu, sph_amd, monkeypatch, sort, path, umf):
     """path 0 = block-staged passes (LDS unions, 16-bit slot rows built from the bins), 1 =
     the row path.  umf = 64 caps the force pass's LDS image at 64 records, so nearly every
-    block runs in the large-union launch; unsorted rows (sort 0) make wide blocks whose
-    unions only fit the LDS image as 32-row blocks (the build's second shape)."""
+    block runs in the large-union launch; unsorted rows (sort 0) make blocks too wide for
+    the build's candidate image, so the build takes its large-image variant."""
     if umf:
         monkeypatch.setenv("SPH_BLKUMF", str(umf))
     s = c2_system(12)

@@ -71,6 +71,51 @@ __host__ __device__ __forceinline__ int blk_tpos(int q) {
   return q - c + U * (c % G) + c / G;
 }
 
+// ---- the union image ---------------------------------------------------------------------
+// A block's union sits in LDS as an image of 16-slot chunks.  Slot s = union position + 1;
+// slot 0 is a sentinel far from every atom (x = 1e100: every pair test fails, every pair
+// term is a finite value times a zero kernel weight), so padded list positions need no
+// bounds test.  A chunk holds its 16 slots' arrays back to back -- a0 (x, y) at +0,
+// a1 (z, P/rho^2) at +256, a2 (vx, vy) at +512, a3 (vz, rho) at +768, e at +1024 (heat,
+// 16-byte stride like the others) -- CH = 1024 (1280 with e) bytes, and a slot-row word
+// holds q = (s/16)*(CH/16) + s%16, the
+// slot's byte offset / 16: every array of the slot is one immediate offset from q*16, and
+// 16 consecutive slots of one array cover the 64 banks once (ds_read_b128: 16 lanes per
+// LDS cycle).  The rho pass keeps a compact image of its own (x, y at 16 s; z at 16 S + 8 s
+// for S slots) and decodes s from q.
+constexpr int BLK_CH = 1024, BLK_CHE = 1280;
+__host__ __device__ inline int blk_q(int s, int cq) { return (s >> 4) * cq + (s & 15); }
+template <int CQ>
+__device__ __forceinline__ int blk_s(int q) { return (q / CQ) * 16 + (q % CQ); }
+// the rho pass's image: S = u + 1 slots of (x, y), z [, type]
+__host__ __device__ inline size_t blk_rho_lds(int u, bool nt1) {
+  const size_t S = (size_t)u + 1;
+  return S * 24 + (nt1 ? 0 : (S + 15) / 16 * 16);
+}
+// LDS bytes of an image for u union atoms (+ the sentinel), with the per-slot type bytes
+// (indexed by q) after it when there are several types
+__host__ __device__ inline size_t blk_lds(int u, int cq, bool nt1) {
+  const size_t nch = ((size_t)u + 16) / 16;
+  return nch * cq * 16 + (nt1 ? 0 : (nch * cq + 15) / 16 * 16);
+}
+// stage atom j's record into slot s of the image (cq*16-byte chunks)
+template <bool HEAT>
+__device__ __forceinline__ void blk_put(unsigned char *img, int s, int cq, const double4 &x,
+                                        const double4 &v, double e) {
+  unsigned char *const r = img + (size_t)(s >> 4) * cq * 16 + (s & 15) * 16;
+  *reinterpret_cast<double2 *>(r) = make_double2(x.x, x.y);
+  *reinterpret_cast<double2 *>(r + 256) = make_double2(x.z, x.w);
+  *reinterpret_cast<double2 *>(r + 512) = make_double2(v.x, v.y);
+  *reinterpret_cast<double2 *>(r + 768) = make_double2(v.z, v.w);
+  if (HEAT) *reinterpret_cast<double *>(r + 1024) = e;
+}
+// the sentinel (slot 0): far away, at rest, P/rho^2 = 0, rho = 1, e = 0
+template <bool HEAT>
+__device__ __forceinline__ void blk_put_sentinel(unsigned char *img) {
+  blk_put<HEAT>(img, 0, 0, make_double4(1e100, 1e100, 1e100, 0.0),
+                make_double4(0.0, 0.0, 0.0, 1.0), 0.0);
+}
+
 // ---- block neighbour build from the bins ------------------------------------------------
 // One 256-thread workgroup per block of R rows builds the block's rows DIRECTLY in slot
 // form, without a global-index list: Neighbor::full_bin membership (neigh_full.cpp:241-344:
@@ -101,7 +146,7 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
             const Coefs *__restrict__ cf, int ucap, int sstride,
             int *__restrict__ ulist, int *__restrict__ ucnt, int *__restrict__ rcnt,
             unsigned short *__restrict__ snbr, int *__restrict__ ovf, int *__restrict__ umax,
-            int bexp) {
+            int cq, int bexp) {
   // bexp (study, SPH_BEXP; outputs meaningless): 1 = no candidate loads, 2 = no row
   // tests, 4 = no slot-row stores, 8 = no union stores
   constexpr int TPR = BLK_TPR, BLK_BT = R * TPR;
@@ -331,7 +376,8 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
       const int bit = __ffs(m) - 1;
       m &= m - 1;
       if (qq < sstride && !(bexp & 4))
-        out[blk_tpos<G, U>(qq)] = (unsigned short)(base + __popc(used & ((1u << bit) - 1u)));
+        out[blk_tpos<G, U>(qq)] =
+            (unsigned short)blk_q(base + 1 + __popc(used & ((1u << bit) - 1u)), cq);
       qq++;
     }
   }
@@ -340,20 +386,7 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
     if (cntr > sstride) atomicMax(ovf, 1 << 21);
   }
   const int cend = min((cntr + U * G - 1) / (U * G) * (U * G), sstride);
-  for (int k = cntr + sub; k < cend; k += TPR) out[blk_tpos<G, U>(k)] = 0;
-}
-
-// LDS images of a block's union (dynamic shared memory, um = largest union of the build)
-struct BlkRhoLds {
-  double2 *xy;
-  double *z;
-  unsigned char *t;
-};
-__host__ __device__ inline size_t blk_rho_lds(int um, bool nt1) {
-  return (size_t)um * (16 + 8) + (nt1 ? 0 : ((size_t)um + 15) / 16 * 16);
-}
-__host__ __device__ inline size_t blk_force_lds(int um, bool heat, bool nt1) {
-  return (size_t)um * 64 + (heat ? (size_t)um * 8 : 0) + (nt1 ? 0 : ((size_t)um + 15) / 16 * 16);
+  for (int k = cntr + sub; k < cend; k += TPR) out[blk_tpos<G, U>(k)] = 0;  // the sentinel
 }
 
 // A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.
@@ -372,41 +405,58 @@ struct SlotWord<4> {
   }
 };
 
-// Walk a row's c slots (chunk-transposed, blk_tpos) with the row's G lanes, U slots per
-// lane per chunk: body(slot, in) for every slot position of the lane (in = position < c;
-// padded positions hold slot 0).  NCH > 0: all of the row's chunks (at most NCH, the
-// host guarantees c <= NCH*U*G) are loaded into registers before the first pair, so the
-// index stream's latency is paid once per row; NCH = 0: the next chunk is prefetched
-// while the current one is evaluated (the slot array is padded by two chunks).
-template <int G, int U, int NCH, class Body>
-__device__ __forceinline__ void blk_walk(const unsigned short *sl, int c, int lane,
-                                         Body body) {
+// A row's c slots (chunk-transposed, blk_tpos) for the row's G lanes, U slots per lane per
+// chunk.  load() issues the lane's slot-word loads -- before the block's staging, so their
+// latency overlaps it; walk() calls body(slot, in) for every slot position of the lane
+// (in = position < c; padded positions hold the sentinel slot).  NCH > 0: all of the
+// row's chunks (at most NCH, the host guarantees c <= NCH*U*G) are held in registers;
+// NCH = 0 (long rows): the next chunk is prefetched while the current one is evaluated
+// (the slot array is padded by two chunks).
+template <int G, int U, int NCH>
+struct BlkSlots {
   typedef typename SlotWord<U>::T SW;
-  if (NCH > 0) {
-    SW w[NCH > 0 ? NCH : 1];
+  SW w[NCH > 0 ? NCH : 1];
+  const unsigned short *sl;
+  __device__ __forceinline__ void load(const unsigned short *row, int c, int lane) {
+    sl = row;
+    if (NCH > 0) {
 #pragma unroll
-    for (int k = 0; k < NCH; k++)
-      w[k] = k * U * G < c ? *reinterpret_cast<const SW *>(sl + k * U * G + U * lane) : SW{};
-#pragma unroll
-    for (int k = 0; k < NCH; k++) {
-      if (k * U * G >= c) break;
-#pragma unroll
-      for (int q = 0; q < U; q++) body(SlotWord<U>::get(w[k], q), k * U * G + q * G + lane < c);
-    }
-  } else {
-    SW wn = *reinterpret_cast<const SW *>(sl + U * lane);
-    for (int k0 = 0; k0 < c; k0 += U * G) {
-      const SW w = wn;
-      wn = *reinterpret_cast<const SW *>(sl + k0 + U * G + U * lane);
-#pragma unroll
-      for (int q = 0; q < U; q++) body(SlotWord<U>::get(w, q), k0 + q * G + lane < c);
+      for (int k = 0; k < NCH; k++)
+        w[k] = k * U * G < c ? *reinterpret_cast<const SW *>(sl + k * U * G + U * lane) : SW{};
+    } else {
+      w[0] = *reinterpret_cast<const SW *>(sl + U * lane);
     }
   }
-}
+  template <class Body>
+  __device__ __forceinline__ void walk(int c, int lane, Body body) {
+    if (NCH > 0) {
+#pragma unroll
+      for (int k = 0; k < NCH; k++) {
+        if (k * U * G >= c) break;
+#pragma unroll
+        for (int q = 0; q < U; q++)
+          body(SlotWord<U>::get(w[k], q), k * U * G + q * G + lane < c);
+      }
+    } else {
+      SW wn = w[0];
+      for (int k0 = 0; k0 < c; k0 += U * G) {
+        const SW cur = wn;
+        wn = *reinterpret_cast<const SW *>(sl + k0 + U * G + U * lane);
+#pragma unroll
+        for (int q = 0; q < U; q++) body(SlotWord<U>::get(cur, q), k0 + q * G + lane < c);
+      }
+    }
+  }
+};
+// union positions staged from registers loaded ahead of the slot rows (the rest, for
+// unions over BLK_SP*threads atoms, in a plain loop)
+constexpr int BLK_SP = 2;
 
 // sph/rhosum over the block union (+ the Tait EOS epilogue: P/rho^2 into xf[i].w, rho into
-// vr[i].w), pair_sph_rhosum.cpp:116-195
-template <int R, int G, int U, int NCH, bool NT1>
+// vr[i].w), pair_sph_rhosum.cpp:116-195.  The cut test rides on the kernel weight:
+// max(1 - rsq/h^2, 0) is zero exactly where rsq >= cutsq = h^2 fails, up to the last bit of
+// rsq/h^2 at rsq = h^2 (a weight ~1e-64 then); one type: sum_j w_j, times m_j K at the end.
+template <int R, int G, int U, int NCH, bool NT1, int CQ>
 __global__ void __launch_bounds__(R * G)
 k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
              const unsigned short *__restrict__ snbr, int sstride,
@@ -416,53 +466,87 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   constexpr int NTH = R * G;
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
-  double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
-  double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)um * 16);
-  unsigned char *const s_t = blk_smem + (size_t)um * 24;
   const int nt1 = cf->ntypes + 1;
   const int b = (int)xcd_block(), tid = threadIdx.x;
-  if (!NT1)
-    for (int t = tid; t < nt1 * nt1; t += NTH) s_c[t] = cf->rho[t];
-  const int u = ucnt[b];
-  const int *const ul = ulist + (size_t)b * ucap;
-  for (int p = tid; p < u; p += NTH) {
-    const int j = ul[p];
-    const double4 x = xf[j];
-    s_xy[p] = make_double2(x.x, x.y);
-    s_z[p] = x.z;
-    if (!NT1) s_t[p] = (unsigned char)ty[j];
-  }
-  __syncthreads();
   const int row = b * R + tid / G, lane = tid & (G - 1);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
+  // loads first: the row's count, the union's atom ids, then the row's slots and the
+  // union's positions, so that one latency covers them all
+  const int u = ucnt[b];
+  const int c = live ? rcnt[rr] : 0;
+  const int *const ul = ulist + (size_t)b * ucap;
+  int jj[BLK_SP];
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++) jj[k] = tid + k * NTH < u ? ul[tid + k * NTH] : -1;
+  BlkSlots<G, U, NCH> sw;
+  sw.load(snbr + (size_t)rr * sstride, c, lane);
   const double4 xi = xf[rr];
   const int it = NT1 ? 1 : ty[rr];
+  double4 gx[BLK_SP];
+  int gt[BLK_SP];
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++)
+    if (jj[k] >= 0) {
+      gx[k] = xf[jj[k]];
+      if (!NT1) gt[k] = ty[jj[k]];
+    }
+  double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
+  double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)(um + 1) * 16);
+  unsigned char *const s_t = blk_smem + (size_t)(um + 1) * 24;
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += NTH) s_c[t] = cf->rho[t];
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++)
+    if (jj[k] >= 0) {
+      const int sl = tid + k * NTH + 1;
+      s_xy[sl] = make_double2(gx[k].x, gx[k].y);
+      s_z[sl] = gx[k].z;
+      if (!NT1) s_t[sl] = (unsigned char)gt[k];
+    }
+  for (int p = tid + BLK_SP * NTH; p < u; p += NTH) {
+    const int j = ul[p];
+    const double4 x = xf[j];
+    s_xy[p + 1] = make_double2(x.x, x.y);
+    s_z[p + 1] = x.z;
+    if (!NT1) s_t[p + 1] = (unsigned char)ty[j];
+  }
+  if (tid == 0) {
+    s_xy[0] = make_double2(1e100, 1e100);
+    s_z[0] = 1e100;
+    if (!NT1) s_t[0] = 1;
+  }
+  __syncthreads();
   const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
-  const int c = live ? rcnt[rr] : 0;
   double acc = 0.0;
-  blk_walk<G, U, NCH>(snbr + (size_t)rr * sstride, c, lane, [&](int sj, bool in) {
+  sw.walk(c, lane, [&](int q, bool) {
+    const int sj = blk_s<CQ>(q);
     const double2 xy = s_xy[sj];
     const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
     const double rsq = dx * dx + dy * dy + dz * dz;
     const RhoPair cc = NT1 ? c1 : s_c[it * nt1 + s_t[sj]];
-    double wf = 1.0 - rsq * cc.ihsq;
+    double wf = fmax(fma(-rsq, cc.ihsq, 1.0), 0.0);
     wf = wf * wf;
     wf = wf * wf;
-    acc += (in && rsq < cc.cutsq) ? cc.mK * wf : 0.0;
+    acc = NT1 ? acc + wf : fma(cc.mK, wf, acc);
   });
   acc = group_sum<G>(acc);
   if (lane == 0 && live) {
-    const double rho = cf->self_rho[it] + acc;
+    const double rho = cf->self_rho[it] + (NT1 ? c1.mK * acc : acc);
     vr[row].w = rho;
     xf[row].w = tait_p_over_rho2(rho, cf->rho0[it], cf->B[it]);
   }
 }
 
 // sph/taitwater[/morris] [+ sph/heatconduction] over the block union (full list, i side
-// only), row2 pair body (k_row2_force).  blist == nullptr: every block whose union fits the
-// um-record LDS image (larger ones return at once); else the blocks listed in blist (the
+// only), pair_sph_taitwater.cpp:139-191, pair_sph_taitwater_morris.cpp:139-191,
+// pair_sph_heatconduction.cpp:103-124.  blist == nullptr: every block whose union fits the
+// um-atom LDS image (larger ones return at once); else the blocks listed in blist (the
 // second launch, with an image as large as the largest union).
+// The styles' cut is their h (cutsq = h^2), so the cut test rides on the weight:
+// d = max(h - r, 0) is zero exactly where rsq < cutsq fails (up to the last bit of r at
+// r = h, a weight ~1e-32 then).  The pair's uniform factors (-m_i m_j wK, m_j wK, -1/2,
+// the heat prefactor) are applied once per row when there is one type, per pair otherwise.
 // EXP (study builds, SPH_EXP): 1 = neighbour records synthesised from the slot (no LDS
 // reads), 2 = LDS reads with a trivial body, 3 = no staging loads (LDS image left as is).
 // Outputs meaningless.
@@ -474,132 +558,158 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             const double4 *__restrict__ vr, const int *__restrict__ ty,
             const double *__restrict__ en, const Coefs *__restrict__ cf,
             double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-            double gz, int um, const int *__restrict__ blist) {
+            double gz, int um, const int *__restrict__ blist, int cq) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr int NTH = R * G;
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ TaitPair s_tp[(TAIT && !NT1) ? NT2 : 1];
   __shared__ HeatPair s_hp[(HEAT && !NT1) ? NT2 : 1];
-  double2 *const s_a0 = reinterpret_cast<double2 *>(blk_smem);              // x, y
-  double2 *const s_a1 = s_a0 + um;                                          // z, P/rho^2
-  double2 *const s_a2 = s_a0 + 2 * (size_t)um;                              // vx, vy
-  double2 *const s_a3 = s_a0 + 3 * (size_t)um;                              // vz, rho
-  double *const s_e = reinterpret_cast<double *>(blk_smem + (size_t)um * 64);  // e (HEAT)
-  unsigned char *const s_t = blk_smem + (size_t)um * (HEAT ? 72 : 64);
   const int nt1 = cf->ntypes + 1;
   const int b = blist ? blist[blockIdx.x] : (int)xcd_block();
   const int tid = threadIdx.x;
   const int u = EXP == 3 ? 0 : ucnt[b];
   if (!blist && u > um) return;  // (workgroup-uniform) left to the large-union launch
+  const int row = b * R + tid / G, lane = tid & (G - 1);
+  const bool live = row < n;
+  const int rr = live ? row : n - 1;
+  // loads first: the row's count, the union's atom ids, then the row's slots and the
+  // union's records, so that one latency covers them all
+  const int c = live ? rcnt[rr] : 0;
+  const int *const ul = ulist + (size_t)b * ucap;
+  int jj[BLK_SP];
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++) jj[k] = tid + k * NTH < u ? ul[tid + k * NTH] : -1;
+  BlkSlots<G, U, NCH> sw;
+  sw.load(snbr + (size_t)rr * sstride, c, lane);
+  const double4 xi = xf[rr];
+  const double4 vi = vr[rr];
+  const double ei = HEAT ? en[rr] : 0.0;
+  const int it = NT1 ? 1 : ty[rr];
+  double4 qx[BLK_SP], qv[BLK_SP];
+  double ge[BLK_SP];
+  int gt[BLK_SP];
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++)
+    if (jj[k] >= 0) {
+      qx[k] = xf[jj[k]];
+      qv[k] = vr[jj[k]];
+      if (HEAT) ge[k] = en[jj[k]];
+      if (!NT1) gt[k] = ty[jj[k]];
+    }
   if (!NT1)
     for (int t = tid; t < nt1 * nt1; t += NTH) {
       if (TAIT) s_tp[t] = cf->tait[t];
       if (HEAT) s_hp[t] = cf->heat[t];
     }
-  const int *const ul = ulist + (size_t)b * ucap;
-  for (int p = tid; p < u; p += NTH) {
+  unsigned char *const s_t = blk_smem + (size_t)((u + 16) >> 4) * cq * 16;
+#pragma unroll
+  for (int k = 0; k < BLK_SP; k++)
+    if (jj[k] >= 0) {
+      const int sl = tid + k * NTH + 1;
+      blk_put<HEAT>(blk_smem, sl, cq, qx[k], qv[k], HEAT ? ge[k] : 0.0);
+      if (!NT1) s_t[blk_q(sl, cq)] = (unsigned char)gt[k];
+    }
+  for (int p = tid + BLK_SP * NTH; p < u; p += NTH) {
     const int j = ul[p];
-    const double4 x = xf[j], v = vr[j];
-    s_a0[p] = make_double2(x.x, x.y);
-    s_a1[p] = make_double2(x.z, x.w);
-    s_a2[p] = make_double2(v.x, v.y);
-    s_a3[p] = make_double2(v.z, v.w);
-    if (HEAT) s_e[p] = en[j];
-    if (!NT1) s_t[p] = (unsigned char)ty[j];
+    blk_put<HEAT>(blk_smem, p + 1, cq, xf[j], vr[j], HEAT ? en[j] : 0.0);
+    if (!NT1) s_t[blk_q(p + 1, cq)] = (unsigned char)ty[j];
+  }
+  if (tid == 0) {
+    blk_put_sentinel<HEAT>(blk_smem);
+    if (!NT1) s_t[0] = 1;
   }
   __syncthreads();
-  const int row = b * R + tid / G, lane = tid & (G - 1);
-  const bool live = row < n;
-  const int rr = live ? row : n - 1;
-  const double4 xi = xf[rr];
-  const double4 vi = vr[rr];
-  const double ei = HEAT ? en[rr] : 0.0;
-  const int it = NT1 ? 1 : ty[rr];
   TaitPair t1{};
   HeatPair h1{};
   if (NT1) {
     if (TAIT) t1 = cf->tait[3];
     if (HEAT) h1 = cf->heat[3];
   }
-  const int c = live ? rcnt[rr] : 0;
-  double fx = 0.0, fy = 0.0, fz = 0.0, drho = 0.0, dE = 0.0;
-  blk_walk<G, U, NCH>(snbr + (size_t)rr * sstride, c, lane, [&](int sj, bool ok) {
+  // F: sum of (d x) sp (- vel sv); E: sum of sp dvdr (- sv vel^2); D: sum of dvdr w; EH:
+  // the heat terms.  One type: sp = (P_i/rho_i^2 + P_j/rho_j^2 [+ fvisc]) w, the row's
+  // factors applied at the end; several types: sp, sv, D and EH terms carry them per pair.
+  double fx = 0.0, fy = 0.0, fz = 0.0, D = 0.0, E = 0.0, EH = 0.0;
+  sw.walk(c, lane, [&](int q, bool) {
+    const unsigned char *const rec = blk_smem + q * 16;
     double2 a0, a1, a2, a3;
     if (EXP == 1) {
-      const double o = (double)(sj & 7);
+      const double o = (double)(q & 7);
       a0 = make_double2(xi.x + 0.25 * o, xi.y + 0.5);
       a1 = make_double2(xi.z - 0.125 * o, xi.w);
       a2 = make_double2(vi.x, vi.y - 0.01 * o);
       a3 = make_double2(vi.z, vi.w);
     } else {
-      a0 = s_a0[sj];
-      a1 = s_a1[sj];
-      a2 = s_a2[sj];
-      a3 = s_a3[sj];
+      a0 = *reinterpret_cast<const double2 *>(rec);
+      a1 = *reinterpret_cast<const double2 *>(rec + 256);
+      a2 = *reinterpret_cast<const double2 *>(rec + 512);
+      a3 = *reinterpret_cast<const double2 *>(rec + 768);
     }
     if (EXP == 2) {
       fx += a0.x + a2.x;
       fy += a0.y + a2.y;
       fz += a1.x + a3.x;
-      drho += a1.y + a3.y;
+      D += a1.y + a3.y;
       return;
     }
     const double dx = xi.x - a0.x, dy = xi.y - a0.y, dz = xi.z - a1.x;
     const double rsq = dx * dx + dy * dy + dz * dz;
-    const int pidx = NT1 ? 3 : it * nt1 + s_t[sj];
+    const int pidx = NT1 ? 3 : it * nt1 + s_t[q];
     const double r = sqrt1(rsq);
     if (TAIT) {
       const TaitPair cc = NT1 ? t1 : s_tp[pidx];
-      const bool hit = ok && rsq < cc.cutsq;
-      double wfd = cc.h - r;
-      wfd = cc.wK * (wfd * wfd);
-      wfd = hit ? wfd : 0.0;
+      const double d = fmax(cc.h - r, 0.0);
+      const double w = NT1 ? d * d : cc.wK * (d * d);
       const double velx = vi.x - a2.x, vely = vi.y - a2.y, velz = vi.z - a3.x;
       const double dvdr = dx * velx + dy * vely + dz * velz;
       if (VISC == SPH_VISC_MONAGHAN) {
-        const double qv = (cc.viscC * dvdr) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
-        const double fvisc = dvdr < 0. ? qv : 0.0;
-        const double fpair = cc.mm * (xi.w + a1.y + fvisc) * wfd;
-        fx += dx * fpair;
-        fy += dy * fpair;
-        fz += dz * fpair;
-        dE += -0.5 * fpair * dvdr;
+        // fvisc = viscC dvdr / ((rsq + eps)(rho_i + rho_j)) for dvdr < 0, else 0
+        const double fv =
+            (cc.viscC * fmin(dvdr, 0.0)) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
+        const double sp = NT1 ? (xi.w + a1.y + fv) * w : cc.mm * ((xi.w + a1.y + fv) * w);
+        fx += dx * sp;
+        fy += dy * sp;
+        fz += dz * sp;
+        E += sp * dvdr;
       } else {
-        double fvisc = cc.viscC * rcp1(vi.w * a3.y);
-        fvisc = hit ? fvisc * ((-cc.mm) * wfd) : 0.0;
-        const double fpair = cc.mm * (xi.w + a1.y) * wfd;
-        fx += dx * fpair + velx * fvisc;
-        fy += dy * fpair + vely * fvisc;
-        fz += dz * fpair + velz * fvisc;
-        dE += -0.5 * (fpair * dvdr + fvisc * (velx * velx + vely * vely + velz * velz));
+        const double sp = NT1 ? (xi.w + a1.y) * w : cc.mm * ((xi.w + a1.y) * w);
+        const double cv = cc.viscC * rcp1(vi.w * a3.y);
+        const double sv = NT1 ? cv * w : cc.mm * (cv * w);
+        fx += dx * sp - velx * sv;
+        fy += dy * sp - vely * sv;
+        fz += dz * sp - velz * sv;
+        E += sp * dvdr - sv * (velx * velx + vely * vely + velz * velz);
       }
-      drho += cc.mj * dvdr * wfd;
+      D += NT1 ? dvdr * w : cc.mj * (dvdr * w);
     }
     if (HEAT) {
       const HeatPair cc = NT1 ? h1 : s_hp[pidx];
-      const bool hit = ok && rsq < cc.cutsq;
-      double wfd = cc.h - r;
-      wfd = cc.wK * (wfd * wfd);
-      wfd = hit ? wfd : 0.0;
-      double deltaE = cc.hmD;
-      deltaE *= (vi.w + a3.y) * rcp1(vi.w * a3.y);
-      deltaE = hit ? deltaE * ((ei - s_e[sj]) * wfd) : 0.0;
-      dE += deltaE;
+      const double d = fmax(cc.h - r, 0.0);
+      const double w = NT1 ? d * d : cc.wK * (d * d);
+      const double ej = *reinterpret_cast<const double *>(rec + 1024);
+      const double t = ((vi.w + a3.y) * rcp1(vi.w * a3.y)) * ((ei - ej) * w);
+      EH += NT1 ? t : cc.hmD * t;
     }
   });
   if (TAIT) {
     fx = group_sum<G>(fx);
     fy = group_sum<G>(fy);
     fz = group_sum<G>(fz);
-    drho = group_sum<G>(drho);
+    D = group_sum<G>(D);
+    E = group_sum<G>(E);
   }
-  dE = group_sum<G>(dE);
+  if (HEAT) EH = group_sum<G>(EH);
   if (lane == 0 && live) {
+    double dE = 0.0;
     if (TAIT) {
+      // one type: F, E scale by m_i m_j wK (mm = -m_i m_j), D by m_j wK
+      const double g = NT1 ? t1.mm * t1.wK : 1.0;
+      const double gd = NT1 ? t1.mj * t1.wK : 1.0;
       const double m = cf->mass[it];
-      fo[row] = make_double4(fx + m * gx, fy + m * gy, fz + m * gz, drho);
+      fo[row] = make_double4(g * fx + m * gx, g * fy + m * gy, g * fz + m * gz, gd * D);
+      dE = -0.5 * (g * E);
     }
+    if (HEAT) dE += NT1 ? (h1.hmD * h1.wK) * EH : EH;
     de[row] = dE;
   }
 }
@@ -639,6 +749,7 @@ struct BlkArgs {
   int nbig = 0;         // blocks with a union larger than umf (listed in blist)
   int sstride = 0;      // slot-row stride (entries)
   int exp = 0;          // study variants (SPH_EXP), 0 in production
+  int cq = BLK_CH / 16;  // image chunk bytes / 16 (BLK_CHE / 16 with the heat term)
   const int *ulist = nullptr, *ucnt = nullptr, *rcnt = nullptr, *blist = nullptr;
   const unsigned short *snbr = nullptr;
   bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
@@ -651,31 +762,31 @@ inline void blk_neigh_t(bool nt1, hipStream_t s, int n, const QBins &q, int dim,
                         const double4 *xf, const int *ty, const double4 *xb, const int *tb,
                         const int *qbeg, const int *xpos, const Coefs *cf, int ucap,
                         int sstride, int *ulist, int *ucnt, int *rcnt, unsigned short *snbr,
-                        int *ovf, int *umax, int bexp) {
+                        int *ovf, int *umax, int cq, int bexp) {
   if (nt1)
     hipLaunchKernelGGL((k_blk_neigh<R, G, U, true, MC>), dim3(blk_blocks(n, R)),
                        dim3(R * BLK_TPR), 0, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf, ucap,
-                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp);
+                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, cq, bexp);
   else
     hipLaunchKernelGGL((k_blk_neigh<R, G, U, false, MC>), dim3(blk_blocks(n, R)),
                        dim3(R * BLK_TPR), 0, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf, ucap,
-                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp);
+                       sstride, ulist, ucnt, rcnt, snbr, ovf, umax, cq, bexp);
 }
 // big: the large candidate image (BLK_MBIG; 32-row shapes only)
 inline void blk_neigh(int shape, bool big, bool nt1, hipStream_t s, int n, const QBins &q,
                       int dim, const double4 *xf, const int *ty, const double4 *xb,
                       const int *tb, const int *qbeg, const int *xpos, const Coefs *cf,
                       int ucap, int sstride, int *ulist, int *ucnt, int *rcnt,
-                      unsigned short *snbr, int *ovf, int *umax, int bexp = 0) {
+                      unsigned short *snbr, int *ovf, int *umax, int cq, int bexp = 0) {
   switch (shape) {
 #define SPH_CASE(k, R, G, U)                                                                \
   case k:                                                                                 \
     if (big && R == 32)                                                                   \
       blk_neigh_t<R, G, U, BLK_MBIG>(nt1, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf,   \
-                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp); \
+                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, cq, bexp); \
     else                                                                                  \
       blk_neigh_t<R, G, U, BLK_MCAP>(nt1, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf,   \
-                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, bexp); \
+                                     ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, cq, bexp); \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE
@@ -686,7 +797,8 @@ template <int R, int G, int U, int NCH, bool NT1>
 inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
                          double4 *vr, const Coefs *cf) {
   const size_t lds = blk_rho_lds(k.um, NT1);
-  auto fn = k_blk_rhosum<R, G, U, NCH, NT1>;
+  auto fn = k.cq == BLK_CH / 16 ? k_blk_rhosum<R, G, U, NCH, NT1, BLK_CH / 16>
+                                : k_blk_rhosum<R, G, U, NCH, NT1, BLK_CHE / 16>;
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
@@ -718,19 +830,18 @@ inline void blk_rhosum(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, c
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
 inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
   auto fn = k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;
-  const bool heat = (MODE & M_HEAT) != 0;
-  // main launch: every block whose union fits umf records; then the large-union blocks
-  const size_t lds = blk_force_lds(k.umf, heat, NT1);
-  const size_t ldsb = blk_force_lds(k.um, heat, NT1);
+  // main launch: every block whose union fits umf atoms; then the large-union blocks
+  const size_t lds = blk_lds(k.umf, k.cq, NT1);
+  const size_t ldsb = blk_lds(k.um, k.cq, NT1);
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)std::max(lds, ldsb)));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
-                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr);
+                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq);
   if (k.nbig > 0)
     hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
                        k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
-                       a.gx, a.gy, a.gz, k.um, k.blist);
+                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq);
 }
 template <int R, int G, int U, int NCH, bool NT1>
 inline void blk_force_n(int visc, int mode, hipStream_t s, const BlkArgs &k, const RowArgs &a) {

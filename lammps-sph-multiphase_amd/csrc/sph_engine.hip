@@ -805,7 +805,7 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
       blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                 dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
-                env_int("SPH_BEXP", 0));
+                blk_cq(), env_int("SPH_BEXP", 0));
       int hm[5];
       SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
@@ -822,8 +822,7 @@ struct sph_engine {
       if (hm[0] != 0) return 2;
       // the largest union's force-pass LDS image (+ the static coefficient tables) must fit
       // the CU's 160 KiB
-      const size_t lds_big = blk_force_lds(std::max(hm[1], 1), (force_mode & M_HEAT) != 0,
-                                           nt1()) +
+      const size_t lds_big = blk_lds(std::max(hm[1], 1), blk_cq(), nt1()) +
                              (nt1() ? 0 : (sizeof(TaitPair) + sizeof(HeatPair)) * NT2);
       if (lds_big > 160 * 1024 - 1024) return 2;
       blk_sh = shape;
@@ -845,8 +844,11 @@ struct sph_engine {
     }
     return 0;
   }
+  // the union image's chunk size / 16 (sph_blk_kernels.h): with the heat term's e array
+  int blk_cq() const { return ((force_mode & M_HEAT) ? BLK_CHE : BLK_CH) / 16; }
   BlkArgs blk_args() const {
     BlkArgs k;
+    k.cq = blk_cq();
     k.n = nlocal;
     k.shape = blk_sh;
     k.exp = row2_exp();

@@ -134,9 +134,10 @@ __device__ __forceinline__ double rcp1(double b) {
   return fma(y, fma(-b, y, 1.0), y);
 }
 // sqrt(x), x >= 0: v_rsq_f64 seed y, r = x*y, one Newton correction r += (x - r^2) y / 2.
-// x is floored at 1e-300 so a coincident pair gives r ~ 1e-150 instead of NaN.
+// x + 1e-300 (== x for any x above ~1e-284) makes a coincident pair give r ~ 1e-150
+// instead of NaN.
 __device__ __forceinline__ double sqrt1(double x) {
-  x = fmax(x, 1e-300);
+  x += 1e-300;
   const double y = __builtin_amdgcn_rsq(x);
   const double r = x * y;
   return fma(fma(-r, r, x), 0.5 * y, r);

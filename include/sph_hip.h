@@ -220,8 +220,10 @@ typedef struct {
   int heat_on;
   double heat_alpha[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
   double heat_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
-  /* body force per unit mass (fix gravity style), added in post_force: f += m*g */
+  /* body force per unit mass (fix gravity style), added in post_force: f += m*g, for the
+     types in gravity_mask (bit t set: type t is in the fix's group; 0 = every type) */
   double gravity[3];
+  int gravity_mask;
   /* brick decomposition (procgrid[0]*procgrid[1]*procgrid[2] bricks, uniform split; 1 1 1 or
      0 0 0 = one brick).  Bricks are numbered x fastest; each must be wider than the ghost
      cutoff (CommBrick maxneed = 1). */

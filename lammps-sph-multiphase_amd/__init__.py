@@ -56,7 +56,7 @@ class EngineConfig(C.Structure):
         ("B", C.c_double * (SPH_MAXTYPES + 1)),
         ("tait_visc_coef", C.c_double * _NT2), ("tait_cut", C.c_double * _NT2),
         ("heat_on", C.c_int), ("heat_alpha", C.c_double * _NT2), ("heat_cut", C.c_double * _NT2),
-        ("gravity", C.c_double * 3),
+        ("gravity", C.c_double * 3), ("gravity_mask", C.c_int),
         ("procgrid", C.c_int * 3), ("rank", C.c_int), ("sort", C.c_int),
         ("kernel_path", C.c_int),
     ]
@@ -332,7 +332,7 @@ def _pair_table(dst, tab, ntypes):
 def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every=10,
                 rhosum=None, tait=None, heat=None, gravity=(0.0, 0.0, 0.0),
                 stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0,
-                kernel_path=0) -> EngineConfig:
+                kernel_path=0, gravity_mask=0) -> EngineConfig:
     """kernel_path: 0 = the production pair passes (block-staged LDS unions + 16-bit slot
     rows; bench.py's path), 1 = the row path (row2 gathers over strided global lists).
     rhosum = dict(nstep, cut); tait = dict(rho0, c0, visc, cut, morris[, B]);
@@ -348,6 +348,7 @@ def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every
     for t in range(ntypes + 1):
         c.mass[t] = float(mass[t])
     c.stationary_mask = stationary_mask
+    c.gravity_mask = gravity_mask
     c.sort = sort
     c.kernel_path = kernel_path
     if rhosum:

@@ -532,7 +532,8 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   });
   acc = group_sum<G>(acc);
   if (lane == 0 && live) {
-    const double rho = cf->self_rho[it] + (NT1 ? c1.mK * acc : acc);
+    const double rho = ((cf->rho_keep >> it) & 1) ? vr[row].w
+                                                   : cf->self_rho[it] + (NT1 ? c1.mK * acc : acc);
     vr[row].w = rho;
     xf[row].w = tait_p_over_rho2(rho, cf->rho0[it], cf->B[it]);
   }

@@ -19,7 +19,11 @@ inline void coef_rhosum(Coefs &c, int dim, int nt, const double *cut, const doub
     const double h = upper(cut, nt, i, i);
     const double wf = (dim == 3) ? 2.1541870227086614782 / (h * h * h)
                                  : 1.5915494309189533576e0 / (h * h);
-    c.self_rho[i] = mass[i] * wf;
+    c.self_rho[i] = h > 0.0 ? mass[i] * wf : 0.0;
+    // no pair of this type has a rhosum coefficient: the type is skipped (hybrid/overlay)
+    bool any = false;
+    for (int j = 1; j <= nt; j++) any = any || upper(cut, nt, i, j) > 0.0;
+    if (!any) c.rho_keep |= 1 << i;
     for (int j = 1; j <= nt; j++) {
       const double hh = upper(cut, nt, i, j);
       const double ih = 1.0 / hh, ihsq = ih * ih;
@@ -28,6 +32,9 @@ inline void coef_rhosum(Coefs &c, int dim, int nt, const double *cut, const doub
       r.ihsq = ihsq;
       r.mK = mass[j] * ((dim == 3) ? 2.1541870227086614782e0 * ihsq * ih
                                    : 1.5915494309189533576e0 * ihsq);
+      // a pair without coefficients (cut 0) contributes nothing: finite zero factors, as
+      // the kernels weight every pair arithmetically instead of branching on the cut
+      if (hh <= 0.0) r = RhoPair{0.0, 0.0, 0.0};
     }
   }
 }
@@ -55,6 +62,11 @@ inline void coef_tait(Coefs &c, int dim, int nt, int visc_variant, const double 
       const double v = upper(visc, nt, i, j);
       t.viscC = (visc_variant == SPH_VISC_MONAGHAN) ? -v * (c0[i] + c0[j]) * h : 2 * v;
       t.eps = 0.01 * h * h;
+      if (h <= 0.0) {  // no coefficients: zero weight, finite factors (see coef_rhosum)
+        t.wK = 0.0;
+        t.viscC = 0.0;
+        t.eps = 1.0;
+      }
     }
 }
 
@@ -71,6 +83,7 @@ inline void coef_heat(Coefs &c, int dim, int nt, const double *alpha, const doub
       p.wK = (dim == 3) ? -25.066903536973515383e0 * ihsq * ihsq * ihsq * ih
                         : -19.098593171027440292e0 * ihsq * ihsq * ihsq;
       p.hmD = 2.0 * mass[i] * mass[j] / (mass[i] + mass[j]) * upper(alpha, nt, i, j);
+      if (h <= 0.0) p.wK = 0.0;  // no coefficients (see coef_rhosum)
     }
 }
 

@@ -1150,7 +1150,8 @@ struct sph_engine {
     // post_force body force (fix gravity style), as the full-list kernel applies it
     if (cfg.gravity[0] != 0.0 || cfg.gravity[1] != 0.0 || cfg.gravity[2] != 0.0)
       hipLaunchKernelGGL(k_add_gravity, dim3(blocks(n)), dim3(BLK), 0, s, n, sc,
-                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], ty.p, fo.p);
+                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], cfg.gravity_mask,
+                         ty.p, fo.p);
     SPH_HIP_TRY(hipStreamSynchronize(s));  // scratch lists are freed on return
     hcnt.release();
     hoff.release();
@@ -1236,7 +1237,9 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     Coefs &c = e->hc;
     c.ntypes = nt;
     c.dim = cfg->dim;
-    for (int t = 0; t <= nt; t++) c.mass[t] = cfg->mass[t];
+    // the body-force mass: the types of the gravity fix's group (gravity_mask, 0 = all)
+    for (int t = 0; t <= nt; t++)
+      c.mass[t] = (cfg->gravity_mask == 0 || ((cfg->gravity_mask >> t) & 1)) ? cfg->mass[t] : 0.0;
     // per-type-pair tables are passed in the engine's fixed (SPH_MAXTYPES+1)^2 layout
     auto repack = [&](const double *src, std::vector<double> &dst) {
       dst.assign((nt + 1) * (nt + 1), 0.0);

@@ -565,12 +565,16 @@ static __global__ void k_reverse(int nghost, int nlocal, const int *__restrict__
   atomicAdd(&de[o], de[nlocal + g]);
 }
 
-// fix gravity-style post_force body force: f += m g (owned)
+// fix gravity post_force body force (fix_gravity.cpp post_force): f += m g for the owned
+// atoms of the fix's group (gmask: bit t = type t in the group; 0 = all)
 static __global__ void k_add_gravity(int n, StepConst sc, double gx, double gy, double gz,
-                                     const int *__restrict__ ty, double4 *__restrict__ fo) {
+                                     int gmask, const int *__restrict__ ty,
+                                     double4 *__restrict__ fo) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double m = sc.mass[ty[i]];
+  const int t = ty[i];
+  if (gmask != 0 && !((gmask >> t) & 1)) return;
+  const double m = sc.mass[t];
   fo[i].x += m * gx;
   fo[i].y += m * gy;
   fo[i].z += m * gz;

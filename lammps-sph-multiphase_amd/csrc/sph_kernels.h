@@ -48,7 +48,11 @@ struct HeatPair {  // sph/heatconduction (pair_sph_heatconduction.cpp:103-129)
 
 struct Coefs {
   int ntypes, dim;
+  // bit t: sph/rhosum has no coefficients for type t, so under hybrid/overlay its rows are
+  // on the skip list (pair_hybrid.cpp:439-471, neigh_derive.cpp:186) and keep their rho
+  int rho_keep;
   double self_rho[MAXT + 1];   // mass[t] * norm / h_tt^3 (pair_sph_rhosum.cpp:116-138)
+  // mass: the body-force (fix gravity) mass of type t -- 0 for types outside the fix's group
   double rho0[MAXT + 1], B[MAXT + 1], mass[MAXT + 1];
   RhoPair rho[NT2];
   TaitPair tait[NT2];
@@ -189,7 +193,7 @@ k_rhosum(int inum, const int *__restrict__ ilist, const int *__restrict__ off,
   }
   acc = group_sum<G>(acc);
   if (lane == 0) {
-    const double rho = s_self[it] + acc;
+    const double rho = (EOS && ((cf->rho_keep >> it) & 1)) ? vr[i].w : s_self[it] + acc;
     if (rho_out) rho_out[i] = rho;
     if (EOS) {
       vr[i].w = rho;

@@ -289,7 +289,7 @@ k_row2_rhosum(int n, int nall, int ntot, const int *__restrict__ off, int stride
     tcnt[row] = tw + tq;
   }
   if (lane == 0 && live) {
-    const double rho = cf->self_rho[it] + acc;
+    const double rho = ((cf->rho_keep >> it) & 1) ? vr[row].w : cf->self_rho[it] + acc;
     vr[row].w = rho;
     xf[row].w = tait_p_over_rho2(rho, cf->rho0[it], cf->B[it]);
   }

@@ -124,6 +124,13 @@ def lib():
                                        _dp, _dp, _dp, _dp]
         L.orc_meso_final.argtypes = [_i, _d, _ip, _dp, C.c_void_p, _dp, _dp, _dp, _dp, _dp,
                                      _dp]
+        L.orc_meso_setup_g.argtypes = [_i, _ip, _i, _dp, _dp]
+        L.orc_meso_initial_g.argtypes = [_i, _d, _d, _ip, _i, _dp, C.c_void_p, _dp, _dp, _dp,
+                                         _dp, _dp, _dp, _dp, _dp]
+        L.orc_meso_final_g.argtypes = [_i, _d, _ip, _i, _dp, C.c_void_p, _dp, _dp, _dp, _dp,
+                                       _dp, _dp]
+        L.orc_meso_stationary.argtypes = [_i, _d, _ip, _i, _dp, _dp, _dp, _dp]
+        L.orc_gravity.argtypes = [_i, _ip, _i, _dp, C.c_void_p, _dp, _dp]
         _lib = L
     return _lib
 
@@ -142,6 +149,8 @@ def ref():
         R.ref_neigh_full.restype = _l
         R.ref_neigh_half_from_full.argtypes = [_i, _i, _dp, _lp, _ip, _lp, C.c_void_p]
         R.ref_neigh_half_from_full.restype = _l
+        R.ref_fix_meso.argtypes = [_i, _i, _i, _i, _d, _ip, _i, _dp, _dp, _dp, _dp, _dp, _dp,
+                                   _dp, _dp, _dp]
         R.ref_rhosum.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
         R.ref_taitwater.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _dp,
                                     _dp, _dp, _lp, _ip, _dp, _dp, _dp]
@@ -402,6 +411,23 @@ class Physics:
     heat: bool = False
     alpha: np.ndarray | None = None
     heat_cut: np.ndarray | None = None
+    # fix meso/stationary on the types of this mask, fix meso on the others
+    stationary_mask: int = 0
+    # fix gravity (style vector, acceleration per unit mass) on the types of gravity_mask
+    # (0 = all)
+    gravity: tuple = (0.0, 0.0, 0.0)
+    gravity_mask: int = 0
+
+    def rho_keep(self, nt):
+        """Types sph/rhosum has no coefficient pair for: under hybrid/overlay their rows are
+        on its skip list (pair_hybrid.cpp:439-471) and keep their rho."""
+        keep = np.zeros(nt + 1, dtype=bool)
+        if self.rhosum_cut is None:
+            return keep
+        c = np.asarray(self.rhosum_cut)
+        for t in range(1, nt + 1):
+            keep[t] = not any(c[min(t, j), max(t, j)] > 0 for j in range(1, nt + 1))
+        return keep
 
     def cutmax(self, nt):
         cm = np.zeros((nt + 1, nt + 1))
@@ -487,7 +513,10 @@ class RefRun:
         nall = g.nall
         g.x[:s.n] = s.x
         if ph.rhosum_nstep > 0 and self.step % ph.rhosum_nstep == 0:
-            s.rho[:] = rhosum(s.dim, g, nt, s.mass, ph.rhosum_cut, self.foff, self.fnb)
+            with np.errstate(all="ignore"):      # (skipped types' self terms: h = 0)
+                rho = rhosum(s.dim, g, nt, s.mass, ph.rhosum_cut, self.foff, self.fnb)
+            upd = ~ph.rho_keep(nt)[s.type]
+            s.rho[upd] = rho[upd]
             self.rho_all = g.gather(s.rho)       # forward_comm_pair
         f = np.zeros((nall, 3))
         drho = np.zeros(nall)
@@ -500,6 +529,9 @@ class RefRun:
             de += heatconduction(s.dim, g, nt, 1, self.e_all, self.rho_all, s.mass, ph.alpha,
                                  ph.heat_cut, self.hoff, self.hnb)
         reverse_comm(g, f, drho, de)
+        if any(a != 0.0 for a in ph.gravity):   # post_force
+            lib().orc_gravity(s.n, s.type, ph.gravity_mask, s.mass, None,
+                              np.asarray(ph.gravity, dtype=np.float64), f)
         self.f = f[:s.n].copy()
         self.drho = drho[:s.n].copy()
         self.de = de[:s.n].copy()
@@ -508,25 +540,43 @@ class RefRun:
     def setup(self):
         self.step = 0
         self._build()                             # borders before setup_pre_force
-        self.vest[:] = self.s.v                   # FixMeso::setup_pre_force (owned only;
-        self.vest_all[:self.s.n] = self.vest      # ghosts keep their border-time vest)
+        # FixMeso::setup_pre_force on the meso group (owned only; ghosts keep their
+        # border-time vest); meso/stationary has none
+        lib().orc_meso_setup_g(self.s.n, self.s.type, self._meso_mask(), self.s.v, self.vest)
+        self.vest_all[:self.s.n] = self.vest
         self._force()
         self.last_build = 0
 
+    def _meso_mask(self):
+        """fix meso's group: every type not under meso/stationary (0 = all)"""
+        sm = self.ph.stationary_mask
+        if sm == 0:
+            return 0
+        return sum(1 << t for t in range(1, self.s.ntypes + 1) if not (sm >> t) & 1)
+
     def run(self, nsteps):
         s, L = self.s, lib()
+        mm, sm = self._meso_mask(), self.ph.stationary_mask
         for _ in range(nsteps):
             self.step += 1
-            L.orc_meso_initial(s.n, self.ph.dt, self.dtf, s.type, s.mass, None, s.x, s.v,
-                               self.f, self.vest, s.rho, self.drho, s.e, self.de)
+            if mm or not sm:
+                L.orc_meso_initial_g(s.n, self.ph.dt, self.dtf, s.type, mm, s.mass, None, s.x,
+                                     s.v, self.f, self.vest, s.rho, self.drho, s.e, self.de)
+            if sm:
+                L.orc_meso_stationary(s.n, self.dtf, s.type, sm, s.rho, self.drho, s.e,
+                                      self.de)
             if (self.step - self.last_build) % self.ph.every == 0:
                 self._build()
                 self.last_build = self.step
             else:
                 self._forward()
             self._force()
-            L.orc_meso_final(s.n, self.dtf, s.type, s.mass, None, s.v, self.f, s.rho,
-                             self.drho, s.e, self.de)
+            if mm or not sm:
+                L.orc_meso_final_g(s.n, self.dtf, s.type, mm, s.mass, None, s.v, self.f,
+                                   s.rho, self.drho, s.e, self.de)
+            if sm:
+                L.orc_meso_stationary(s.n, self.dtf, s.type, sm, s.rho, self.drho, s.e,
+                                      self.de)
 
     def numneigh_full(self):
         return np.diff(self.foff).astype(np.int32)

@@ -46,6 +46,9 @@
 #include "pair_sph_heatconduction_phasechange.h"
 #include "pair_sph_colorgradient.h"
 #include "pair_sph_surfacetension.h"
+#include "group.h"
+#include "fix_meso.h"
+#include "fix_meso_stationary.h"
 
 using namespace LAMMPS_NS;
 
@@ -602,6 +605,67 @@ int ref_surfacetension(int dim, int ntypes, int nlocal, int nghost, int newton,
   for (int i = 0; i < nlocal + nghost; i++)
     for (int k = 0; k < 3; k++) f[3 * i + k] = w.lmp->atom->f[i][k];
   free_list(l);
+  return 0;
+}
+
+// FixMeso / FixMesoStationary (fix_meso.cpp, fix_meso_stationary.cpp), built by their own
+// constructors ("ID group style", Fix::Fix -> Group::find) on the group "g" = the atoms whose
+// type is in tmask (0: group "all"), then init() (dtv, dtf from update->dt, force->ftm2v) and
+// one call: phase 0 = setup_pre_force (FixMeso), 1 = initial_integrate, 2 = final_integrate.
+// Arrays are owned atoms, updated in place.
+int ref_fix_meso(int stationary, int phase, int nlocal, int ntypes, double dt, const int *type,
+                 int tmask, const double *mass, double *x, double *v, const double *f,
+                 double *vest, double *rho, const double *drho, double *e, const double *de) {
+  World w(3, ntypes, nlocal, 0, 1, 0);
+  Atom *a = w.lmp->atom;
+  a->firstgroup = -1;  // (Atom::Atom's default; the zero-allocated Atom has 0 = "all")
+  w.lmp->update->dt = dt;
+  w.lmp->force->ftm2v = 1.0;
+  Group *grp = new Group(w.lmp);
+  w.lmp->group = grp;
+  grp->names[1] = new char[2];
+  strcpy(grp->names[1], "g");
+  grp->ngroup = 2;
+  for (int t = 0; t <= ntypes; t++) a->mass[t] = mass[t];
+  for (int i = 0; i < nlocal; i++) {
+    for (int k = 0; k < 3; k++) {
+      a->x[i][k] = x[3 * i + k];
+      a->v[i][k] = v[3 * i + k];
+      a->f[i][k] = f[3 * i + k];
+      a->vest[i][k] = vest[3 * i + k];
+    }
+    a->type[i] = type[i];
+    a->mask[i] = 1 | (((tmask >> type[i]) & 1) ? grp->bitmask[1] : 0);
+    a->rho[i] = rho[i];
+    a->drho[i] = drho[i];
+    a->e[i] = e[i];
+    a->de[i] = de[i];
+  }
+  char id[] = "f1", all[] = "all", g[] = "g", meso[] = "meso", stat[] = "meso/stationary";
+  char *arg[3] = {id, tmask ? g : all, stationary ? stat : meso};
+  Fix *fix;
+  if (stationary)
+    fix = new FixMesoStationary(w.lmp, 3, arg);
+  else
+    fix = new FixMeso(w.lmp, 3, arg);
+  fix->init();
+  if (phase == 0) {
+    if (stationary) return -1;  // (meso/stationary has no setup_pre_force)
+    fix->setup_pre_force(0);
+  } else if (phase == 1) {
+    fix->initial_integrate(0);
+  } else {
+    fix->final_integrate();
+  }
+  for (int i = 0; i < nlocal; i++) {
+    for (int k = 0; k < 3; k++) {
+      x[3 * i + k] = a->x[i][k];
+      v[3 * i + k] = a->v[i][k];
+      vest[3 * i + k] = a->vest[i][k];
+    }
+    rho[i] = a->rho[i];
+    e[i] = a->e[i];
+  }
   return 0;
 }
 

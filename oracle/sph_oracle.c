@@ -808,6 +808,70 @@ void orc_meso_setup(int nlocal, const double *v, double *vest) {
   memcpy(vest, v, sizeof(double) * 3 * (size_t)nlocal);
 }
 
+static int in_group(const int *type, int tmask, int i) {
+  return tmask == 0 || ((tmask >> type[i]) & 1);
+}
+
+/* FixMeso::setup_pre_force (fix_meso.cpp:68-85): vest = v for the group's atoms */
+void orc_meso_setup_g(int nlocal, const int *type, int tmask, const double *v, double *vest) {
+  for (int i = 0; i < nlocal; i++)
+    if (in_group(type, tmask, i))
+      for (int k = 0; k < 3; k++) vest[3 * i + k] = v[3 * i + k];
+}
+
+/* FixMeso::initial_integrate (fix_meso.cpp:91-140) over the group's atoms */
+void orc_meso_initial_g(int nlocal, double dtv, double dtf, const int *type, int tmask,
+                        const double *mass, const double *rmass, double *x, double *v,
+                        const double *f, double *vest, double *rho, const double *drho,
+                        double *e, const double *de) {
+  for (int i = 0; i < nlocal; i++) {
+    if (!in_group(type, tmask, i)) continue;
+    const double dtfm = rmass ? dtf / rmass[i] : dtf / mass[type[i]];
+    e[i] += dtf * de[i];
+    rho[i] += dtf * drho[i];
+    for (int k = 0; k < 3; k++) {
+      vest[3 * i + k] = v[3 * i + k] + 2.0 * dtfm * f[3 * i + k];
+      v[3 * i + k] += dtfm * f[3 * i + k];
+      x[3 * i + k] += dtv * v[3 * i + k];
+    }
+  }
+}
+
+/* FixMeso::final_integrate (fix_meso.cpp:144-180) over the group's atoms */
+void orc_meso_final_g(int nlocal, double dtf, const int *type, int tmask, const double *mass,
+                      const double *rmass, double *v, const double *f, double *rho,
+                      const double *drho, double *e, const double *de) {
+  for (int i = 0; i < nlocal; i++) {
+    if (!in_group(type, tmask, i)) continue;
+    const double dtfm = rmass ? dtf / rmass[i] : dtf / mass[type[i]];
+    for (int k = 0; k < 3; k++) v[3 * i + k] += dtfm * f[3 * i + k];
+    e[i] += dtf * de[i];
+    rho[i] += dtf * drho[i];
+  }
+}
+
+/* FixMesoStationary::initial_integrate / final_integrate (fix_meso_stationary.cpp:71-112):
+   the group's atoms integrate only e and rho; x, v and vest stay */
+void orc_meso_stationary(int nlocal, double dtf, const int *type, int tmask, double *rho,
+                         const double *drho, double *e, const double *de) {
+  for (int i = 0; i < nlocal; i++) {
+    if (!in_group(type, tmask, i)) continue;
+    e[i] += dtf * de[i];
+    rho[i] += dtf * drho[i];
+  }
+}
+
+/* FixGravity::post_force (fix_gravity.cpp:244-295), style vector: acc = magnitude * unit
+   direction (set_acceleration, :320-336); f += massone * acc for the group's owned atoms */
+void orc_gravity(int nlocal, const int *type, int tmask, const double *mass,
+                 const double *rmass, const double *acc, double *f) {
+  for (int i = 0; i < nlocal; i++) {
+    if (!in_group(type, tmask, i)) continue;
+    const double m = rmass ? rmass[i] : mass[type[i]];
+    for (int k = 0; k < 3; k++) f[3 * i + k] += m * acc[k];
+  }
+}
+
 void orc_meso_initial(int nlocal, double dtv, double dtf, const int *type,
                       const double *mass, const double *rmass, double *x, double *v,
                       const double *f, double *vest, double *rho, const double *drho,

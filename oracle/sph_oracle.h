@@ -146,8 +146,23 @@ void orc_surfacetension(int dim, int nlocal, int newton_pair, const double *x,
                         const double *cg, const double *cut, const double *cutsq,
                         const long *off, const int *neigh, double *f);
 
-/* ---- integrator (fix meso) -------------------------------------------------------- */
+/* ---- integrators (fix meso, fix meso/stationary, fix gravity) ------------------------
+   tmask: the fix's group as a type mask (bit t: type t in the group; 0 = all atoms) */
 void orc_meso_setup(int nlocal, const double *v, double *vest);
+void orc_meso_setup_g(int nlocal, const int *type, int tmask, const double *v, double *vest);
+void orc_meso_initial_g(int nlocal, double dtv, double dtf, const int *type, int tmask,
+                        const double *mass, const double *rmass, double *x, double *v,
+                        const double *f, double *vest, double *rho, const double *drho,
+                        double *e, const double *de);
+void orc_meso_final_g(int nlocal, double dtf, const int *type, int tmask, const double *mass,
+                      const double *rmass, double *v, const double *f, double *rho,
+                      const double *drho, double *e, const double *de);
+/* FixMesoStationary::initial_integrate == ::final_integrate (fix_meso_stationary.cpp:71-112) */
+void orc_meso_stationary(int nlocal, double dtf, const int *type, int tmask, double *rho,
+                         const double *drho, double *e, const double *de);
+/* FixGravity::post_force, style vector (fix_gravity.cpp:244-295, :320-336): f += m*acc */
+void orc_gravity(int nlocal, const int *type, int tmask, const double *mass,
+                 const double *rmass, const double *acc, double *f);
 void orc_meso_initial(int nlocal, double dtv, double dtf, const int *type,
                       const double *mass, const double *rmass, double *x, double *v,
                       const double *f, double *vest, double *rho, const double *drho,

@@ -2,6 +2,8 @@
 finishes in seconds) and the oracle evaluations the HIP path is compared against."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import pyoracle as po
@@ -14,6 +16,36 @@ def c2_system(n=8, seed=12345, dim=3):
 def c3_system(n=8, seed=12345):
     return po.cubic_lattice(n, seed=seed, ntypes=2, type2_frac=0.5, mass=(1.0, 0.5),
                             rho=(1.0, 0.5), e=(1.0, 2.0))
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def water_collapse_system():
+    """C1: the reference's examples/USER/sph/water_collapse/data.initial (fixture
+    golden/water_collapse.npz, made by golden/make_water_collapse.py): 15,702 atoms, 2-D,
+    boundary f f p, atom_style meso."""
+    d = np.load(os.path.join(GOLDEN, "water_collapse.npz"))
+    return po.System(2, d["boxlo"].copy(), d["boxhi"].copy(), (0, 0, 1), d["x"].copy(),
+                     d["v"].copy(), d["type"].astype(np.int32), d["rho"].copy(), d["e"].copy(),
+                     d["cv"].copy(), 2, d["mass"].copy())
+
+
+def water_collapse_physics(h=0.03, c=10.0):
+    """water_collapse.lmp: pair_style hybrid/overlay sph/rhosum 1 sph/taitwater;
+    pair_coeff * * sph/taitwater 1000 c 1.0 h (rho0, soundspeed, viscosity, cut);
+    pair_coeff 1 1 sph/rhosum h; fix gravity -9.81 vector 0 1 0 on water (type 1); fix meso
+    on water, meso/stationary on bc (type 2); neighbor 0.3 h bin, every 5; dt = 0.1 h / c."""
+    rc = np.zeros((3, 3))
+    rc[1, 1] = h
+    tc = np.zeros((3, 3))
+    tc[1:, 1:] = h
+    visc = np.zeros((3, 3))
+    visc[1:, 1:] = 1.0
+    return po.Physics(skin=0.3 * h, dt=0.1 * h / c, every=5, rhosum_nstep=1, rhosum_cut=rc,
+                      rho0=np.array([0.0, 1000.0, 1000.0]), c0=np.array([0.0, c, c]),
+                      visc=visc, tait_cut=tc, stationary_mask=1 << 2,
+                      gravity=(0.0, -9.81, 0.0), gravity_mask=1 << 1)
 
 
 def prepared(sysm, ph: po.Physics, rho_jitter=0.02, vseed=7):

@@ -27,7 +27,8 @@ def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None, kernel_path=0):
         kw["heat"] = dict(alpha=ph.alpha, cut=ph.heat_cut)
     cfg = sph_amd.make_config(s.dim, nt, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
                               neigh_every=every or ph.every, sort=sort,
-                              kernel_path=kernel_path, **kw)
+                              kernel_path=kernel_path, stationary_mask=ph.stationary_mask,
+                              gravity=ph.gravity, gravity_mask=ph.gravity_mask, **kw)
     eng = sph_amd.Engine(cfg)
     eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)
     return eng

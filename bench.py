@@ -1,7 +1,7 @@
 """Benchmark of the MI355X USER-SPH engine on BASELINE.json's headline workload.
 
     python bench.py [--gpus N] [--scaling strong|weak] [--steps K] [--warmup W] [--edge 100]
-                    [--no-cpu] [--workload c2|c3|c2pair|c5pair]
+                    [--no-cpu] [--workload c2|c3|c5|c2pair|c5pair]
 
 Workload (BASELINE.json configs[1]): 1M particles on a jittered 100^3 cubic lattice,
 periodic, hybrid/overlay sph/rhosum (nstep 1, h 3) + sph/taitwater (rho0 1, c0 10,
@@ -638,6 +638,129 @@ def c5_pair_cpu(d):
                       ", ".join(f"{k} {v:.3f} s" for k, v in t.items())}
 
 
+def c5_system(n, dim=3, rv=0.05):
+    """BASELINE C5 geometry (examples/USER/sph/bubble_growth/bubble.lmp, vars.lmp, in.phases):
+    unit box, lattice sc dx = 1/n with origin 0.5, liquid (type 1), vapour (type 2) inside the
+    script's 'region rsq sphere ... 0.05' at the centre; rho_l 1, rho_v 0.1, cv 0.04 / 0.06,
+    e = cv T (T_l = Tinf = 1, T_v = Tc = 0), rmass = dx^dim rho (in.phases 'set type mass')."""
+    dx = 1.0 / n
+    nz = n if dim == 3 else 1
+    g = np.stack(np.meshgrid(np.arange(n), np.arange(n), np.arange(nz), indexing="ij"),
+                 -1).reshape(-1, 3)
+    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]
+    x = (g + 0.5) * dx
+    if dim == 2:
+        x[:, 2] = 0.0
+    c = np.array([0.5, 0.5, 0.5 if dim == 3 else 0.0])
+    vap = ((x - c) ** 2).sum(1) < rv * rv
+    t = np.where(vap, 2, 1).astype(np.int32)
+    rho = np.where(vap, 0.1, 1.0)
+    cv = np.where(vap, 0.06, 0.04)
+    e = np.where(vap, 0.0, 0.04)
+    return x, np.zeros_like(x), t, rho, e, cv, rho * dx ** dim
+
+
+def c5_physics(n, dim=3):
+    """bubble.lmp:57-73 pair stack with vars.lmp values (h = 3 dx, neighbor 0 bin, every 1),
+    dt = the min of settimestep.lmp's limits, fix phase_change Tc 0 Tt 0.1 Hwv 8 dr dx/2
+    mass_v h 1 2 1 123456 0.01."""
+    dx = 1.0 / n
+    h = 3.0 * dx
+    rho_l, rho_v, cv_l, cv_v = 1.0, 0.1, 0.04, 0.06
+    c_l, c_v = 200.0 / np.sqrt(rho_l), 200.0 / np.sqrt(rho_v)
+    eta_l, eta_v, D_l, D_v, alpha = 1.0, 0.69, 0.2, 0.6, 500.0
+    t2 = lambda a11, a12, a22: np.array([[0, 0, 0], [0, a11, a12], [0, a12, a22]], float)
+    hh = t2(h, h, h)
+    mp = dict(rhosum_nstep=1, rhosum_cut=hh, cg_nstep=1, cg_alpha=t2(0.0, alpha, 0.0),
+              cg_cut=hh, rho0=[0.0, rho_l, rho_v], c0=[0.0, c_l, c_v], gamma=[0.0, 1.0, 1.0],
+              rbg=[0.0, 0.0, 0.0], visc=t2(eta_l, 2 * eta_l * eta_v / (eta_l + eta_v), eta_v),
+              tait_cut=hh, st_cut=hh,
+              heat_alpha=t2(D_l, 2 * D_l * D_v / (D_l + D_v), D_v), heat_cut=hh,
+              heat_fixflag=np.array([[0, 0, 0], [0, 0, 2], [0, 2, 0]]), heat_tc=t2(0, 0, 0))
+    beta = 0.1
+    dt = min(beta * 1.44 * rho_v * cv_v * dx ** 2 / D_v, beta * 1.44 * rho_l * cv_l * dx ** 2 / D_l,
+             dx * dx / (8.0 * eta_v) * rho_v, dx * dx / (8.0 * eta_l) * rho_l,
+             0.25 * np.sqrt(rho_v * dx ** 3 / (6 * alpha)), 0.25 * np.sqrt(rho_l * dx ** 3 / (6 * alpha)),
+             0.25 * dx / c_v, 0.25 * dx / c_l)
+    pc = dict(Tc=0.0, Tt=0.1, Hwv=8.0, dr=0.5 * dx, to_mass=dx ** dim * rho_v, cutoff=h,
+              from_type=1, to_type=2, nevery=1, seed=123456, prob=0.01)
+    return mp, dt, pc
+
+
+def c5_main(args, sph):
+    """C5 on the device-resident engine: the bubble_growth stack + fix phase_change on one
+    GPU (the largest single-GPU C5, 159^3 = 4.02M), rebuilding every step as the script
+    does.  `value` = particle-steps/s of the whole step (integration, phase change, rebuild,
+    the five pair passes, reverse comm)."""
+    n = args.edge
+    x, v, t, rho, e, cv, rmass = c5_system(n)
+    mp, dt, pc = c5_physics(n)
+    N = x.shape[0]
+    cfg = sph.make_config(3, 2, [0.0] * 3, [1.0] * 3, [1, 1, 1], [0.0, 1.0, 1.0], 0.0, dt,
+                          neigh_every=1, mp=mp)
+    eng = sph.Engine(cfg)
+    eng.set_atoms(x, v, t, rho, e, cv)
+    eng.set_atoms_multiphase(rmass, cv)
+    eng.phase_change(pc["Tc"], pc["Tt"], pc["Hwv"], pc["dr"], pc["to_mass"], pc["cutoff"],
+                     pc["from_type"], pc["to_type"], nevery=pc["nevery"], seed=pc["seed"],
+                     prob=pc["prob"])
+    with stdout_to_stderr():
+        eng.setup()
+        eng.run(args.warmup)
+    eng.sync()
+    eng.set_timing(True)
+    t0 = time.perf_counter()
+    eng.run(args.steps)
+    eng.sync()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    nloc = st["nlocal"]
+    n_full = st["nbr_full"] / max(nloc, 1)
+    n_half = n_full / 2.0
+    by = c5_pair_bytes(n_half, n_full)
+    b_full = by["rhosum/multiphase"] + by["colorgradient"]
+    b_half = by["taitwater/multiphase"] + by["surfacetension"] + by["heatconduction/phasechange"]
+    ms_full = st["ms_rhosum"] / max(st["n_rhosum"], 1)
+    ms_half = st["ms_tait"] / max(st["n_tait"], 1)
+    ach_half = b_half * nloc / (ms_half * 1e-3) / 1e9
+    ach_full = b_full * nloc / (ms_full * 1e-3) / 1e9
+    mpst = eng.get_atoms_multiphase()
+    out = {
+        "metric": "particle-steps/s, C5 bubble_growth multiphase stack + fix phase_change",
+        "value": N * args.steps / elapsed, "unit": "particle-steps/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (bubble_growth geometry: sc lattice, vapour sphere r 0.05)",
+        "config": {"workload": f"C5: {N} particles ({n}^3), bubble_growth/bubble.lmp stack "
+                               "(rhosum/multiphase, colorgradient, taitwater/multiphase, "
+                               "surfacetension, heatconduction/phasechange) + fix phase_change "
+                               "every step, rebuild every step, skin 0",
+                   "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
+                   "n_full_per_particle": n_full, "n_half_per_particle": n_half,
+                   "atoms_inserted": mpst["ninserted"], "dt": dt,
+                   "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm",
+                     "kernel": "k_mp_gather (taitwater/multiphase + surfacetension + "
+                               "heatconduction/phasechange fused: full-list gather, each pair "
+                               "in its half-list orientation)",
+                     "achieved": ach_half, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": ach_half / PEAK_HBM_GBS, "traffic": None,
+                     "bytes_per_particle": b_half, "ms_per_launch": ms_half},
+        "kernels": {"full-list passes (rhosum/multiphase + colorgradient)":
+                        {"ms_per_step": ms_full, "achieved_GBs": ach_full,
+                         "bytes_per_particle": b_full},
+                    "neighbor_build_and_phase_change_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
+                    "integrate_ms_per_step": st["ms_integrate"] / args.steps,
+                    "reverse_comm_ms_per_step": st["ms_comm"] / args.steps},
+    }
+    if not args.no_cpu:
+        d = c5_pair_system(args.c5_cpu_n)
+        out["cpu_baseline"] = c5_pair_cpu(d)
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -650,9 +773,14 @@ def main():
                     help="lattice edge (default 100; c5pair 80: C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
-    ap.add_argument("--workload", choices=["c2", "c3", "c2pair", "c5pair"], default="c2",
+    ap.add_argument("--c5-cpu-n", type=int, default=40,
+                    help="c5: edge of the two-phase block the reference's five styles are "
+                         "timed on for cpu_baseline")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5", "c2pair", "c5pair"], default="c2",
                     help="c2: the headline engine step (default); c3: two-phase Morris + "
-                         "heat conduction engine step (config 3); c2pair: rhosum + taitwater "
+                         "heat conduction engine step (config 3); c5: the bubble_growth "
+                         "multiphase stack + fix phase_change on the engine (--edge 159 = "
+                         "4.02M, the largest single-GPU C5); c2pair: rhosum + taitwater "
                          "through the pair-style layer; c5pair: the multiphase pair passes "
                          "through the pair-style layer (--edge sets n^3)")
     ap.add_argument("--path", type=int, default=int(os.environ.get("SPH_PATH", "0")),
@@ -686,6 +814,10 @@ def main():
         assert world == 1, "the pair-layer workloads run on one GPU"
         args.edge = args.edge or 80
         return (c2_pair_main if args.workload == "c2pair" else c5_pair_main)(args, sph)
+    if args.workload == "c5":
+        assert world == 1, "the C5 workload runs on one GPU (fix phase_change: one brick)"
+        args.edge = args.edge or 159
+        return c5_main(args, sph)
     args.edge = args.edge or 100
     if args.workload == "c3":
         assert world == 1, "the C3 workload runs on one GPU"

@@ -195,6 +195,35 @@ int sph_hip_phasechange_finish(int nlocal, const double *dmass, double *rmass, d
  * ==================================================================================== */
 #define SPH_MAXTYPES 8
 
+/* Multiphase stack of examples/USER/sph/bubble_growth/bubble.lmp:57-73 (atom_style
+   meso/multiphase: per-atom rmass, cv, colorgradient; quintic kernel), run by the engine
+   in place of the sph/rhosum, taitwater and heatconduction styles of sph_engine_config.
+   Per-pair tables in the (SPH_MAXTYPES+1)^2 layout, upper triangle (i <= j) read and
+   mirrored as init_one does.  Sequence per step (hybrid/overlay order): rhosum/multiphase
+   and colorgradient over the full list (owned rows; their misnamed pack_comm moves
+   nothing, so ghosts keep their comm-time rho and colorgradient), then
+   taitwater/multiphase, surfacetension and heatconduction/phasechange over the half list
+   with Newton-3 and reverse comm.  fix meso integrates with rmass. */
+typedef struct {
+  int rhosum_nstep;            /* sph/rhosum/multiphase N (0 = off); cut = h per pair */
+  double rhosum_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  int cg_nstep;                /* sph/colorgradient N (0 = off): alpha, cut per pair */
+  double cg_alpha[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double cg_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  int tait_on;                 /* sph/taitwater/multiphase: per type rho0, c, gamma, rbg */
+  double rho0[SPH_MAXTYPES + 1], soundspeed[SPH_MAXTYPES + 1], gamma[SPH_MAXTYPES + 1];
+  double rbackground[SPH_MAXTYPES + 1];
+  double tait_visc[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double tait_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  int st_on;                   /* sph/surfacetension: cut per pair */
+  double st_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  int heat_on;                 /* sph/heatconduction/phasechange: alpha, cut, fixflag, tc */
+  double heat_alpha[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double heat_cut[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  double heat_tc[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+  int heat_fixflag[(SPH_MAXTYPES + 1) * (SPH_MAXTYPES + 1)];
+} sph_engine_mp_config;
+
 typedef struct {
   int dim;                     /* 2 or 3 */
   int ntypes;                  /* <= SPH_MAXTYPES */
@@ -238,6 +267,8 @@ typedef struct {
      1 = row path: rows gather neighbour records from HBM through a strided global-index
          list (the round-1 production path) */
   int kernel_path;
+  /* multiphase stack (NULL: the single-phase styles above); copied at create */
+  const sph_engine_mp_config *mp;
 } sph_engine_config;
 
 typedef struct {
@@ -282,6 +313,23 @@ int sph_engine_set_tags(sph_engine *e, const int *tags);
 int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
                          const int *type, const double *rho, const double *en,
                          const double *cv);
+/* Multiphase engines: per-atom rmass and cv (and the initial colorgradient, n*3, may be
+   NULL = 0) of the set_atoms atoms, in the same order.  After set_atoms, before setup. */
+int sph_engine_set_atoms_multiphase(sph_engine *e, const double *rmass, const double *cv,
+                                    const double *cg);
+/* fix phase_change on a one-brick multiphase engine (FixPhaseChange::pre_exchange at steps
+   1, 1+nevery, ...; the rebuild follows): p's sublo/subhi/boxhi/top are filled by the
+   engine, p->dt must be the engine's dt.  Candidates meet the Park-Miller stream (seed) in
+   ascending tag order -- the reference's atom order on one process (new atoms are
+   appended and LAMMPS sorts atoms only every 1000 steps by default).  New atoms get tags
+   n, n+1, ... in creation order (atom->tag_extend), type to_type.  Before setup. */
+int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int nevery,
+                            int seed);
+/* Multiphase fields of the owned atoms in get_atoms order (any pointer may be NULL):
+   rmass, cv, colorgradient (n*3), vest (n*3), type; *ninserted = atoms created so far. */
+int sph_engine_get_atoms_multiphase(sph_engine *e, double *rmass, double *cv, double *cg,
+                                    double *vest, int *type, int64_t *ninserted);
+
 /* Verlet::setup: forced rebuild + forces at step 0. */
 int sph_engine_setup(sph_engine *e);
 /* Verlet::run(nsteps). */

@@ -42,6 +42,23 @@ _i, _d, _vp = C.c_int, C.c_double, C.c_void_p
 _lib = None
 
 
+class EngineMpConfig(C.Structure):
+    """sph_engine_mp_config (include/sph_hip.h section 2): the bubble_growth stack."""
+    _fields_ = [
+        ("rhosum_nstep", C.c_int), ("rhosum_cut", C.c_double * _NT2),
+        ("cg_nstep", C.c_int), ("cg_alpha", C.c_double * _NT2), ("cg_cut", C.c_double * _NT2),
+        ("tait_on", C.c_int), ("rho0", C.c_double * (SPH_MAXTYPES + 1)),
+        ("soundspeed", C.c_double * (SPH_MAXTYPES + 1)),
+        ("gamma", C.c_double * (SPH_MAXTYPES + 1)),
+        ("rbackground", C.c_double * (SPH_MAXTYPES + 1)),
+        ("tait_visc", C.c_double * _NT2), ("tait_cut", C.c_double * _NT2),
+        ("st_on", C.c_int), ("st_cut", C.c_double * _NT2),
+        ("heat_on", C.c_int), ("heat_alpha", C.c_double * _NT2),
+        ("heat_cut", C.c_double * _NT2), ("heat_tc", C.c_double * _NT2),
+        ("heat_fixflag", C.c_int * _NT2),
+    ]
+
+
 class EngineConfig(C.Structure):
     _fields_ = [
         ("dim", C.c_int), ("ntypes", C.c_int),
@@ -59,6 +76,7 @@ class EngineConfig(C.Structure):
         ("gravity", C.c_double * 3), ("gravity_mask", C.c_int),
         ("procgrid", C.c_int * 3), ("rank", C.c_int), ("sort", C.c_int),
         ("kernel_path", C.c_int),
+        ("mp", C.POINTER(EngineMpConfig)),
     ]
 
 
@@ -129,6 +147,9 @@ EXPORTS = {
     "sph_engine_sync": (_i, [_vp]),
     "sph_engine_pair_passes": (_i, [_vp, _i]),
     "sph_engine_rebuild_passes": (_i, [_vp, _i]),
+    "sph_engine_set_atoms_multiphase": (_i, [_vp, _dp, _vp, _vp]),
+    "sph_engine_phase_change": (_i, [_vp, _vp, _i, _i]),
+    "sph_engine_get_atoms_multiphase": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 
@@ -332,7 +353,7 @@ def _pair_table(dst, tab, ntypes):
 def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every=10,
                 rhosum=None, tait=None, heat=None, gravity=(0.0, 0.0, 0.0),
                 stationary_mask=0, sort=1, procgrid=(1, 1, 1), rank=0,
-                kernel_path=0, gravity_mask=0) -> EngineConfig:
+                kernel_path=0, gravity_mask=0, mp=None) -> EngineConfig:
     """kernel_path: 0 = the production pair passes (block-staged LDS unions + 16-bit slot
     rows; bench.py's path), 1 = the row path (row2 gathers over strided global lists).
     rhosum = dict(nstep, cut); tait = dict(rho0, c0, visc, cut, morris[, B]);
@@ -368,7 +389,48 @@ def make_config(dim, ntypes, boxlo, boxhi, periodic, mass, skin, dt, neigh_every
         c.heat_on = 1
         _pair_table(c.heat_alpha, heat["alpha"], ntypes)
         _pair_table(c.heat_cut, heat["cut"], ntypes)
+    if mp is not None:
+        m = mp_config(ntypes, **mp)
+        c.mp = C.pointer(m)
+        c._mp_keep = m  # (the engine copies it at create)
     return c
+
+
+def mp_config(ntypes, rhosum_nstep=1, rhosum_cut=None, cg_nstep=1, cg_alpha=None, cg_cut=None,
+              rho0=None, c0=None, gamma=None, rbg=None, visc=None, tait_cut=None, st_cut=None,
+              heat_alpha=None, heat_cut=None, heat_fixflag=None, heat_tc=None) -> EngineMpConfig:
+    """The multiphase stack: tables (ntypes+1, ntypes+1), per-type arrays (ntypes+1); a style
+    is on when its cut table is given (rhosum/colorgradient also need nstep > 0)."""
+    m = EngineMpConfig()
+    if rhosum_cut is not None and rhosum_nstep > 0:
+        m.rhosum_nstep = int(rhosum_nstep)
+        _pair_table(m.rhosum_cut, rhosum_cut, ntypes)
+    if cg_cut is not None and cg_nstep > 0:
+        m.cg_nstep = int(cg_nstep)
+        _pair_table(m.cg_cut, cg_cut, ntypes)
+        _pair_table(m.cg_alpha, cg_alpha, ntypes)
+    if tait_cut is not None:
+        m.tait_on = 1
+        for t in range(ntypes + 1):
+            m.rho0[t], m.soundspeed[t] = float(rho0[t]), float(c0[t])
+            m.gamma[t], m.rbackground[t] = float(gamma[t]), float(rbg[t])
+        _pair_table(m.tait_visc, visc, ntypes)
+        _pair_table(m.tait_cut, tait_cut, ntypes)
+    if st_cut is not None:
+        m.st_on = 1
+        _pair_table(m.st_cut, st_cut, ntypes)
+    if heat_cut is not None:
+        m.heat_on = 1
+        _pair_table(m.heat_alpha, heat_alpha, ntypes)
+        _pair_table(m.heat_cut, heat_cut, ntypes)
+        if heat_tc is not None:
+            _pair_table(m.heat_tc, heat_tc, ntypes)
+        if heat_fixflag is not None:
+            ff = np.asarray(heat_fixflag)
+            for i in range(ntypes + 1):
+                for j in range(ntypes + 1):
+                    m.heat_fixflag[i * (SPH_MAXTYPES + 1) + j] = int(ff[i, j])
+    return m
 
 
 def comm_uid() -> bytes:
@@ -420,6 +482,33 @@ class Engine:
         e = None if e is None else np.ascontiguousarray(e, dtype=np.float64)
         cv = None if cv is None else np.ascontiguousarray(cv, dtype=np.float64)
         _chk(self.L.sph_engine_set_atoms(self.h, x.shape[0], x, v, t, rho, _ptr(e), _ptr(cv)))
+
+    def set_atoms_multiphase(self, rmass, cv=None, cg=None):
+        rmass = np.ascontiguousarray(rmass, dtype=np.float64)
+        cv = None if cv is None else np.ascontiguousarray(cv, dtype=np.float64)
+        cg = None if cg is None else np.ascontiguousarray(cg, dtype=np.float64)
+        _chk(self.L.sph_engine_set_atoms_multiphase(self.h, rmass, _ptr(cv), _ptr(cg)))
+
+    def phase_change(self, Tc, Tt, Hwv, dr, to_mass, cutoff, from_type, to_type, nevery=1,
+                     seed=123456, prob=0.0, energy_chance=0, rate=0.0, maxattempt=10):
+        """fix phase_change Tc Tt Hwv dr mass cutoff from to nevery seed prob|ENERGY rate."""
+        p = PhaseChangeParams()
+        p.Tc, p.Tt, p.Hwv, p.dr, p.to_mass, p.cutoff = Tc, Tt, Hwv, dr, to_mass, cutoff
+        p.from_type, p.to_type = from_type, to_type
+        p.energy_chance, p.change_chance, p.rate = energy_chance, prob, rate
+        p.maxattempt = maxattempt
+        _chk(self.L.sph_engine_phase_change(self.h, C.byref(p), nevery, seed))
+
+    def get_atoms_multiphase(self):
+        n = self.nlocal
+        out = dict(rmass=np.zeros(n), cv=np.zeros(n), cg=np.zeros((n, 3)), vest=np.zeros((n, 3)),
+                   type=np.zeros(n, dtype=np.int32))
+        ni = C.c_int64(0)
+        _chk(self.L.sph_engine_get_atoms_multiphase(
+            self.h, out["rmass"].ctypes.data, out["cv"].ctypes.data, out["cg"].ctypes.data,
+            out["vest"].ctypes.data, out["type"].ctypes.data, C.byref(ni)))
+        out["ninserted"] = ni.value
+        return out
 
     def setup(self):
         _chk(self.L.sph_engine_setup(self.h))

@@ -300,8 +300,7 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
       for (int p = lo + sub; p < hi; p += TPR) {
         const int pw = p - p0;
         const double2 cxy = s_cxy[pw];
-        const double dx = xi.x - cxy.x, dy = xi.y - cxy.y, dz = xi.z - s_cz[pw];
-        const double rsq = dx * dx + dy * dy + dz * dz;
+        const double rsq = rsq_ref(xi.x - cxy.x, xi.y - cxy.y, xi.z - s_cz[pw]);
         if (rsq <= (NT1 ? cns1 : crow[s_ct[pw]]) && s_cid[pw] != row) {
           atomicOr(&s_bm[r][p >> 5], 1u << (p & 31));
           cntr++;

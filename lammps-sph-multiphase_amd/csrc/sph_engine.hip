@@ -20,6 +20,8 @@
 #include "sph_dispatch.h"
 #include "sph_blk_kernels.h"
 #include "sph_engine_kernels.h"
+#include "sph_engine_mp.h"
+#include "sph_pc.h"
 #include "sph_row2_kernels.h"
 #include "sph_util.h"
 
@@ -113,6 +115,21 @@ struct sph_engine {
   double cutneighmax = 0.0, cutghost = 0.0;
   StepConst sc{};
   int force_mode = 0;  // M_TAIT | M_HEAT
+
+  // multiphase stack (cfg.mp, sph_engine_mp.h): per-atom rmass, cv, colorgradient of owned
+  // atoms and ghosts, and the ghosts' v (comm vel yes)
+  bool mp = false;
+  sph_engine_mp_config mpc{};
+  MpCoefs hm{};
+  MpCoefs *dm = nullptr;
+  DBuf<double> rm, cvv, rho_tmp, dmass, xbuf, xbuf2, rhoS, rhoF;
+  DBuf<double4> cg, cgS, cgF;
+  // fix phase_change (one brick): parameters, stream state, next call, atoms created
+  bool pc = false;
+  sph_phasechange_params pcp{};
+  int pc_nevery = 1, pc_seed = 0;
+  int64_t pc_next = 1, pc_inserted = 0;
+  int tag_next = 0;  // tag of the next created atom (atom->tag_extend on one brick)
 
   int nlocal = 0, nghost = 0;
   // brick decomposition (CommBrick): this brick's grid location, face neighbours, swaps
@@ -255,6 +272,21 @@ struct sph_engine {
     vr.reserve(nall, keep, s);
     en.reserve(nall, keep, s);
     ty.reserve(nall, keep, s);
+    if (mp) {
+      vel.reserve(nall, keep, s);
+      rm.reserve(nall, keep, s);
+      cvv.reserve(nall, keep, s);
+      cg.reserve(nall, keep, s);
+    }
+  }
+  // extra multiphase fields: atoms src[0..n) (nullptr: 0..n) -> xbuf -> atoms first..
+  void mpx_copy(int n, const int *src, int first, DBuf<double> &buf) {
+    if (!mp || n <= 0) return;
+    buf.reserve((size_t)MPX * n, false, s);
+    hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(n)), dim3(BLK), 0, s, n, src, vel.p, rm.p, cvv.p,
+                       cg.p, buf.p);
+    hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
+                       first, buf.p, vel.p, rm.p, cvv.p, cg.p);
   }
   bool nt1() const { return cfg.ntypes == 1; }
 
@@ -319,6 +351,11 @@ struct sph_engine {
     SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, n, 0, kb, s));
     // twins of equal capacity: the swaps below then never reallocate (a growing twin would
     // cost a hipMalloc + a synchronising hipFree at every rebuild)
+    if (mp) {  // the extra fields in the new order, packed before the permutation
+      xbuf.reserve((size_t)MPX * n, false, s);
+      hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, vel.p, rm.p,
+                         cvv.p, cg.p, xbuf.p);
+    }
     xf2.reserve_exact(xf.cap);
     vr2.reserve_exact(vr.cap);
     en2.reserve_exact(en.cap);
@@ -333,6 +370,9 @@ struct sph_engine {
     std::swap(ty, ty2);
     std::swap(vel, vel2);
     std::swap(tag, tag2);
+    if (mp)
+      hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
+                         0, xbuf.p, vel.p, rm.p, cvv.p, cg.p);
   }
 
   // kernel_path 0: block-staged passes (production; the row path takes over for a build
@@ -448,9 +488,42 @@ struct sph_engine {
                              (const BorderRec *)(cbr.p + (dir ? ro : 0)), xf.p, vr.p, en.p,
                              ty.p);
       }
+      if (mp) mpx_swap_pair(a, b);
       nall += nr;
     }
     nghost = nall - nlocal;
+  }
+
+  // the extra multiphase fields of a dimension's two swaps (pack_border_vel / pack_comm_vel
+  // of atom_vec_meso_multiphase.cpp): lists -> the peers -> firstrecv..
+  void mpx_swap_pair(Swap &a, Swap &b) {
+    const size_t rec = MPX * sizeof(double);
+    const size_t sa = (size_t)a.nsend * rec, sb = (size_t)b.nsend * rec;
+    const size_t ra = (size_t)a.nrecv * rec, rb = (size_t)b.nrecv * rec;
+    const size_t so = (sa + 255) & ~(size_t)255, ro = (ra + 255) & ~(size_t)255;
+    cbs.reserve(std::max<size_t>(so + sb, 1), true, s);
+    cbr.reserve(std::max<size_t>(ro + rb, 1), true, s);
+    if (a.nsend)
+      hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(a.nsend)), dim3(BLK), 0, s, a.nsend, a.list.p,
+                         vel.p, rm.p, cvv.p, cg.p, (double *)cbs.p);
+    if (b.nsend)
+      hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(b.nsend)), dim3(BLK), 0, s, b.nsend, b.list.p,
+                         vel.p, rm.p, cvv.p, cg.p, (double *)(cbs.p + so));
+    if (a.remote) {
+      tr->exchange2(cbs.p, sa, a.sendproc, cbr.p, ra, a.recvproc, cbs.p + so, sb, b.sendproc,
+                    cbr.p + ro, rb, b.recvproc, s);
+    } else {
+      if (ra) SPH_HIP_TRY(hipMemcpyAsync(cbr.p, cbs.p, ra, hipMemcpyDeviceToDevice, s));
+      if (rb) SPH_HIP_TRY(hipMemcpyAsync(cbr.p + ro, cbs.p + so, rb, hipMemcpyDeviceToDevice, s));
+    }
+    if (a.nrecv)
+      hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(a.nrecv)), dim3(BLK), 0, s, a.nrecv,
+                         (const int *)nullptr, a.firstrecv, (const double *)cbr.p, vel.p, rm.p,
+                         cvv.p, cg.p);
+    if (b.nrecv)
+      hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(b.nrecv)), dim3(BLK), 0, s, b.nrecv,
+                         (const int *)nullptr, b.firstrecv, (const double *)(cbr.p + ro), vel.p,
+                         rm.p, cvv.p, cg.p);
   }
 
   // Per-step forward traffic, one dimension at a time: the two swaps of a dimension send
@@ -492,6 +565,31 @@ struct sph_engine {
           hipLaunchKernelGGL(k_unpack_forward, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s,
                              sw.nrecv, sw.firstrecv, (const double *)buf, xf.p, vr.p, en.p);
         });
+    if (mp)
+      for (int k = 0; k + 1 < nswap; k += 2) mpx_swap_pair(swaps[k], swaps[k + 1]);
+  }
+
+  // comm->reverse_comm_fix of one per-atom double (fix phase_change's dmass)
+  void reverse1(double *a) {
+    if (!multi()) {
+      if (nghost)
+        hipLaunchKernelGGL(k_reverse1, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal,
+                           gowner.p, a);
+      return;
+    }
+    for (int k = nswap - 1; k >= 0; k--) {
+      Swap &sw = swaps[k];
+      cbs.reserve((size_t)(sw.nrecv > 0 ? sw.nrecv : 1) * sizeof(double), true, s);
+      cbr.reserve((size_t)(sw.nsend > 0 ? sw.nsend : 1) * sizeof(double), true, s);
+      if (sw.nrecv)
+        hipLaunchKernelGGL(k_pack_rev1, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s, sw.nrecv,
+                           sw.firstrecv, a, (double *)cbs.p);
+      swap_move(sw.remote, (size_t)sw.nrecv * sizeof(double), sw.recvproc,
+                (size_t)sw.nsend * sizeof(double), sw.sendproc);
+      if (sw.nsend)
+        hipLaunchKernelGGL(k_unpack_rev1, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                           sw.list.p, (const double *)cbr.p, a);
+    }
   }
 
   // comm->forward_comm_pair of sph/rhosum: rho (+ the EOS term)
@@ -542,6 +640,12 @@ struct sph_engine {
       if (nl)
         hipLaunchKernelGGL(k_pack_mig, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, xf.p,
                            vr.p, vel.p, en.p, ty.p, tag.p, (MigRec *)cbs.p);
+      if (mp && nl) {  // the leavers' extra fields, then the stayers' compacted
+        xbuf.reserve((size_t)MPX * nl, false, s);
+        hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, vel.p,
+                           rm.p, cvv.p, cg.p, xbuf.p);
+        mpx_copy(nst, sel2.p, 0, xbuf2);
+      }
       if (nl) {  // compact the staying atoms to the front (order kept)
         DBuf<unsigned char> keep;
         keep.reserve((size_t)(nst > 0 ? nst : 1) * sizeof(MigRec));
@@ -565,6 +669,11 @@ struct sph_engine {
         cbr.reserve((size_t)(nr > 0 ? nr : 1) * sizeof(MigRec));
         tr->exchange(cbs.p, (size_t)nl * sizeof(MigRec), dest, cbr.p, (size_t)nr * sizeof(MigRec),
                      src, s);
+        if (mp) {
+          xbuf2.reserve((size_t)MPX * (nr > 0 ? nr : 1), false, s);
+          tr->exchange((unsigned char *)xbuf.p, (size_t)nl * MPX * sizeof(double), dest,
+                       (unsigned char *)xbuf2.p, (size_t)nr * MPX * sizeof(double), src, s);
+        }
         if (nr == 0) continue;
         flags.reserve(nr);
         hipLaunchKernelGGL(k_flag_mine, dim3(blocks(nr)), dim3(BLK), 0, s, nr, d, sublo[d],
@@ -576,6 +685,9 @@ struct sph_engine {
         tag.reserve((size_t)nlocal + nm, true, s);
         hipLaunchKernelGGL(k_gather_mig, dim3(blocks(nm)), dim3(BLK), 0, s, nm, sel2.p,
                            (const MigRec *)cbr.p, nlocal, xf.p, vr.p, vel.p, en.p, ty.p, tag.p);
+        if (mp)
+          hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(nm)), dim3(BLK), 0, s, nm, sel2.p,
+                             nlocal, (const double *)xbuf2.p, vel.p, rm.p, cvv.p, cg.p);
         nlocal += nm;
       }
     }
@@ -623,6 +735,7 @@ struct sph_engine {
         gimg.reserve((size_t)nall + ns - nlocal, true, s);
         hipLaunchKernelGGL(k_append_ghosts, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sel.p,
                            nlocal, nall, d, pbc, shift, xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p);
+        mpx_copy(ns, sel.p, nall, xbuf);
         nall += ns;
       }
     }
@@ -870,6 +983,7 @@ struct sph_engine {
   // from the bins (no global-index list on a plain rebuild); the row path's strided list
   // if a block overflows its LDS image.
   void build_all(bool need_csr) {
+    need_csr = need_csr || mp;  // (the multiphase passes walk the CSR full and half lists)
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
     if (multi()) exchange_multi();
     if (cfg.sort) sort_owned();
@@ -877,6 +991,13 @@ struct sph_engine {
     bin_q();
     blk = false;
     if (need_csr || !want_blk()) list_q(need_csr);
+    if (mp) {  // the half list's orientation of every pair, as of this build
+      if (nlocal)
+        hipLaunchKernelGGL(k_mp_orient, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, nlocal,
+                           off.p, nbr.p, xf.p);
+      ov_ready = false;
+      return;
+    }
     if (want_blk()) {
       blk = build_blk();
       if (blk && !need_csr) {
@@ -972,6 +1093,7 @@ struct sph_engine {
     Scope t(this, T_COMM);
     hipLaunchKernelGGL(k_forward, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal, box,
                        gowner.p, gimg.p, xf.p, vr.p, en.p);
+    mpx_copy(nghost, gowner.p, nlocal, xbuf);
   }
 
   RowArgs row_args() {
@@ -1030,6 +1152,10 @@ struct sph_engine {
   // list: block path, row path (row2 kernels), or the generic CSR kernels for a list past
   // the row2 kernels' 32-bit offsets.  The setup step's force pass walks the half list.
   void pair_compute(bool do_rhosum, bool setup = false) {
+    if (mp) {
+      pair_compute_mp();
+      return;
+    }
     const int nall = nlocal + nghost;
     bool tight = false;
     if (do_rhosum) {
@@ -1158,6 +1284,227 @@ struct sph_engine {
     hnbr.release();
   }
 
+  // ---- multiphase stack -------------------------------------------------------------
+  static dim3 mp_rows(int rows) { return dim3((unsigned)(((long long)rows * 8 + 255) / 256)); }
+  // hybrid/overlay of bubble.lmp:57-73 in order: rhosum/multiphase and colorgradient over
+  // the full list (owned rows; no forward comm of either, A.6-1), then taitwater/multiphase,
+  // surfacetension and heatconduction/phasechange fused in one gather over the full list,
+  // each pair in its half-list orientation (k_mp_gather: the reference's Newton-3 scatter +
+  // reverse comm, without atomics or comm)
+  void pair_compute_mp() {
+    const int n = nlocal, nall = nlocal + nghost;
+    fo.reserve(n > 0 ? n : 1, true, s);
+    de.reserve(n > 0 ? n : 1, true, s);
+    if (n == 0) return;
+    MpArgs a{};
+    a.inum = n;
+    a.nlocal = n;
+    a.newton = 1;
+    a.dim = cfg.dim;
+    a.ilist = nullptr;  // (rows = owned atoms)
+    a.off = off.p;
+    a.nbr = nbr.p;
+    a.xf = xf.p;
+    a.vr = vr.p;
+    a.ty = ty.p;
+    a.rm = rm.p;
+    a.en = en.p;
+    a.cv = cvv.p;
+    a.mc = dm;
+    // the stale version: rho and colorgradient as communicated (k_mp_gather)
+    rhoS.reserve(nall);
+    cgS.reserve(nall);
+    hipLaunchKernelGGL(k_mp_snap, dim3(blocks(nall)), dim3(BLK), 0, s, nall, vr.p, cg.p, rhoS.p,
+                       cgS.p);
+    const bool rdue = mpc.rhosum_nstep > 0 && step % mpc.rhosum_nstep == 0;
+    const bool cdue = mpc.cg_nstep > 0 && step % mpc.cg_nstep == 0;
+    {
+      Scope t(this, T_RHO);
+      if (rdue) {
+        rho_tmp.reserve(nall);
+        a.rho = rho_tmp.p;
+        hipLaunchKernelGGL(k_mp_rhosum<8>, mp_rows(n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mp_rho_store, dim3(blocks(n)), dim3(BLK), 0, s, n, rho_tmp.p, vr.p);
+      }
+      if (cdue) {
+        a.cg = cg.p;
+        hipLaunchKernelGGL(k_mp_colorgradient<8>, mp_rows(n), dim3(256), 0, s, a);
+      }
+    }
+    // the fresh version: the owned atoms' new values, forwarded to the ghosts
+    const double *rF = rhoS.p;
+    const double4 *cF = cgS.p;
+    if (rdue || cdue) {
+      Scope t(this, T_COMM);
+      rhoF.reserve(nall);
+      cgF.reserve(nall);
+      hipLaunchKernelGGL(k_mp_snap, dim3(blocks(n)), dim3(BLK), 0, s, n, vr.p, cg.p, rhoF.p,
+                         cgF.p);
+      forward_fresh();
+      rF = rhoF.p;
+      cF = cgF.p;
+    }
+    Scope t(this, T_TAIT);
+    if (!mpc.tait_on && !mpc.st_on)
+      SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, n * sizeof(double4), s));
+    if (!mpc.heat_on) SPH_HIP_TRY(hipMemsetAsync(de.p, 0, n * sizeof(double), s));
+    MpArgs h = a;
+    h.vel = vel.p;
+    h.rhoS = rhoS.p;
+    h.rhoF = rF;
+    h.cgS = cgS.p;
+    h.cgF = cF;
+    h.fo = fo.p;
+    h.de = de.p;
+    const int sel = (mpc.tait_on ? 1 : 0) | (mpc.st_on ? 2 : 0) | (mpc.heat_on ? 4 : 0);
+    switch (sel) {
+#define SPH_MPG(k, T, S, H) \
+  case k: hipLaunchKernelGGL((k_mp_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h); break;
+      SPH_MPG(1, true, false, false)
+      SPH_MPG(2, false, true, false)
+      SPH_MPG(3, true, true, false)
+      SPH_MPG(4, false, false, true)
+      SPH_MPG(5, true, false, true)
+      SPH_MPG(6, false, true, true)
+      SPH_MPG(7, true, true, true)
+#undef SPH_MPG
+      default: break;
+    }
+  }
+
+  // rhoF / cgF of the ghosts from their owners (the values the reference's half-list pass
+  // uses for a pair evaluated in the owner's row, k_mp_gather)
+  void forward_fresh() {
+    if (!multi()) {
+      if (nghost)
+        hipLaunchKernelGGL(k_mp_fwd_fresh, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, nlocal,
+                           gowner.p, rhoF.p, cgF.p);
+      return;
+    }
+    forward_dims(
+        4 * sizeof(double),
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_mp_pack_fresh, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
+                             sw.list.p, rhoF.p, cgF.p, (double *)buf);
+        },
+        [&](Swap &sw, unsigned char *buf) {
+          hipLaunchKernelGGL(k_mp_unpack_fresh, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s,
+                             sw.nrecv, sw.firstrecv, (const double *)buf, rhoF.p, cgF.p);
+        });
+  }
+
+  // ordered indices i in [0, n) with flag[i] != 0 (int flags) -> out; host sync
+  int select_flagged_i(const int *flag, int n, DBuf<int> &out) {
+    out.reserve(n > 0 ? n : 1);
+    nsel.reserve(1);
+    if (n == 0) return 0;
+    hipcub::CountingInputIterator<int> it(0);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flag, out.p, nsel.p, n, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flag, out.p, nsel.p, n, s));
+    return read_scalar(nsel.p);
+  }
+
+  // FixPhaseChange::pre_exchange (fix_phase_change.cpp:167-352) on the last build's full
+  // list, owned atoms as integrated, ghosts as last communicated; the rebuild follows
+  void phase_change() {
+    Scope t(this, T_NEIGH);
+    const int n = nlocal, nall = nlocal + nghost;
+    if (n == 0) return;
+    sph_phasechange_params p = pcp;
+    for (int k = 0; k < 3; k++) {
+      p.sublo[k] = sublo[k];
+      p.subhi[k] = subhi[k];
+      p.boxhi[k] = box.hi[k];
+      p.top[k] = myloc[k] == pg[k] - 1;
+    }
+    const PcDev pd{cfg.dim, p.from_type, p.to_type, p.Tc, p.to_mass, p.cutoff};
+    DBuf<int> flag, cand, otag, rows, idx;
+    DBuf<double> rec, gat, Wd, vals, nrec;
+    flag.reserve(n);
+    hipLaunchKernelGGL(k_pc_flags, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
+                       ty.p, en.p, cvv.p, pd, flag.p);
+    const int ncand = select_flagged_i(flag.p, n, cand);
+    if (ncand == 0) return;  // (dmass 0: the finish loop leaves rmass and e as they are)
+    rec.reserve((size_t)8 * ncand);
+    gat.reserve((size_t)9 * ncand);
+    otag.reserve(ncand);
+    hipLaunchKernelGGL(k_pc_candidates<8>, mp_rows(ncand), dim3(256), 0, s, ncand, cand.p,
+                       (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p, 4,
+                       ty.p, rm.p, pd, rec.p);
+    hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
+                       vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
+    std::vector<int> hc(ncand), ht(ncand);
+    std::vector<double> hr((size_t)8 * ncand), hg((size_t)9 * ncand);
+    SPH_HIP_TRY(hipMemcpyAsync(hc.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(ht.data(), otag.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(hr.data(), rec.p, hr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(hg.data(), gat.p, hg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    // the reference meets the candidates in its atom order: tag order on one process
+    std::vector<int> ord(ncand);
+    for (int k = 0; k < ncand; k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return ht[a] < ht[b]; });
+    std::vector<PcCand> cands(ncand);
+    for (int q = 0; q < ncand; q++) {
+      const int k = ord[q];
+      PcCand &c = cands[q];
+      const double *g = &hg[(size_t)9 * k];
+      for (int d = 0; d < 3; d++) {
+        c.x[d] = g[d];
+        c.cg[d] = g[3 + d];
+      }
+      c.e = g[6];
+      c.cv = g[7];
+      c.rho = g[8];
+      for (int d = 0; d < 8; d++) c.rec[d] = hr[(size_t)8 * k + d];
+    }
+    std::vector<int> ins_k;
+    std::vector<double> ins_rec;
+    pc_replay(p, cfg.dim, pc_seed, cands, ins_k, ins_rec);
+    const int nins = (int)ins_k.size();
+    if (nins == 0) return;
+    std::vector<int> hidx(nins);
+    std::vector<double> hval(nins), hW(nins);
+    for (int q = 0; q < nins; q++) {
+      const int k = ord[ins_k[q]];
+      hidx[q] = hc[k];  // the candidate's row = its atom (identity row list)
+      hval[q] = ins_rec[(size_t)13 * q + 9];
+      hW[q] = hr[(size_t)8 * k + 1];
+    }
+    idx.reserve(nins);
+    vals.reserve(nins);
+    Wd.reserve(nins);
+    nrec.reserve((size_t)13 * nins);
+    dmass.reserve(nall);
+    SPH_HIP_TRY(hipMemcpyAsync(idx.p, hidx.data(), nins * sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(vals.p, hval.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(Wd.p, hW.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(nrec.p, ins_rec.data(), ins_rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipMemsetAsync(dmass.p, 0, nall * sizeof(double), s));
+    // e_i = (e_i - Hwv)/2 of the atoms that changed phase, the donors' dmass, its reverse
+    // comm, rmass -= dmass and e renormalised, then the new atoms
+    hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
+    hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
+                       (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p);
+    reverse1(dmass.p);
+    hipLaunchKernelGGL(k_pc_finish, dim3(blocks(n)), dim3(BLK), 0, s, n, dmass.p, rm.p, en.p);
+    ensure_atoms((size_t)n + nins, true);  // (over the ghost slots: the rebuild follows)
+    vel.reserve((size_t)n + nins, true, s);
+    tag.reserve((size_t)n + nins, true, s);
+    fo.reserve((size_t)n + nins, true, s);
+    de.reserve((size_t)n + nins, true, s);
+    hipLaunchKernelGGL(k_pc_append, dim3(blocks(nins)), dim3(BLK), 0, s, nins, nrec.p, n,
+                       p.to_type, tag_next, xf.p, vr.p, vel.p, en.p, rm.p, cvv.p, cg.p, ty.p,
+                       tag.p, fo.p, de.p);
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // (the scratch buffers are freed on return)
+    nlocal = n + nins;
+    nghost = 0;
+    tag_next += nins;
+    pc_inserted += nins;
+  }
+
   bool rhosum_due() const {
     return cfg.rhosum_nstep > 0 && (step % cfg.rhosum_nstep) == 0;
   }
@@ -1186,13 +1533,18 @@ struct sph_engine {
         Scope t(this, T_INT);
         if (k == 0)
           hipLaunchKernelGGL(k_initial_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s,
-                             nlocal, sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
+                             nlocal, sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p, rm.p);
         else
           hipLaunchKernelGGL(k_final_initial, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
-                             sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p);
+                             sc, xf.p, vr.p, en.p, ty.p, vel.p, fo.p, de.p, rm.p);
       }
       const int every = cfg.neigh_every > 0 ? cfg.neigh_every : 1;
-      if ((step - last_build) % every == 0) {
+      const bool pc_due = pc && step == pc_next;  // (the fix forces this reneighbor)
+      if (pc_due) {
+        phase_change();
+        pc_next += pc_nevery;
+      }
+      if (pc_due || (step - last_build) % every == 0) {
         rebuild();
         last_build = (int)step;
         pair_compute(rhosum_due());
@@ -1207,11 +1559,63 @@ struct sph_engine {
     if (nsteps > 0) {
       Scope t(this, T_INT);
       hipLaunchKernelGGL(k_final_integrate, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, sc,
-                         vr.p, en.p, ty.p, vel.p, fo.p, de.p);
+                         vr.p, en.p, ty.p, vel.p, fo.p, de.p, rm.p);
     }
     SPH_HIP_TRY(hipGetLastError());
   }
 };
+
+// MpCoefs of the multiphase stack from the engine's (SPH_MAXTYPES+1)^2 tables (upper
+// triangle mirrored like init_one; the coeff() formulas as sph_multiphase.hip's), and the
+// stack's cutoffs into cutmax ((nt+1)^2, upper triangle)
+static void coef_mp(MpCoefs &m, const sph_engine_mp_config &c, int dim, int nt,
+                    std::vector<double> &cutmax) {
+  const int n1 = nt + 1, M1 = SPH_MAXTYPES + 1;
+  m = MpCoefs{};
+  m.ntypes = nt;
+  m.dim = dim;
+  auto up = [&](const double *t, int i, int j) { return j >= i ? t[i * M1 + j] : t[j * M1 + i]; };
+  auto upi = [&](const int *t, int i, int j) { return j >= i ? t[i * M1 + j] : t[j * M1 + i]; };
+  auto cut = [&](bool on, const double *t) {
+    if (!on) return;
+    for (int i = 0; i <= nt; i++)
+      for (int j = i; j <= nt; j++) cutmax[i * n1 + j] = std::max(cutmax[i * n1 + j], t[i * M1 + j]);
+  };
+  for (int i = 0; i <= nt; i++)
+    for (int j = 0; j <= nt; j++) {
+      const int k = i * n1 + j;
+      m.rcut[k] = up(c.rhosum_cut, i, j);
+      m.rcutsq[k] = m.rcut[k] * m.rcut[k];
+      m.calpha[k] = up(c.cg_alpha, i, j);
+      m.ccut[k] = up(c.cg_cut, i, j);
+      m.ccutsq[k] = m.ccut[k] * m.ccut[k];
+      m.tvisc[k] = up(c.tait_visc, i, j);
+      m.tcut[k] = up(c.tait_cut, i, j);
+      m.tcutsq[k] = m.tcut[k] * m.tcut[k];
+      m.scut[k] = up(c.st_cut, i, j);
+      m.scutsq[k] = m.scut[k] * m.scut[k];
+      m.halpha[k] = up(c.heat_alpha, i, j);
+      m.hcut[k] = up(c.heat_cut, i, j);
+      m.hcutsq[k] = m.hcut[k] * m.hcut[k];
+      m.htc[k] = up(c.heat_tc, i, j);
+      m.hfix[k] = upi(c.heat_fixflag, i, j);
+    }
+  if (c.tait_on)
+    for (int t = 1; t <= nt; t++) {
+      SPH_REQUIRE(c.gamma[t] != 0.0 && c.rho0[t] != 0.0, SPH_HIP_EINVAL,
+                  "type %d: gamma and rho0 must be non-zero", t);
+      m.rho0[t] = c.rho0[t];
+      m.gamma[t] = c.gamma[t];
+      m.rbg[t] = c.rbackground[t];
+      // B = c^2 rho0 / gamma, pair_sph_taitwater_multiphase.cpp:243-250
+      m.B[t] = c.soundspeed[t] * c.soundspeed[t] * c.rho0[t] / c.gamma[t];
+    }
+  cut(c.rhosum_nstep > 0, c.rhosum_cut);
+  cut(c.cg_nstep > 0, c.cg_cut);
+  cut(c.tait_on != 0, c.tait_cut);
+  cut(c.st_on != 0, c.st_cut);
+  cut(c.heat_on != 0, c.heat_cut);
+}
 
 extern "C" {
 
@@ -1267,6 +1671,14 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
       for (size_t k = 0; k < cutmax.size(); k++) cutmax[k] = std::max(cutmax[k], tmpc[k]);
       e->force_mode |= M_HEAT;
     }
+    if (cfg->mp) {
+      SPH_REQUIRE(cfg->rhosum_nstep == 0 && !cfg->tait_on && !cfg->heat_on, SPH_HIP_EINVAL,
+                  "the multiphase stack replaces the single-phase styles (turn them off)");
+      e->mp = true;
+      e->mpc = *cfg->mp;
+      e->cfg.mp = nullptr;
+      coef_mp(e->hm, e->mpc, cfg->dim, nt, cutmax);
+    }
     // mirror upper triangle into a symmetric max-cut table (init_one semantics)
     for (int i = 1; i <= nt; i++)
       for (int j = 1; j < i; j++) cutmax[i * (nt + 1) + j] = cutmax[j * (nt + 1) + i];
@@ -1319,6 +1731,10 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     SPH_HIP_TRY(hipStreamCreateWithFlags(&e->s, hipStreamNonBlocking));
     SPH_HIP_TRY(hipMalloc(&e->dc, sizeof(Coefs)));
     SPH_HIP_TRY(hipMemcpy(e->dc, &e->hc, sizeof(Coefs), hipMemcpyHostToDevice));
+    if (e->mp) {
+      SPH_HIP_TRY(hipMalloc(&e->dm, sizeof(MpCoefs)));
+      SPH_HIP_TRY(hipMemcpy(e->dm, &e->hm, sizeof(MpCoefs), hipMemcpyHostToDevice));
+    }
     SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));
   } catch (...) {
     delete e;
@@ -1335,7 +1751,12 @@ int sph_engine_destroy(sph_engine *e) {
   if (e->s) (void)hipStreamSynchronize(e->s);
   if (e->s2) (void)hipStreamSynchronize(e->s2);
   for (auto *b : {&e->xf, &e->vr, &e->vel, &e->fo, &e->xf2, &e->vr2, &e->vel2, &e->xb}) b->release();
-  for (auto *b : {&e->en, &e->en2, &e->de}) b->release();
+  for (auto *b : {&e->en, &e->en2, &e->de, &e->rm, &e->cvv, &e->rho_tmp, &e->dmass, &e->xbuf,
+                  &e->xbuf2})
+    b->release();
+  for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
+  for (auto *b : {&e->cg, &e->cgS, &e->cgF}) b->release();
+  if (e->dm) (void)hipFree(e->dm);
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
                   &e->ccnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
@@ -1368,13 +1789,14 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   SPH_API_BEGIN
   SPH_REQUIRE(e && n >= 0 && (n == 0 || (x && v && type && rho)), SPH_HIP_EINVAL,
               "sph_engine_set_atoms: bad argument");
-  (void)cv;  // cv is carried only by the multiphase heat styles (not in this engine yet)
   SPH_HIP_TRY(hipSetDevice(e->device));
   for (int i = 0; i < n; i++)
     SPH_REQUIRE(type[i] >= 1 && type[i] <= e->cfg.ntypes, SPH_HIP_EINVAL,
                 "atom %d has type %d outside [1,%d]", i, type[i], e->cfg.ntypes);
   e->nlocal = n;
   e->nghost = 0;
+  e->tag_next = n;
+  e->pc_inserted = 0;
   e->ensure_atoms(n > 0 ? n : 1, false);
   e->vel.reserve(n > 0 ? n : 1);
   e->fo.reserve(n > 0 ? n : 1);
@@ -1401,8 +1823,108 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
     SPH_HIP_TRY(hipMemsetAsync(e->fo.p, 0, n * sizeof(double4), e->s));
     SPH_HIP_TRY(hipMemsetAsync(e->de.p, 0, n * sizeof(double), e->s));
   }
+  if (e->mp && n > 0) {  // per-type mass, cv (default 1, create_atom), colorgradient 0
+    std::vector<double> hm(n), hc(n);
+    for (int i = 0; i < n; i++) {
+      hm[i] = e->cfg.mass[type[i]];
+      hc[i] = cv ? cv[i] : 1.0;
+    }
+    SPH_HIP_TRY(hipMemcpyAsync(e->rm.p, hm.data(), n * sizeof(double), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->cvv.p, hc.data(), n * sizeof(double), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemsetAsync(e->cg.p, 0, n * sizeof(double4), e->s));
+  }
   SPH_HIP_TRY(hipStreamSynchronize(e->s));
   e->setup_done = false;
+  SPH_API_END
+}
+
+int sph_engine_set_atoms_multiphase(sph_engine *e, const double *rmass, const double *cv,
+                                    const double *cg) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && e->mp, SPH_HIP_EINVAL,
+              "sph_engine_set_atoms_multiphase: not a multiphase engine (cfg.mp)");
+  const int n = e->nlocal;
+  SPH_REQUIRE(n == 0 || rmass, SPH_HIP_EINVAL, "sph_engine_set_atoms_multiphase: NULL rmass");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  if (n == 0) return SPH_HIP_OK;
+  for (int i = 0; i < n; i++)
+    SPH_REQUIRE(rmass[i] > 0.0, SPH_HIP_EINVAL, "atom %d has rmass %g <= 0", i, rmass[i]);
+  std::vector<double> hc(n, 1.0);
+  std::vector<double4> hg(n, make_double4(0.0, 0.0, 0.0, 0.0));
+  for (int i = 0; i < n; i++) {
+    if (cv) hc[i] = cv[i];
+    if (cg) hg[i] = make_double4(cg[3 * i], cg[3 * i + 1], cg[3 * i + 2], 0.0);
+  }
+  SPH_HIP_TRY(hipMemcpyAsync(e->rm.p, rmass, n * sizeof(double), hipMemcpyHostToDevice, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(e->cvv.p, hc.data(), n * sizeof(double), hipMemcpyHostToDevice, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(e->cg.p, hg.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  e->setup_done = false;
+  SPH_API_END
+}
+
+int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int nevery,
+                            int seed) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && p, SPH_HIP_EINVAL, "sph_engine_phase_change: NULL argument");
+  SPH_REQUIRE(e->mp, SPH_HIP_EINVAL,
+              "fix phase_change needs atom_style meso/multiphase (a multiphase engine)");
+  SPH_REQUIRE(!e->multi(), SPH_HIP_EINVAL,
+              "sph_engine_phase_change: one brick only (new tags need a global tag_extend)");
+  SPH_REQUIRE(seed > 0, SPH_HIP_EINVAL, "Invalid seed for Park random # generator");
+  SPH_REQUIRE(nevery >= 1, SPH_HIP_EINVAL, "sph_engine_phase_change: nevery < 1");
+  SPH_REQUIRE(p->to_mass > 0.0 && p->maxattempt >= 1 && p->cutoff > 0.0, SPH_HIP_EINVAL,
+              "sph_engine_phase_change: bad parameters");
+  SPH_REQUIRE(p->from_type >= 1 && p->from_type <= e->cfg.ntypes && p->to_type >= 1 &&
+                  p->to_type <= e->cfg.ntypes,
+              SPH_HIP_EINVAL, "sph_engine_phase_change: type outside [1,%d]", e->cfg.ntypes);
+  e->pc = true;
+  e->pcp = *p;
+  e->pcp.dt = e->cfg.dt;
+  e->pc_nevery = nevery;
+  e->pc_seed = seed;
+  e->pc_next = e->step + 1;  // next_reneighbor = ntimestep + 1 (fix_phase_change.cpp:120)
+  SPH_API_END
+}
+
+int sph_engine_get_atoms_multiphase(sph_engine *e, double *rmass, double *cv, double *cg,
+                                    double *vest, int *type, int64_t *ninserted) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_get_atoms_multiphase: NULL engine");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  if (ninserted) *ninserted = e->pc_inserted;
+  const int n = e->nlocal;
+  if (n == 0) return SPH_HIP_OK;
+  std::vector<double> hm(n, 0.0), hc(n, 1.0);
+  std::vector<double4> hg(n, make_double4(0, 0, 0, 0)), hv(n);
+  std::vector<int> ht(n), hty(n);
+  if (e->mp) {
+    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), e->rm.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->cvv.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(hg.data(), e->cg.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  }
+  SPH_HIP_TRY(hipMemcpyAsync(hv.data(), e->vr.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hty.data(), e->ty.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  const bool local_order = e->multi() || e->global_tags;
+  for (int i = 0; i < n; i++) {
+    const int t = local_order ? i : ht[i];
+    SPH_REQUIRE(t >= 0 && t < n, SPH_HIP_ERUNTIME, "corrupt tag %d", t);
+    if (rmass) rmass[t] = e->mp ? hm[i] : e->cfg.mass[hty[i]];
+    if (cv) cv[t] = hc[i];
+    if (cg) {
+      cg[3 * t] = hg[i].x;
+      cg[3 * t + 1] = hg[i].y;
+      cg[3 * t + 2] = hg[i].z;
+    }
+    if (vest) {
+      vest[3 * t] = hv[i].x;
+      vest[3 * t + 1] = hv[i].y;
+      vest[3 * t + 2] = hv[i].z;
+    }
+    if (type) type[t] = hty[i];
+  }
   SPH_API_END
 }
 

@@ -21,7 +21,8 @@ static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restr
                                            const int *__restrict__ ty,
                                            double4 *__restrict__ vel,
                                            const double4 *__restrict__ fo,
-                                           const double *__restrict__ de) {
+                                           const double *__restrict__ de,
+                                           const double *__restrict__ rm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int t = ty[i];
@@ -32,7 +33,7 @@ static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restr
   if (!((sc.stationary_mask >> t) & 1)) {
     double4 x = xf[i];
     double4 v = vel[i];
-    const double dtfm = sc.dtf / sc.mass[t];
+    const double dtfm = sc.dtf / (rm ? rm[i] : sc.mass[t]);  // rmass if per-atom
     vv.x = v.x + 2.0 * dtfm * f.x;
     vv.y = v.y + 2.0 * dtfm * f.y;
     vv.z = v.z + 2.0 * dtfm * f.z;
@@ -53,14 +54,15 @@ static __global__ void k_final_integrate(int n, StepConst sc, double4 *__restric
                                          double *__restrict__ en, const int *__restrict__ ty,
                                          double4 *__restrict__ vel,
                                          const double4 *__restrict__ fo,
-                                         const double *__restrict__ de) {
+                                         const double *__restrict__ de,
+                                         const double *__restrict__ rm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int t = ty[i];
   const double4 f = fo[i];
   if (!((sc.stationary_mask >> t) & 1)) {
     double4 v = vel[i];
-    const double dtfm = sc.dtf / sc.mass[t];
+    const double dtfm = sc.dtf / (rm ? rm[i] : sc.mass[t]);  // rmass if per-atom
     v.x += dtfm * f.x;
     v.y += dtfm * f.y;
     v.z += dtfm * f.z;
@@ -78,7 +80,8 @@ static __global__ void k_final_initial(int n, StepConst sc, double4 *__restrict_
                                        double4 *__restrict__ vr, double *__restrict__ en,
                                        const int *__restrict__ ty, double4 *__restrict__ vel,
                                        const double4 *__restrict__ fo,
-                                       const double *__restrict__ de) {
+                                       const double *__restrict__ de,
+                                       const double *__restrict__ rm) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int t = ty[i];
@@ -93,7 +96,7 @@ static __global__ void k_final_initial(int n, StepConst sc, double4 *__restrict_
   if (!((sc.stationary_mask >> t) & 1)) {
     double4 x = xf[i];
     double4 v = vel[i];
-    const double dtfm = sc.dtf / sc.mass[t];
+    const double dtfm = sc.dtf / (rm ? rm[i] : sc.mass[t]);  // rmass if per-atom
     v.x += dtfm * f.x;      // final
     v.y += dtfm * f.y;
     v.z += dtfm * f.z;
@@ -479,8 +482,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
-      const double rsq = dx * dx + dy * dy + dz * dz;
+      const double rsq = rsq_ref(xi.x - xj[u].x, xi.y - xj[u].y, xi.z - xj[u].z);
       const bool hit = (p0 + lane + u * G < T) && (xj[u].w != di) &&
                        rsq <= (NT1 ? cns1 : crow[tj[u]]);
       if (FILL) {

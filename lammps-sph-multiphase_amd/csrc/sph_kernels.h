@@ -91,6 +91,15 @@ __host__ __device__ __forceinline__ int tpos(int q, int G, int pi) {
   return q - c + 4 * slot_lane(c % G, G, pi) + c / G;
 }
 
+// rsq in the reference's operation order and rounding (its x86-64 build has no FMA, so no
+// contraction: neigh_full.cpp:305-312), for the neighbour-list membership test
+// rsq <= cutneighsq -- bit-exact also for atoms on a lattice, whose distances tie with the
+// cutoff
+__device__ __forceinline__ double rsq_ref(double dx, double dy, double dz) {
+#pragma clang fp contract(off)
+  return dx * dx + dy * dy + dz * dz;
+}
+
 template <int G>
 __device__ __forceinline__ double group_sum(double v) {
 #pragma unroll

@@ -18,6 +18,11 @@
 
 namespace sph {
 
+// Engine full lists carry the half list's orientation of each pair, frozen at the build as
+// the reference's half list is (k_mp_orient), in bit 31 of the entry: mask with MP_NMASK
+// (LAMMPS' NEIGHMASK idiom).  Lists from the pair-style layer never set it.
+constexpr int MP_NMASK = 0x7fffffff;
+
 struct MpCoefs {
   int ntypes, dim;
   // rhosum/multiphase: h = cut[it][jt]
@@ -83,6 +88,12 @@ struct MpArgs {
   int rev;             // half list with its reverse list: j share gathered (k_mp_half REV)
   const int *roff, *rnbr;  // reverse half list: row j holds the atoms whose half row has j
   int nrows;               // reverse rows (nall with newton_pair, else nlocal)
+  // k_mp_gather: v of every atom, and rho / colorgradient in two versions -- S (stale: the
+  // values the atoms' ghost copies carry, i.e. before this step's rhosum / colorgradient)
+  // and F (fresh: after them, forwarded to the ghosts too)
+  const double4 *vel;
+  const double *rhoS, *rhoF;
+  const double4 *cgS, *cgF;
 };
 
 template <int G>
@@ -92,13 +103,13 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
   if (row >= a.inum) return;
   const MpCoefs *c = a.mc;
   const int nt1 = c->ntypes + 1;
-  const int i = a.ilist[row];
+  const int i = a.ilist ? a.ilist[row] : row;
   const double4 xi = a.xf[i];
   const int it = a.ty[i];
   const int dim = a.dim;
   double acc = 0.0;
   for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int j = a.nbr[k];
+    const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xf[j];
     const int jt = a.ty[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
@@ -189,13 +200,13 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
   if (row >= a.inum) return;
   const MpCoefs *c = a.mc;
   const int nt1 = c->ntypes + 1;
-  const int i = a.ilist[row];
+  const int i = a.ilist ? a.ilist[row] : row;
   const double4 xi = a.xf[i];
   const int it = a.ty[i];
   const double sigmai = a.vr[i].w / a.rm[i];
   double gx = 0.0, gy = 0.0, gz = 0.0;
   for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int j = a.nbr[k];
+    const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xf[j];
     const int jt = a.ty[j];
     const int p = it * nt1 + jt;
@@ -368,6 +379,120 @@ __global__ void __launch_bounds__(256) k_mp_half(MpArgs a) {
     a.fo[r].x += sx;
     a.fo[r].y += sy;
     a.fo[r].z += sz;
+  }
+}
+
+// The three half-list styles fused and gathered over the FULL list (the device-resident
+// engine): the reference evaluates each pair once, with the half list's row atom first
+// (half_from_full_newton: owned j if i < j, ghost j if above i in z, y, x), adds the value
+// to that atom and subtracts it from the other (Newton-3, then reverse comm for ghosts).
+// Here every owned atom walks its full row and evaluates each pair in that same
+// orientation -- F(i,j) when the pair is i's, F(j,i) when it is j's (or, for a ghost j, its
+// owner's image pair) -- adding or subtracting it: the same pair values, gather-only, no
+// atomics, no reverse comm.  With the stale-ghost quirk (ghosts keep their
+// comm-time rho and colorgradient) the reference's value of a pair depends on which side
+// is owned where it is evaluated: the pair's row atom uses its fresh values when owned, and
+// the other atom its fresh values when owned, stale ones when a ghost.  So for owned i and
+// neighbour j: owned j -> both fresh; ghost j in i's half row -> i fresh, j stale; ghost j
+// whose image pair belongs to j's owner (evaluated there with the owner fresh and i's ghost
+// copy stale) -> j fresh, i stale.  fo[i].xyz and de[i] of the owned rows are overwritten
+// (fo.w = drho = 0: none of the styles has a drho term).
+__device__ __forceinline__ bool mp_half_keep(int i, int j, int nlocal, const double4 &xi,
+                                             const double4 &xj) {
+  if (j < nlocal) return i < j;
+  if (xj.z < xi.z) return false;
+  if (xj.z == xi.z) {
+    if (xj.y < xi.y) return false;
+    if (xj.y == xi.y && xj.x < xi.x) return false;
+  }
+  return true;
+}
+// set bit 31 of the full-list entries whose pair the half list gives to the row atom
+static __global__ void k_mp_orient(int n, int nlocal, const int *__restrict__ off,
+                                   int *__restrict__ nbr, const double4 *__restrict__ xf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double4 xi = xf[i];
+  for (int k = off[i]; k < off[i + 1]; k++) {
+    const int j = nbr[k];
+    if (mp_half_keep(i, j, nlocal, xi, xf[j])) nbr[k] = j | ~MP_NMASK;
+  }
+}
+template <class T>
+__device__ __forceinline__ T mp_sel(bool c, const T &a, const T &b) {
+  return c ? a : b;
+}
+
+template <int G, bool TAIT, bool SURF, bool HEAT>
+__global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const MpCoefs *c = a.mc;
+  const int dim = a.dim;
+  const int i = a.ilist ? a.ilist[row] : row;
+  const double4 xi = a.xf[i], v4i = a.vel[i];
+  const int ti = a.ty[i];
+  const double mi = a.rm[i];
+  const double Ti = HEAT ? a.en[i] / a.cv[i] : 0.0;  // sph_energy2t
+  const double rFi = a.rhoF[i], rSi = a.rhoS[i];
+  const double4 cFi = SURF ? a.cgF[i] : make_double4(0, 0, 0, 0);
+  const double4 cSi = SURF ? a.cgS[i] : make_double4(0, 0, 0, 0);
+  double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
+  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+    const int jr = a.nbr[k];
+    const int j = jr & MP_NMASK;
+    const double4 xj = a.xf[j], v4j = a.vel[j];
+    const int tj = a.ty[j];
+    const double mj = a.rm[j];
+    const bool own = jr < 0;  // (bit 31: the pair is i's in the half list, k_mp_orient)
+    const bool gj = j >= a.nlocal;
+    const bool fi = !(gj && !own), fj = !gj || !own;  // fresh or stale values (see above)
+    const double rhoi = fi ? rFi : rSi;
+    const double rhoj = fj ? a.rhoF[j] : a.rhoS[j];
+    const double sg = own ? 1.0 : -1.0;
+    // the pair's row atom (p) and neighbour (q) in the half list
+    const double4 xp = mp_sel(own, xi, xj), xq = mp_sel(own, xj, xi);
+    const int tp = own ? ti : tj, tq = own ? tj : ti;
+    const double mp = own ? mi : mj, mq = own ? mj : mi;
+    const double rp = own ? rhoi : rhoj, rq = own ? rhoj : rhoi;
+    if (TAIT) {
+      const double4 vi = make_double4(v4i.x, v4i.y, v4i.z, rhoi);
+      const double4 vj = make_double4(v4j.x, v4j.y, v4j.z, rhoj);
+      double3 F;
+      if (mp_tait_pair(c, dim, xp, mp_sel(own, vi, vj), tp, mp, xq, mp_sel(own, vj, vi), tq, mq,
+                       F)) {
+        fx += sg * F.x;
+        fy += sg * F.y;
+        fz += sg * F.z;
+      }
+    }
+    if (SURF) {
+      const double4 ci = fi ? cFi : cSi;
+      const double4 cj = fj ? a.cgF[j] : a.cgS[j];
+      const double4 cp = mp_sel(own, ci, cj), cq = mp_sel(own, cj, ci);
+      double3 F;
+      if (mp_surf_pair(c, dim, xp, tp, mp / rp, cp, st_abs(dim, cp), xq, tq, mq / rq, cq, F)) {
+        fx += sg * F.x;
+        fy += sg * F.y;
+        fz += sg * F.z;
+      }
+    }
+    if (HEAT) {
+      const double Tj = a.en[j] / a.cv[j];
+      double d;
+      // de_p += deltaE m_q, de_q -= deltaE m_p (pair_sph_heatconduction_phasechange.cpp:132-136)
+      if (mp_heat_pair(c, dim, xp, tp, rp, own ? Ti : Tj, xq, tq, rq, own ? Tj : Ti, d))
+        dE += sg * d * mj;
+    }
+  }
+  fx = group_sum<G>(fx);
+  fy = group_sum<G>(fy);
+  fz = group_sum<G>(fz);
+  dE = group_sum<G>(dE);
+  if (lane == 0) {
+    if (TAIT || SURF) a.fo[i] = make_double4(fx, fy, fz, 0.0);
+    if (HEAT) a.de[i] = dE;
   }
 }
 

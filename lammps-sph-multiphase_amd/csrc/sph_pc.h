@@ -1,0 +1,258 @@
+// sph_pc.h -- fix phase_change (FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-352),
+// shared by the pair-style layer (sph_phasechange.hip) and the device-resident engine.
+//
+// Split by what the work is:
+//  * device, parallel over atoms: the candidate test (type == to_type, T = e/cv >= Tc),
+//    and for every candidate one walk of its full-list row giving isfromphasearound()
+//    (:538-563) and the quintic weights of the from_type donors with their weighted
+//    velocity sums (:233-289) -- everything that does not depend on the random stream;
+//  * host, sequential over the (few) candidates: the Park-Miller draws (RanPark::uniform,
+//    random_park.cpp:42-49), the insertion positions (create_newpos / create_newpos_simple,
+//    :466-520) and the sub-domain test (insert_one_atom, :425-456), which must consume the
+//    stream exactly in the reference's order;
+//  * device again: the mass taken from the donors (dmass[j] += to_mass w_j / W) for the
+//    candidates that did change phase, scattered with fp64 atomics onto owned and ghost j.
+// Every candidate is evaluated on the atoms as they were when pre_exchange began.  (The
+// reference creates each new atom at index nlocal inside the candidate loop, over the
+// first ghost slot, which later candidates' list walks then read, and create_atom zeroes
+// that slot's drho = dmass entry: with several insertions per call and a donor ghost in
+// that slot the reference's result depends on this aliasing.  Not reproduced; DESIGN.md.)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "../../include/sph_hip.h"
+#include "sph_mp_kernels.h"
+
+namespace sph {
+
+struct PcDev {
+  int dim, from_type, to_type;
+  double Tc, to_mass, cutoff;
+};
+
+// candidate flags over rows (ilist: row -> atom, nullptr = identity)
+static __global__ void k_pc_flags(int inum, const int *__restrict__ ilist,
+                                  const int *__restrict__ ty, const double *__restrict__ en,
+                                  const double *__restrict__ cv, PcDev p,
+                                  int *__restrict__ flag) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= inum) return;
+  const int i = ilist ? ilist[r] : r;
+  const double Ti = en[i] / cv[i];  // sph_energy2t
+  flag[r] = (!(Ti < p.Tc) && ty[i] == p.to_type) ? 1 : 0;
+}
+
+__device__ __forceinline__ double pc_w(int dim, double r) {
+  return quintic_w(dim, r);  // sph_kernel_quintic{2,3}d(sqrt(rsq)*cutoff), :247-251 (A.6-3)
+}
+
+// one record per candidate: {around, W, Sv[3], Svest[3]} over the candidate's list row;
+// vel holds v with vstride doubles per atom (3: packed xyz, 4: double4)
+template <int G>
+__global__ void __launch_bounds__(256)
+k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__ ilist,
+                const int *__restrict__ off, const int *__restrict__ nbr,
+                const double4 *__restrict__ xf, const double4 *__restrict__ vr,
+                const double *__restrict__ vel, int vstride, const int *__restrict__ ty,
+                const double *__restrict__ rm, PcDev p, double *__restrict__ rec) {
+  const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (k >= ncand) return;
+  const int row = cand[k];
+  const int i = ilist ? ilist[row] : row;
+  const double4 xi = xf[i];
+  const double cut2 = p.cutoff * p.cutoff;
+  int around = 0;
+  double W = 0.0, sv0 = 0.0, sv1 = 0.0, sv2 = 0.0, se0 = 0.0, se1 = 0.0, se2 = 0.0;
+  for (int q = off[row] + lane; q < off[row + 1]; q += G) {
+    const int j = nbr[q] & MP_NMASK;
+    if (ty[j] != p.from_type) continue;
+    const double4 xj = xf[j];
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    if (rsq_ref(dx, dy, dz) <= cut2) around = 1;  // (a decision: the reference's rounding)
+    if (rm[j] > 0.5 * p.to_mass) {
+      const double w = pc_w(p.dim, sqrt(rsq) * p.cutoff);
+      const double4 vj = vr[j];
+      const double *const v = vel + (size_t)vstride * j;
+      W += w;
+      sv0 += w * v[0];
+      sv1 += w * v[1];
+      sv2 += w * v[2];
+      se0 += w * vj.x;
+      se1 += w * vj.y;
+      se2 += w * vj.z;
+    }
+  }
+  around = group_sum_i<G>(around);
+  W = group_sum<G>(W);
+  sv0 = group_sum<G>(sv0);
+  sv1 = group_sum<G>(sv1);
+  sv2 = group_sum<G>(sv2);
+  se0 = group_sum<G>(se0);
+  se1 = group_sum<G>(se1);
+  se2 = group_sum<G>(se2);
+  if (lane == 0) {
+    double *o = rec + 8 * (size_t)k;
+    o[0] = around > 0 ? 1.0 : 0.0;
+    o[1] = W;
+    o[2] = sv0;
+    o[3] = sv1;
+    o[4] = sv2;
+    o[5] = se0;
+    o[6] = se1;
+    o[7] = se2;
+  }
+}
+
+// dmass[j] += to_mass * w_j / W over the donors of every inserted candidate
+template <int G>
+__global__ void __launch_bounds__(256)
+k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wtot,
+           const int *__restrict__ ilist, const int *__restrict__ off,
+           const int *__restrict__ nbr, const double4 *__restrict__ xf,
+           const int *__restrict__ ty, const double *__restrict__ rm, PcDev p,
+           double *__restrict__ dmass) {
+  const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (k >= nins) return;
+  const int row = rows[k];
+  const int i = ilist ? ilist[row] : row;
+  const double4 xi = xf[i];
+  const double W = Wtot[k];
+  for (int q = off[row] + lane; q < off[row + 1]; q += G) {
+    const int j = nbr[q] & MP_NMASK;
+    if (ty[j] != p.from_type || !(rm[j] > 0.5 * p.to_mass)) continue;
+    const double4 xj = xf[j];
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    atomicAdd(&dmass[j], p.to_mass * pc_w(p.dim, sqrt(rsq) * p.cutoff) / W);
+  }
+}
+
+// ---- host side: the random stream, in the reference's order ----------------------------
+inline double park_uniform(int &seed) {  // RanPark::uniform, random_park.cpp:42-49
+  const int IA = 16807, IM = 2147483647, IQ = 127773, IR = 2836;
+  const double AM = 1.0 / IM;
+  const int k = seed / IQ;
+  seed = IA * (seed - k * IQ) - IR * k;
+  if (seed < 0) seed += IM;
+  return AM * seed;
+}
+
+inline bool pc_owns(const sph_phasechange_params &p, int dim, const double *c) {  // :441-452
+  if (c[0] >= p.sublo[0] && c[0] < p.subhi[0] && c[1] >= p.sublo[1] && c[1] < p.subhi[1] &&
+      c[2] >= p.sublo[2] && c[2] < p.subhi[2])
+    return true;
+  if (dim == 3 && c[2] >= p.boxhi[2] && p.top[2] && c[0] >= p.sublo[0] && c[0] < p.subhi[0] &&
+      c[1] >= p.sublo[1] && c[1] < p.subhi[1])
+    return true;
+  if (dim == 2 && c[1] >= p.boxhi[1] && p.top[1] && c[0] >= p.sublo[0] && c[0] < p.subhi[0])
+    return true;
+  return false;
+}
+
+inline void pc_newpos_simple(int &seed, const double *x, double delta, double *c) {  // :466-470
+  c[0] = x[0] + (park_uniform(seed) - 0.5) * delta;
+  c[1] = x[1] + (park_uniform(seed) - 0.5) * delta;
+  c[2] = x[2] + (park_uniform(seed) - 0.5) * delta;
+}
+
+inline void pc_newpos(int dim, int &seed, const double *x, const double *cg, double delta,
+                      double *c) {  // :472-520, with the reference's b1abs test on b2 (:494)
+  const double CG_SMALL = 1.0e-20;
+  double eij[3];
+  if (dim == 3) {
+    double b1[3] = {-cg[1], cg[0], 0.0};
+    const double b1abs = std::sqrt(b1[0] * b1[0] + b1[1] * b1[1] + b1[2] * b1[2]);
+    if (b1abs > CG_SMALL)
+      for (double &b : b1) b = b / b1abs;
+    const double den = std::pow(cg[1], 2) + std::pow(cg[0], 2);
+    double b2[3] = {-cg[0] * cg[1] * cg[2] / den, -cg[2] * std::pow(cg[1], 2) / den, cg[1]};
+    const double b2abs = std::sqrt(b2[0] * b2[0] + b2[1] * b2[1] + b2[2] * b2[2]);
+    if (b1abs > CG_SMALL)
+      for (double &b : b2) b = b / b2abs;
+    const double a = park_uniform(seed) - 0.5;
+    const double b = park_uniform(seed) - 0.5;
+    for (int d = 0; d < 3; d++) eij[d] = a * b1[d] + b * b2[d];
+  } else {
+    double a = park_uniform(seed);
+    a = (a > 0.5) ? 1.0 : -1.0;
+    eij[0] = -a * cg[1];
+    eij[1] = a * cg[0];
+    eij[2] = 0.0;
+  }
+  const double eabs = std::sqrt(eij[0] * eij[0] + eij[1] * eij[1] + eij[2] * eij[2]);
+  for (int d = 0; d < 3; d++) c[d] = x[d] + eij[d] * delta / eabs;
+}
+
+// What the stream needs of one candidate (in the order the reference meets them)
+struct PcCand {
+  double x[3], cg[3], e, cv, rho;
+  double rec[8];  // k_pc_candidates: around, W, Sv[3], Svest[3]
+};
+
+// The candidate loop of pre_exchange (:198-321).  For each candidate that changes phase:
+// its index in `c` (ins_k), its new energy e_i = (e_i - Hwv)/2, and the new atom's
+// 13-double record {x[3], v[3], vest[3], e, rmass, rho, cv} (ins_rec).
+inline void pc_replay(const sph_phasechange_params &p, int dim, int &seed,
+                      const std::vector<PcCand> &c, std::vector<int> &ins_k,
+                      std::vector<double> &ins_rec) {
+  ins_k.clear();
+  ins_rec.clear();
+  for (size_t k = 0; k < c.size(); k++) {
+    const PcCand &a = c[k];
+    const double Ti = a.e / a.cv;
+    const bool around = a.rec[0] != 0.0;
+    bool change;
+    if (p.energy_chance) {
+      const double threshold = (a.e - p.Tc * a.cv) / p.Hwv * p.dt * p.rate;
+      change = (park_uniform(seed) < threshold) && around;
+    } else {
+      change = (park_uniform(seed) < p.change_chance) && (Ti > p.Tt) && around;
+    }
+    if (!change) continue;
+    double coord[3];
+    bool ok = false;
+    double delta = p.dr;
+    int na = 0;
+    do {
+      pc_newpos(dim, seed, a.x, a.cg, delta, coord);
+      ok = pc_owns(p, dim, coord);
+      delta = 0.75 * delta;
+      na++;
+    } while (!ok && na < p.maxattempt);
+    if (!ok) {
+      delta = p.dr;
+      na = 0;
+      do {
+        pc_newpos_simple(seed, a.x, delta, coord);
+        ok = pc_owns(p, dim, coord);
+        delta = 0.75 * delta;
+        na++;
+      } while (!ok && na < p.maxattempt);
+    }
+    if (!ok) continue;
+    const double W = a.rec[1];
+    const double energy_aux = 0.5 * (a.e - p.Hwv);  // :317-320
+    double o[13];
+    o[0] = coord[0];
+    o[1] = coord[1];
+    o[2] = coord[2];
+    for (int d = 0; d < 3; d++) {
+      o[3 + d] = (a.rec[2 + d] * p.to_mass / W) / p.to_mass;  // dmom / to_mass (:300-302)
+      o[6 + d] = (a.rec[5 + d] * p.to_mass / W) / p.to_mass;  // dmomest / to_mass
+    }
+    o[9] = energy_aux;
+    o[10] = p.to_mass;
+    o[11] = a.rho;
+    o[12] = a.cv;
+    ins_k.push_back((int)k);
+    ins_rec.insert(ins_rec.end(), o, o + 13);
+  }
+}
+
+}  // namespace sph

@@ -580,3 +580,260 @@ class RefRun:
 
     def numneigh_full(self):
         return np.diff(self.foff).astype(np.int32)
+
+
+# ---------------------------------------------------------------------------------------
+# C5: the multiphase stack of examples/USER/sph/bubble_growth/bubble.lmp:57-73 on atom_style
+# meso/multiphase (per-atom rmass, cv, colorgradient), Verlet with fix meso (rmass) and
+# fix phase_change (pre_exchange on its reneighbor steps), one process, newton on.
+# ---------------------------------------------------------------------------------------
+@dataclass
+class MpPhysics:
+    """pair_style hybrid/overlay sph/rhosum/multiphase N sph/colorgradient N
+    sph/taitwater/multiphase sph/surfacetension sph/heatconduction/phasechange (tables are
+    (nt+1, nt+1), upper triangle read) + fix phase_change (pc dict, or None)."""
+
+    skin: float = 0.0
+    dt: float = 1e-4
+    every: int = 1
+    rhosum_nstep: int = 1
+    rhosum_cut: np.ndarray | None = None
+    cg_nstep: int = 1
+    cg_alpha: np.ndarray | None = None
+    cg_cut: np.ndarray | None = None
+    tait: bool = True
+    rho0: np.ndarray | None = None
+    c0: np.ndarray | None = None
+    gamma: np.ndarray | None = None
+    rbg: np.ndarray | None = None
+    visc: np.ndarray | None = None
+    tait_cut: np.ndarray | None = None
+    st: bool = True
+    st_cut: np.ndarray | None = None
+    heat: bool = True
+    heat_alpha: np.ndarray | None = None
+    heat_cut: np.ndarray | None = None
+    heat_fixflag: np.ndarray | None = None
+    heat_tc: np.ndarray | None = None
+    pc: dict | None = None
+
+    def tables(self):
+        return [(self.rhosum_nstep > 0, self.rhosum_cut), (self.cg_nstep > 0, self.cg_cut),
+                (self.tait, self.tait_cut), (self.st, self.st_cut), (self.heat, self.heat_cut)]
+
+    def cutmax(self, nt):
+        cm = np.zeros((nt + 1, nt + 1))
+        for on, c in self.tables():
+            if on and c is not None:
+                cm = np.maximum(cm, np.asarray(c))
+        for i in range(nt + 1):
+            for j in range(i):
+                cm[i, j] = cm[j, i]
+        return cm
+
+
+def _sym(t):
+    """coeff() upper triangle mirrored like init_one"""
+    t = np.array(t, dtype=np.float64 if np.asarray(t).dtype.kind == "f" else np.int32)
+    for i in range(t.shape[0]):
+        for j in range(i):
+            t[i, j] = t[j, i]
+    return np.ascontiguousarray(t)
+
+
+def pc_params(sysm: System, pc: dict, dt: float) -> PcParams:
+    p = PcParams()
+    p.dim = sysm.dim
+    for k in ("Tc", "Tt", "Hwv", "dr", "to_mass", "cutoff"):
+        setattr(p, k, float(pc[k]))
+    p.from_type, p.to_type = int(pc["from_type"]), int(pc["to_type"])
+    p.energy_chance = int(pc.get("energy_chance", 0))
+    p.change_chance = float(pc.get("prob", 0.0))
+    p.rate = float(pc.get("rate", 0.0))
+    p.dt = dt
+    p.maxattempt = int(pc.get("maxattempt", 10))
+    for k in range(3):
+        p.sublo[k], p.subhi[k], p.boxhi[k] = sysm.boxlo[k], sysm.boxhi[k], sysm.boxhi[k]
+        p.top[k] = 1
+    return p
+
+
+class MpRefRun:
+    """C5 Verlet (verlet.cpp:222-308) over the C restatement: initial_integrate (fix meso,
+    rmass) -> [pre_exchange: fix phase_change] -> pbc/borders/lists or forward comm (comm
+    vel yes: x, v, rho, cg, rmass, e, vest) -> rhosum/multiphase, colorgradient (owned rows;
+    the styles' misnamed pack_comm moves nothing, so ghosts keep their comm-time rho and cg,
+    SURVEY A.6-1) -> taitwater/multiphase, surfacetension, heatconduction/phasechange on the
+    half list with Newton-3 -> reverse comm (f, de) -> final_integrate.  Atom order = tag
+    order (new atoms appended, no sort)."""
+
+    def __init__(self, sysm: System, ph: MpPhysics, cg=None):
+        self.s = sysm.copy()
+        assert self.s.rmass is not None
+        self.ph = ph
+        nt = sysm.ntypes
+        self.cns, self.cutneighmax = cutneighsq(nt, ph.cutmax(nt), ph.skin)
+        n = sysm.n
+        self.vest = np.zeros((n, 3))
+        self.cg = np.zeros((n, 3)) if cg is None else np.array(cg, dtype=np.float64)
+        self.f = np.zeros((n, 3))
+        self.drho = np.zeros(n)
+        self.de = np.zeros(n)
+        self.step = 0
+        self.last_build = 0
+        self.dtf = 0.5 * ph.dt
+        self.next_pc = 1                      # next_reneighbor = ntimestep + 1 (:120)
+        self.seed = int(ph.pc["seed"]) if ph.pc else 0
+        self.ninserted = 0
+        self.tabs = {}
+        for name in ("rhosum_cut", "cg_alpha", "cg_cut", "visc", "tait_cut", "st_cut",
+                     "heat_alpha", "heat_cut", "heat_tc"):
+            v = getattr(ph, name)
+            self.tabs[name] = _sym(v) if v is not None else np.zeros((nt + 1, nt + 1))
+        ff = ph.heat_fixflag if ph.heat_fixflag is not None else np.zeros((nt + 1, nt + 1))
+        self.tabs["heat_fixflag"] = _sym(np.asarray(ff, dtype=np.int32))
+        if ph.tait:
+            g = np.where(ph.gamma != 0, ph.gamma, 1.0)     # (type 0 unused)
+            self.B = np.ascontiguousarray(ph.c0 * ph.c0 * ph.rho0 / g, dtype=np.float64)
+
+    def _ghost_fields(self):
+        s, g = self.s, self.g
+        self.v_all = g.gather(s.v)
+        self.vest_all = g.gather(self.vest)
+        self.rho_all = g.gather(s.rho)
+        self.e_all = g.gather(s.e)
+        self.cv_all = g.gather(s.cv)
+        self.rm_all = g.gather(s.rmass)
+        self.cg_all = g.gather(self.cg)
+
+    def _build(self):
+        s = self.s
+        lib().orc_pbc(C.byref(s.domain()), s.n, s.x)
+        self.g = borders(s, self.cutneighmax)
+        self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
+        self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
+        self._ghost_fields()
+
+    def _forward(self):
+        g, s = self.g, self.s
+        xa = g.x
+        xa[:s.n] = s.x
+        lib().orc_forward_comm(C.byref(s.domain()), g.nlocal, g.nghost, g.owner,
+                               np.ascontiguousarray(g.image.ravel()), xa, None, None, None)
+        self._ghost_fields()
+
+    def _force(self):
+        s, g, ph, L = self.s, self.g, self.ph, lib()
+        nt, n, nall = s.ntypes, s.n, g.nall
+        T = self.tabs
+        g.x[:n] = s.x
+        if ph.rhosum_nstep > 0 and self.step % ph.rhosum_nstep == 0:
+            rho = np.zeros(nall)
+            c = T["rhosum_cut"]
+            L.orc_rhosum_multiphase(s.dim, n, g.x, g.type, nt, self.rm_all, c, c * c,
+                                    self.foff, _nz(self.fnb), rho)
+            s.rho[:] = rho[:n]
+            self.rho_all[:n] = s.rho           # ghosts keep their comm-time rho (A.6-1)
+        if ph.cg_nstep > 0 and self.step % ph.cg_nstep == 0:
+            cgo = np.zeros((nall, 3))
+            c = T["cg_cut"]
+            L.orc_colorgradient(s.dim, n, g.x, self.rho_all, self.rm_all, g.type, nt,
+                                T["cg_alpha"], c, c * c, self.foff, _nz(self.fnb), cgo)
+            self.cg[:] = cgo[:n]
+            self.cg_all[:n] = self.cg          # ghosts keep their comm-time cg (A.6-1)
+        f = np.zeros((nall, 3))
+        de = np.zeros(nall)
+        if ph.tait:
+            c = T["tait_cut"]
+            # the style reads atom->v (comm vel yes), pair_sph_taitwater_multiphase.cpp:103
+            L.orc_taitwater_multiphase(s.dim, n, 1, g.x, np.ascontiguousarray(self.v_all),
+                                       self.rho_all, g.type, nt, self.rm_all,
+                                       np.ascontiguousarray(ph.rho0, dtype=np.float64),
+                                       np.ascontiguousarray(ph.c0, dtype=np.float64), self.B,
+                                       np.ascontiguousarray(ph.gamma, dtype=np.float64),
+                                       np.ascontiguousarray(ph.rbg, dtype=np.float64),
+                                       T["visc"], c, c * c, self.hoff, _nz(self.hnb), f)
+        if ph.st:
+            c = T["st_cut"]
+            L.orc_surfacetension(s.dim, n, 1, g.x, self.rho_all, self.rm_all, g.type, nt,
+                                 np.ascontiguousarray(self.cg_all), c, c * c, self.hoff,
+                                 _nz(self.hnb), f)
+        if ph.heat:
+            c = T["heat_cut"]
+            L.orc_heatconduction_phasechange(s.dim, n, 1, g.x, self.e_all, self.cv_all,
+                                             self.rho_all, self.rm_all, g.type, nt,
+                                             T["heat_alpha"], T["heat_fixflag"].ctypes.data,
+                                             T["heat_tc"].ctypes.data,
+                                             c, c * c, self.hoff, _nz(self.hnb), de)
+        reverse_comm(g, f, None, de)
+        self.f = f[:n].copy()
+        self.drho = np.zeros(n)
+        self.de = de[:n].copy()
+
+    def _phase_change(self):
+        """FixPhaseChange::pre_exchange (fix_phase_change.cpp:167-352) on the last build's
+        full list: owned x as integrated, ghosts as last communicated."""
+        s, g, L = self.s, self.g, lib()
+        n = s.n
+        p = pc_params(s, self.ph.pc, self.ph.dt)
+        x_all = np.ascontiguousarray(np.concatenate([s.x, g.x[n:]]))
+        v_all = np.ascontiguousarray(np.concatenate([s.v, self.v_all[n:]]))
+        vest_all = np.ascontiguousarray(np.concatenate([self.vest, self.vest_all[n:]]))
+        e_all = np.ascontiguousarray(np.concatenate([s.e, self.e_all[n:]]))
+        rm_all = np.ascontiguousarray(np.concatenate([s.rmass, self.rm_all[n:]]))
+        rho_all = np.ascontiguousarray(np.concatenate([s.rho, self.rho_all[n:]]))
+        cv_all = np.ascontiguousarray(np.concatenate([s.cv, self.cv_all[n:]]))
+        cg_all = np.ascontiguousarray(np.concatenate([self.cg, self.cg_all[n:]]))
+        seed, nins, rec, par, dmass = phasechange(p, self.seed, n, x_all, v_all, vest_all,
+                                                  cg_all, e_all, rm_all, rho_all, cv_all,
+                                                  g.type, self.foff, self.fnb)
+        self.seed = seed
+        s.e[:] = e_all[:n]
+        reverse_comm(g, None, dmass, None)        # comm->reverse_comm_fix (:324)
+        L.orc_phasechange_finish(n, dmass, s.rmass, s.e)
+        if nins:
+            to = int(self.ph.pc["to_type"])
+            s.x = np.concatenate([s.x, rec[:, 0:3]])
+            s.v = np.concatenate([s.v, rec[:, 3:6]])
+            self.vest = np.concatenate([self.vest, rec[:, 6:9]])
+            s.e = np.concatenate([s.e, rec[:, 9]])
+            s.rmass = np.concatenate([s.rmass, rec[:, 10]])
+            s.rho = np.concatenate([s.rho, rec[:, 11]])
+            s.cv = np.concatenate([s.cv, rec[:, 12]])
+            s.type = np.concatenate([s.type, np.full(nins, to, dtype=np.int32)])
+            self.cg = np.concatenate([self.cg, np.zeros((nins, 3))])   # create_atom
+            for k in ("f",):
+                setattr(self, k, np.concatenate([getattr(self, k), np.zeros((nins, 3))]))
+            self.drho = np.concatenate([self.drho, np.zeros(nins)])
+            self.de = np.concatenate([self.de, np.zeros(nins)])
+            self.ninserted += nins
+        return nins
+
+    def setup(self):
+        self.step = 0
+        self._build()
+        lib().orc_meso_setup(self.s.n, self.s.v, self.vest)   # FixMeso::setup_pre_force
+        self._force()
+        self.last_build = 0
+
+    def run(self, nsteps):
+        s, L, ph = self.s, lib(), self.ph
+        for _ in range(nsteps):
+            self.step += 1
+            L.orc_meso_initial_g(s.n, ph.dt, self.dtf, s.type, 0, s.mass, s.rmass.ctypes.data,
+                                 s.x, s.v, self.f, self.vest, s.rho, self.drho, s.e, self.de)
+            pc_due = ph.pc is not None and self.step == self.next_pc
+            if pc_due or (self.step - self.last_build) % ph.every == 0:
+                if pc_due:
+                    self._phase_change()
+                    self.next_pc += int(ph.pc.get("nevery", 1))
+                self._build()
+                self.last_build = self.step
+            else:
+                self._forward()
+            self._force()
+            L.orc_meso_final_g(s.n, self.dtf, s.type, 0, s.mass, s.rmass.ctypes.data, s.v,
+                               self.f, s.rho, self.drho, s.e, self.de)
+
+    def numneigh_full(self):
+        return np.diff(self.foff).astype(np.int32)

@@ -84,3 +84,68 @@ def oracle_forces(sysm, ph: po.Physics, P, newton=1, reverse=True):
     if reverse:
         po.reverse_comm(g, f, drho, de)
     return f, drho, de
+
+
+def bubble_system(nx=10, dim=3, rv=None):
+    """C5 geometry (examples/USER/sph/bubble_growth/bubble.lmp, vars.lmp, in.phases): unit box,
+    lattice sc (sq) dx = 1/nx with origin 0.5, liquid (type 1) everywhere, vapour (type 2)
+    inside a sphere at the centre (radius rv, default 1.01 dx: the 8 (4) central sites);
+    rho_l 1, rho_v 0.1, cv_l 0.04, cv_v 0.06, e = cv T with T_l = Tinf = 1, T_v = Tc = 0,
+    per-atom mass = dx^dim rho."""
+    dx = 1.0 / nx
+    nz = nx if dim == 3 else 1
+    g = np.stack(np.meshgrid(np.arange(nx), np.arange(nx), np.arange(nz), indexing="ij"),
+                 -1).reshape(-1, 3)
+    g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]      # create_atoms: x fastest
+    x = (g + 0.5) * dx
+    if dim == 2:
+        x[:, 2] = 0.0
+    c = np.array([0.5, 0.5, 0.5 if dim == 3 else 0.0])
+    rv = 1.01 * dx if rv is None else rv
+    vap = ((x - c) ** 2).sum(1) < rv * rv
+    t = np.where(vap, 2, 1).astype(np.int32)
+    rho = np.where(vap, 0.1, 1.0)
+    cv = np.where(vap, 0.06, 0.04)
+    e = np.where(vap, 0.06 * 0.0, 0.04 * 1.0)
+    boxhi = np.array([1.0, 1.0, 1.0 if dim == 3 else dx])
+    s = po.System(dim, np.zeros(3), boxhi, (1, 1, 1 if dim == 3 else 0), x, np.zeros_like(x), t,
+                  rho, e, cv, 2, np.zeros(3), rmass=rho * dx ** dim)
+    return s
+
+
+def bubble_physics(nx=10, dim=3, dt=None, prob=0.01, Tt=0.1, pc=True, nevery=1, seed=123456):
+    """bubble.lmp:57-73 pair stack with vars.lmp values (h = 3 dx, neighbor 0 bin, every 1)
+    and fix phase_change Tc Tt Hwv dr mass_v cutoff 1 2 nevery seed prob (:105-109).
+    dt defaults to a small multiple of the script's stability limits."""
+    dx = 1.0 / nx
+    h = 3.0 * dx
+    rho_l, rho_v = 1.0, 0.1
+    c_l, c_v = 200.0 / np.sqrt(rho_l), 200.0 / np.sqrt(rho_v)
+    eta_l, eta_v = 1.0, 0.69
+    eta_ld = 2 * eta_l * eta_v / (eta_v + eta_l)
+    D_l, D_v = 0.2, 0.6
+    D_ld = 2 * D_l * D_v / (D_v + D_l)
+    alpha = 500.0
+    hh = np.zeros((3, 3))
+    hh[1:, 1:] = h
+    cga = np.zeros((3, 3))
+    cga[1, 2] = alpha
+    visc = np.zeros((3, 3))
+    visc[1, 1], visc[1, 2], visc[2, 2] = eta_l, eta_ld, eta_v
+    hal = np.zeros((3, 3))
+    hal[1, 1], hal[1, 2], hal[2, 2] = D_l, D_ld, D_v
+    ff = np.zeros((3, 3), dtype=np.int32)
+    ff[1, 2] = 2                       # "1 2 ... NULL Tc": type 2 held at Tc
+    tc = np.zeros((3, 3))
+    if dt is None:
+        dt = 0.25 * 0.25 * dx / c_v
+    pcd = None
+    if pc:
+        pcd = dict(Tc=0.0, Tt=Tt, Hwv=8.0, dr=0.5 * dx, to_mass=dx ** dim * rho_v, cutoff=h,
+                   from_type=1, to_type=2, nevery=nevery, seed=seed, prob=prob)
+    return po.MpPhysics(skin=0.0, dt=dt, every=1, rhosum_cut=hh.copy(), cg_alpha=cga,
+                        cg_cut=hh.copy(), rho0=np.array([0.0, rho_l, rho_v]),
+                        c0=np.array([0.0, c_l, c_v]), gamma=np.array([0.0, 1.0, 1.0]),
+                        rbg=np.zeros(3), visc=visc, tait_cut=hh.copy(), st_cut=hh.copy(),
+                        heat_alpha=hal, heat_cut=hh.copy(), heat_fixflag=ff, heat_tc=tc,
+                        pc=pcd)

@@ -964,7 +964,7 @@ def main():
 
 
 def attach_pmc_traffic(out, kname, alg_bytes, world, args):
-    """HBM traffic per launch of the roofline kernel from PMC counters, measured on THIS
+    """HBM traffic per step of the roofline kernel from PMC counters, measured on THIS
     workload by tools/pmc_traffic.sh and committed as profiles/<round>/pmc_traffic.json with
     the kernel, config and commit it was taken on.  Attached as `traffic` only when that
     record matches this run (same kernel family, single GPU, same lattice edge and steps);
@@ -978,16 +978,15 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args):
         if (meta.get("world") != world or meta.get("edge") != args.edge
                 or meta.get("path") != args.path):
             continue
-        for k, v in rec.items():
-            if k.startswith("_"):
-                continue
-            if k.split("<")[0].split("::")[-1] == kname and v.get("traffic_bytes"):
-                out["roofline"]["traffic"] = v["traffic_bytes"] / 1e9
-                out["roofline"]["traffic_unit"] = (
-                    f"GB per launch (PMC 2*FETCH_SIZE + WRITE_SIZE, tools/pmc_traffic.sh, "
-                    f"profiles/{rnd}/pmc_traffic.json, commit {meta.get('commit', '?')})")
-                out["roofline"]["algorithmic_GB_per_launch"] = alg_bytes / 1e9
-                return
+        v = rec.get(kname, {})
+        if v.get("traffic_bytes"):
+            out["roofline"]["traffic"] = v["traffic_bytes"] / 1e9
+            out["roofline"]["traffic_unit"] = (
+                f"GB per step of {kname} (its launches summed; PMC 2*FETCH_SIZE + WRITE_SIZE, "
+                f"tools/pmc_traffic.sh, profiles/{rnd}/pmc_traffic.json, commit "
+                f"{meta.get('commit', '?')})")
+            out["roofline"]["algorithmic_GB_per_step"] = alg_bytes / 1e9
+            return
 
 
 if __name__ == "__main__":

@@ -3,7 +3,7 @@
 # separate rocprofv3 --pmc passes (they do not fit one pass; no tracing domains mixed in),
 # then tools/pmc_traffic.py applies the gfx950 FETCH_SIZE x2 correction
 # (MI355X_MICROARCH.md, HBM) and writes OUTDIR/pmc_traffic.json.
-# Usage: tools/pmc_traffic.sh OUTDIR [bench args...]
+# Usage: [META="k=v ..."] tools/pmc_traffic.sh OUTDIR [bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$(realpath -m "$1"); shift
@@ -14,4 +14,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
   python3 "$R/bench.py" "$@" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o pmc -- \
   python3 "$R/bench.py" "$@" > "$OUT/write.log" 2>&1
-python3 "$R/tools/pmc_traffic.py" "$OUT" > "$OUT/pmc_traffic.json"
+python3 "$R/tools/pmc_traffic.py" "$OUT" $META > "$OUT/pmc_traffic.json"

@@ -330,6 +330,23 @@ int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int 
 int sph_engine_get_atoms_multiphase(sph_engine *e, double *rmass, double *cv, double *cg,
                                     double *vest, int *type, int64_t *ninserted);
 
+/* Restart records of the owned atoms (one brick), in get_atoms order, in the reference's
+   per-atom restart layout: meso -- AtomVecMeso::pack_restart (atom_vec_meso.cpp:726-757),
+   17 doubles {17, x[3], tag, type, mask, image (each an int64 bit pattern, LAMMPS ubuf),
+   v[3], rho, e, cv, vest[3]}; multiphase -- AtomVecMesoMultiPhase::pack_restart
+   (atom_vec_meso_multiphase.cpp:887-916), 21 doubles {21, x[3], tag, type, mask, image (as
+   plain doubles, as that routine writes them), v[3], rho, colorgradient[3], rmass, e, cv,
+   vest[3]}.  tag = 1 + the set_atoms index (LAMMPS tags start at 1), mask = 1 (group all),
+   image = the packed imageint (lmptype.h, 10 bits per dimension, 512 = zero) counted by
+   Domain::pbc.  buf == NULL: only *rec_size (17 or 21) is returned; else cap >= nlocal *
+   rec_size doubles. */
+int sph_engine_write_restart(sph_engine *e, double *buf, int64_t cap, int *rec_size);
+/* Atoms from n restart records of the engine's layout (tags a permutation of 1..n; the
+   atom with tag t becomes set_atoms index t-1): x, v, vest, rho, e, cv, type, image (and
+   rmass, colorgradient for a multiphase engine).  Replaces set_atoms; before setup (whose
+   FixMeso::setup_pre_force sets vest = v again, as a LAMMPS run after read_restart does). */
+int sph_engine_read_restart(sph_engine *e, int n, const double *buf);
+
 /* Verlet::setup: forced rebuild + forces at step 0. */
 int sph_engine_setup(sph_engine *e);
 /* Verlet::run(nsteps). */

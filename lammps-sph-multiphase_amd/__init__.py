@@ -150,6 +150,8 @@ EXPORTS = {
     "sph_engine_set_atoms_multiphase": (_i, [_vp, _dp, _vp, _vp]),
     "sph_engine_phase_change": (_i, [_vp, _vp, _i, _i]),
     "sph_engine_get_atoms_multiphase": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "sph_engine_write_restart": (_i, [_vp, _vp, C.c_int64, C.POINTER(_i)]),
+    "sph_engine_read_restart": (_i, [_vp, _i, _dp]),
 }
 
 
@@ -509,6 +511,18 @@ class Engine:
             out["vest"].ctypes.data, out["type"].ctypes.data, C.byref(ni)))
         out["ninserted"] = ni.value
         return out
+
+    def write_restart(self) -> np.ndarray:
+        """(nlocal, 17 | 21) restart records, AtomVecMeso{,MultiPhase}::pack_restart layout."""
+        rec = _i(0)
+        _chk(self.L.sph_engine_write_restart(self.h, None, 0, C.byref(rec)))
+        buf = np.zeros((self.nlocal, rec.value))
+        _chk(self.L.sph_engine_write_restart(self.h, buf.ctypes.data, buf.size, C.byref(rec)))
+        return buf
+
+    def read_restart(self, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.float64)
+        _chk(self.L.sph_engine_read_restart(self.h, buf.shape[0], buf))
 
     def setup(self):
         _chk(self.L.sph_engine_setup(self.h))

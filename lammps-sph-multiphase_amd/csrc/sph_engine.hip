@@ -130,6 +130,7 @@ struct sph_engine {
   int pc_nevery = 1, pc_seed = 0;
   int64_t pc_next = 1, pc_inserted = 0;
   int tag_next = 0;  // tag of the next created atom (atom->tag_extend on one brick)
+  std::vector<double> cv_by_tag;  // single-phase engines: the constant cv, for restarts
 
   int nlocal = 0, nghost = 0;
   // brick decomposition (CommBrick): this brick's grid location, face neighbours, swaps
@@ -984,7 +985,7 @@ struct sph_engine {
   // if a block overflows its LDS image.
   void build_all(bool need_csr) {
     need_csr = need_csr || mp;  // (the multiphase passes walk the CSR full and half lists)
-    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p);
+    hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p, vel.p);
     if (multi()) exchange_multi();
     if (cfg.sort) sort_owned();
     borders();
@@ -1797,6 +1798,9 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   e->nghost = 0;
   e->tag_next = n;
   e->pc_inserted = 0;
+  e->cv_by_tag.assign(n, 1.0);
+  if (cv)
+    for (int i = 0; i < n; i++) e->cv_by_tag[i] = cv[i];
   e->ensure_atoms(n > 0 ? n : 1, false);
   e->vel.reserve(n > 0 ? n : 1);
   e->fo.reserve(n > 0 ? n : 1);
@@ -1808,7 +1812,7 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   for (int i = 0; i < n; i++) {
     hx[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
     hv[i] = make_double4(0.0, 0.0, 0.0, rho[i]);  // vest = 0 until setup_pre_force
-    hvel[i] = make_double4(v[3 * i], v[3 * i + 1], v[3 * i + 2], 0.0);
+    hvel[i] = make_double4(v[3 * i], v[3 * i + 1], v[3 * i + 2], (double)IMG_ZERO);
     he[i] = en ? en[i] : 0.0;
     ht[i] = i;
     hty[i] = type[i];
@@ -1924,6 +1928,151 @@ int sph_engine_get_atoms_multiphase(sph_engine *e, double *rmass, double *cv, do
       vest[3 * t + 2] = hv[i].z;
     }
     if (type) type[t] = hty[i];
+  }
+  SPH_API_END
+}
+
+// LAMMPS ubuf (lmptype.h): an integer stored as the bit pattern of an int64 in a double
+static double ubuf_d(int64_t v) {
+  double d;
+  memcpy(&d, &v, sizeof d);
+  return d;
+}
+static int64_t ubuf_i(double d) {
+  int64_t v;
+  memcpy(&v, &d, sizeof v);
+  return v;
+}
+
+int sph_engine_write_restart(sph_engine *e, double *buf, int64_t cap, int *rec_size) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_write_restart: NULL engine");
+  SPH_REQUIRE(!e->multi() && !e->global_tags, SPH_HIP_EINVAL,
+              "sph_engine_write_restart: one brick with implicit tags");
+  const int rec = e->mp ? 21 : 17;
+  if (rec_size) *rec_size = rec;
+  if (!buf) return SPH_HIP_OK;
+  const int n = e->nlocal;
+  SPH_REQUIRE(cap >= (int64_t)n * rec, SPH_HIP_EINVAL,
+              "sph_engine_write_restart: buffer of %lld doubles < %lld", (long long)cap,
+              (long long)n * rec);
+  if (n == 0) return SPH_HIP_OK;
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  std::vector<double4> hx(n), hv(n), hr(n), hg(n, make_double4(0, 0, 0, 0));
+  std::vector<double> he(n), hm(n, 0.0), hc(n, 1.0);
+  std::vector<int> ht(n), hty(n);
+  SPH_HIP_TRY(hipMemcpyAsync(hx.data(), e->xf.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hv.data(), e->vel.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hr.data(), e->vr.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(he.data(), e->en.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(hty.data(), e->ty.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  SPH_HIP_TRY(hipMemcpyAsync(ht.data(), e->tag.p, n * sizeof(int), hipMemcpyDeviceToHost, e->s));
+  if (e->mp) {
+    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), e->rm.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(hc.data(), e->cvv.p, n * sizeof(double), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(hg.data(), e->cg.p, n * sizeof(double4), hipMemcpyDeviceToHost, e->s));
+  }
+  SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  for (int i = 0; i < n; i++) {
+    const int t = ht[i];
+    SPH_REQUIRE(t >= 0 && t < n, SPH_HIP_ERUNTIME, "corrupt tag %d", t);
+    const double cv = e->mp ? hc[i] : (t < (int)e->cv_by_tag.size() ? e->cv_by_tag[t] : 1.0);
+    double *o = buf + (size_t)rec * t;
+    const int img = (int)hv[i].w;
+    int m = 0;
+    o[m++] = rec;
+    o[m++] = hx[i].x;
+    o[m++] = hx[i].y;
+    o[m++] = hx[i].z;
+    if (e->mp) {  // plain doubles (atom_vec_meso_multiphase.cpp:892-895)
+      o[m++] = t + 1;
+      o[m++] = hty[i];
+      o[m++] = 1;
+      o[m++] = img;
+    } else {  // ubuf bit patterns (atom_vec_meso.cpp:731-734)
+      o[m++] = ubuf_d(t + 1);
+      o[m++] = ubuf_d(hty[i]);
+      o[m++] = ubuf_d(1);
+      o[m++] = ubuf_d(img);
+    }
+    o[m++] = hv[i].x;
+    o[m++] = hv[i].y;
+    o[m++] = hv[i].z;
+    o[m++] = hr[i].w;
+    if (e->mp) {
+      o[m++] = hg[i].x;
+      o[m++] = hg[i].y;
+      o[m++] = hg[i].z;
+      o[m++] = hm[i];
+    }
+    o[m++] = he[i];
+    o[m++] = cv;
+    o[m++] = hr[i].x;
+    o[m++] = hr[i].y;
+    o[m++] = hr[i].z;
+  }
+  SPH_API_END
+}
+
+int sph_engine_read_restart(sph_engine *e, int n, const double *buf) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && n >= 0 && (n == 0 || buf), SPH_HIP_EINVAL,
+              "sph_engine_read_restart: bad argument");
+  SPH_REQUIRE(!e->multi(), SPH_HIP_EINVAL, "sph_engine_read_restart: one brick");
+  const int rec = e->mp ? 21 : 17;
+  std::vector<double> x(3 * (size_t)n), v(3 * (size_t)n), vest(3 * (size_t)n), rho(n), en(n),
+      cv(n), rm(n), cg(3 * (size_t)n);
+  std::vector<int> type(n), img(n), seen(n, 0);
+  for (int k = 0; k < n; k++) {
+    const double *o = buf + (size_t)rec * k;
+    SPH_REQUIRE((int)o[0] == rec, SPH_HIP_EINVAL,
+                "record %d has %g values, this engine's layout has %d", k, o[0], rec);
+    int64_t tg, ty, im;
+    if (e->mp) {
+      tg = (int64_t)o[4];
+      ty = (int64_t)o[5];
+      im = (int64_t)o[7];
+    } else {
+      tg = ubuf_i(o[4]);
+      ty = ubuf_i(o[5]);
+      im = ubuf_i(o[7]);
+    }
+    SPH_REQUIRE(tg >= 1 && tg <= n && !seen[tg - 1], SPH_HIP_EINVAL,
+                "record %d: tag %lld is not a new one of 1..%d", k, (long long)tg, n);
+    const int i = (int)tg - 1;
+    seen[i] = 1;
+    type[i] = (int)ty;
+    img[i] = (int)im;
+    int m = 8;
+    for (int d = 0; d < 3; d++) {
+      x[3 * i + d] = o[1 + d];
+      v[3 * i + d] = o[m++];
+    }
+    rho[i] = o[m++];
+    if (e->mp) {
+      for (int d = 0; d < 3; d++) cg[3 * i + d] = o[m++];
+      rm[i] = o[m++];
+    }
+    en[i] = o[m++];
+    cv[i] = o[m++];
+    for (int d = 0; d < 3; d++) vest[3 * i + d] = o[m++];
+  }
+  int rc = sph_engine_set_atoms(e, n, x.data(), v.data(), type.data(), rho.data(), en.data(),
+                                cv.data());
+  if (rc != SPH_HIP_OK) return rc;
+  if (e->mp) {
+    rc = sph_engine_set_atoms_multiphase(e, rm.data(), cv.data(), cg.data());
+    if (rc != SPH_HIP_OK) return rc;
+  }
+  if (n > 0) {  // vest and the image flags, which set_atoms does not take
+    std::vector<double4> hr(n), hv(n);
+    for (int i = 0; i < n; i++) {
+      hr[i] = make_double4(vest[3 * i], vest[3 * i + 1], vest[3 * i + 2], rho[i]);
+      hv[i] = make_double4(v[3 * i], v[3 * i + 1], v[3 * i + 2], (double)img[i]);
+    }
+    SPH_HIP_TRY(hipMemcpyAsync(e->vr.p, hr.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(e->vel.p, hv.data(), n * sizeof(double4), hipMemcpyHostToDevice, e->s));
+    SPH_HIP_TRY(hipStreamSynchronize(e->s));
   }
   SPH_API_END
 }

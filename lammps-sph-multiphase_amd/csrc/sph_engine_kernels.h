@@ -137,25 +137,40 @@ struct Box {
   int periodic[3];
 };
 
-// Domain::pbc (domain.cpp:478-560), orthogonal box
-static __global__ void k_pbc(int n, Box b, double4 *__restrict__ xf) {
+// image flags, packed as LAMMPS' imageint (lmptype.h SMALLBIG: 10 bits per dimension,
+// IMGMAX = 512 = zero image), carried in the owned atoms' vel[i].w (an exact integer)
+constexpr int IMG_MASK = 1023, IMG_MAX = 512, IMG_BITS = 10;
+constexpr int IMG_ZERO = (IMG_MAX << (2 * IMG_BITS)) | (IMG_MAX << IMG_BITS) | IMG_MAX;
+
+// Domain::pbc (domain.cpp:478-560), orthogonal box: wrap into the box, counting the image
+static __global__ void k_pbc(int n, Box b, double4 *__restrict__ xf, double4 *__restrict__ vel) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double4 x = xf[i];
   double c[3] = {x.x, x.y, x.z};
+  int img = (int)vel[i].w;
+  const int img0 = img;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     if (!b.periodic[k]) continue;
-    if (c[k] < b.lo[k]) c[k] += b.prd[k];
+    const int sh = k * IMG_BITS;
+    if (c[k] < b.lo[k]) {
+      c[k] += b.prd[k];
+      const int idim = (((img >> sh) & IMG_MASK) - 1) & IMG_MASK;
+      img = (img & ~(IMG_MASK << sh)) | (idim << sh);
+    }
     if (c[k] >= b.hi[k]) {
       c[k] -= b.prd[k];
       c[k] = fmax(c[k], b.lo[k]);
+      const int idim = (((img >> sh) & IMG_MASK) + 1) & IMG_MASK;
+      img = (img & ~(IMG_MASK << sh)) | (idim << sh);
     }
   }
   x.x = c[0];
   x.y = c[1];
   x.z = c[2];
   xf[i] = x;
+  if (img != img0) vel[i].w = (double)img;
 }
 
 // ---- borders (one process: the left/right neighbor is this rank itself) -------------

@@ -5,7 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "sph_kernels.h"
+#include "sph_engine_kernels.h"
 
 namespace sph {
 
@@ -43,7 +43,7 @@ static __global__ void k_mpx_unpack(int n, const int *__restrict__ sel, int firs
   if (k >= n) return;
   const double *const o = buf + (size_t)MPX * (sel ? sel[k] : k);
   const int i = first + k;
-  vel[i] = make_double4(o[0], o[1], o[2], 0.0);
+  vel[i] = make_double4(o[0], o[1], o[2], vel[i].w);  // (w: the owned atoms' image flags)
   rm[i] = o[3];
   cv[i] = o[4];
   cg[i] = make_double4(o[5], o[6], o[7], 0.0);
@@ -170,7 +170,7 @@ static __global__ void k_pc_append(int n, const double *__restrict__ rec, int fi
   const double *const o = rec + 13 * (size_t)k;
   const int i = first + k;
   xf[i] = make_double4(o[0], o[1], o[2], 0.0);
-  vel[i] = make_double4(o[3], o[4], o[5], 0.0);
+  vel[i] = make_double4(o[3], o[4], o[5], (double)IMG_ZERO);  // create_atom: zero image
   vr[i] = make_double4(o[6], o[7], o[8], o[11]);
   en[i] = o[9];
   rm[i] = o[10];

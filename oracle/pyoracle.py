@@ -487,7 +487,9 @@ class RefRun:
     # -- helpers -------------------------------------------------------------------------
     def _build(self):
         s = self.s
+        x0 = s.x.copy()
         lib().orc_pbc(C.byref(s.domain()), s.n, s.x)
+        self.image = getattr(self, "image", np.zeros((s.n, 3), np.int64)) + pbc_images(s, x0)
         self.g = borders(s, self.cutneighmax)
         self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
@@ -708,7 +710,12 @@ class MpRefRun:
 
     def _build(self):
         s = self.s
+        x0 = s.x.copy()
         lib().orc_pbc(C.byref(s.domain()), s.n, s.x)
+        im = getattr(self, "image", np.zeros((0, 3), np.int64))
+        if im.shape[0] < s.n:   # (created atoms: zero image, create_atom)
+            im = np.concatenate([im, np.zeros((s.n - im.shape[0], 3), np.int64)])
+        self.image = im + pbc_images(s, x0)
         self.g = borders(s, self.cutneighmax)
         self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
@@ -837,3 +844,88 @@ class MpRefRun:
 
     def numneigh_full(self):
         return np.diff(self.foff).astype(np.int32)
+
+
+# ---------------------------------------------------------------------------------------
+# Restart records (the per-atom layout of the reference's restart files) and image flags
+# ---------------------------------------------------------------------------------------
+IMGMAX, IMGBITS = 512, 10   # lmptype.h (LAMMPS_SMALLBIG): imageint = int, 10 bits per dim
+
+
+def img_pack(image):
+    """(n, 3) image counts -> packed imageint, lmptype.h / atom.cpp"""
+    im = np.asarray(image, dtype=np.int64) + IMGMAX
+    return ((im[:, 2] << (2 * IMGBITS)) | (im[:, 1] << IMGBITS) | im[:, 0]).astype(np.int64)
+
+
+def pbc_images(sysm: System, x_before: np.ndarray) -> np.ndarray:
+    """The image change Domain::pbc (domain.cpp:478-560) applied: -1 for a wrap from below
+    lo (x += prd), +1 for one from at/above hi (x -= prd)."""
+    prd = sysm.boxhi - sysm.boxlo
+    d = np.zeros(x_before.shape, dtype=np.int64)
+    for k in range(3):
+        if sysm.periodic[k] and prd[k] > 0:
+            d[:, k] = np.rint((x_before[:, k] - sysm.x[:, k]) / prd[k]).astype(np.int64)
+    return d
+
+
+def _ubuf(a):
+    return np.asarray(a, dtype=np.int64).view(np.float64)
+
+
+def pack_restart_meso(x, tag, type_, image, v, rho, e, cv, vest, mask=None):
+    """AtomVecMeso::pack_restart (atom_vec_meso.cpp:726-757): 17 doubles per atom, the ints
+    as ubuf bit patterns (lmptype.h)."""
+    n = x.shape[0]
+    mask = np.ones(n, np.int64) if mask is None else mask
+    out = np.zeros((n, 17))
+    out[:, 0] = 17
+    out[:, 1:4] = x
+    out[:, 4] = _ubuf(tag)
+    out[:, 5] = _ubuf(type_)
+    out[:, 6] = _ubuf(mask)
+    out[:, 7] = _ubuf(image)
+    out[:, 8:11] = v
+    out[:, 11] = rho
+    out[:, 12] = e
+    out[:, 13] = cv
+    out[:, 14:17] = vest
+    return out
+
+
+def pack_restart_multiphase(x, tag, type_, image, v, rho, cg, rmass, e, cv, vest, mask=None):
+    """AtomVecMesoMultiPhase::pack_restart (atom_vec_meso_multiphase.cpp:887-916): 21 doubles
+    per atom, the ints as plain doubles (that routine assigns them directly)."""
+    n = x.shape[0]
+    mask = np.ones(n) if mask is None else mask
+    out = np.zeros((n, 21))
+    out[:, 0] = 21
+    out[:, 1:4] = x
+    out[:, 4] = tag
+    out[:, 5] = type_
+    out[:, 6] = mask
+    out[:, 7] = image
+    out[:, 8:11] = v
+    out[:, 11] = rho
+    out[:, 12:15] = cg
+    out[:, 15] = rmass
+    out[:, 16] = e
+    out[:, 17] = cv
+    out[:, 18:21] = vest
+    return out
+
+
+def unpack_restart(buf):
+    """AtomVecMeso{,MultiPhase}::unpack_restart (atom_vec_meso.cpp:763-800,
+    atom_vec_meso_multiphase.cpp:922-960) of a (n, 17 | 21) record array."""
+    buf = np.asarray(buf)
+    mp = buf.shape[1] == 21
+    ints = (lambda c: buf[:, c].astype(np.int64)) if mp else (lambda c: buf[:, c].view(np.int64))
+    d = dict(x=buf[:, 1:4], tag=ints(4), type=ints(5), mask=ints(6), image=ints(7),
+             v=buf[:, 8:11], rho=buf[:, 11])
+    if mp:
+        d.update(cg=buf[:, 12:15], rmass=buf[:, 15], e=buf[:, 16], cv=buf[:, 17],
+                 vest=buf[:, 18:21])
+    else:
+        d.update(e=buf[:, 12], cv=buf[:, 13], vest=buf[:, 14:17])
+    return d

@@ -1,0 +1,130 @@
+"""Restart records: the engine's state in the reference's per-atom
+restart layout -- AtomVecMeso::pack_restart (atom_vec_meso.cpp:726-757, 17 doubles, ints as
+ubuf bit patterns) and AtomVecMesoMultiPhase::pack_restart (atom_vec_meso_multiphase.cpp:
+887-916, 21 doubles, ints as plain doubles) -- with image flags counted as Domain::pbc does
+(domain.cpp:478-560).  Checked against the oracle's restatement of the layouts on the
+oracle's own state, round-tripped write -> read -> write bit-identically, and continued:
+read_restart + setup + run equals the oracle restarted from the same state."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+from conftest import rel_err
+from scenarios import bubble_physics, bubble_system, c2_system
+
+TOL = 1e-10
+
+
+def drifting_c2(n=8):
+    """C2 box drifting +x fast enough that atoms wrap the periodic boundary within 12 steps"""
+    s = c2_system(n)
+    s.v[:, 0] += 10.0
+    ph = po.c2_physics()
+    ph.dt = 1e-2
+    ph.every = 4
+    return s, ph
+
+
+def test_layouts_roundtrip():
+    rng = np.random.default_rng(5)
+    n = 7
+    x, v, vest, cg = (rng.normal(size=(n, 3)) for _ in range(4))
+    tag = np.arange(1, n + 1)
+    typ = rng.integers(1, 3, n)
+    img = po.img_pack(rng.integers(-3, 4, size=(n, 3)))
+    rho, e, cv, rm = (rng.uniform(0.5, 2, n) for _ in range(4))
+    m = po.pack_restart_meso(x, tag, typ, img, v, rho, e, cv, vest)
+    d = po.unpack_restart(m)
+    assert m.shape == (n, 17) and np.all(m[:, 0] == 17)
+    assert np.array_equal(d["tag"], tag) and np.array_equal(d["image"], img)
+    assert np.array_equal(d["vest"], vest) and np.array_equal(d["e"], e)
+    # ubuf: the int64 bit pattern, not the value
+    assert m[0, 4] != tag[0] and np.array([m[0, 4]]).view(np.int64)[0] == tag[0]
+    p = po.pack_restart_multiphase(x, tag, typ, img, v, rho, cg, rm, e, cv, vest)
+    d = po.unpack_restart(p)
+    assert p.shape == (n, 21) and p[0, 4] == tag[0]
+    assert np.array_equal(d["cg"], cg) and np.array_equal(d["rmass"], rm)
+    assert np.array_equal(d["image"], img)
+
+
+def test_oracle_images_unwrap_continuously():
+    s, ph = drifting_c2()
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    prd = s.boxhi - s.boxlo
+    x0 = ref.s.x + ref.image * prd   # (setup's pbc already wrapped the jittered edge atoms)
+    ref.run(12)
+    unwrapped = ref.s.x + ref.image * prd
+    assert (ref.image[:, 0] != 0).any(), "no atom wrapped"
+    # the unwrapped drift is smooth: ~ v dt per step, never a jump of one box length
+    assert np.abs(unwrapped - x0).max() < 2.0
+
+
+def _oracle_records(ref, mp=False):
+    s = ref.s
+    n = s.n
+    tag = np.arange(1, n + 1)
+    img = po.img_pack(ref.image)
+    if mp:
+        return po.pack_restart_multiphase(s.x, tag, s.type, img, s.v, s.rho, ref.cg, s.rmass,
+                                          s.e, s.cv, ref.vest)
+    return po.pack_restart_meso(s.x, tag, s.type, img, s.v, s.rho, s.e, s.cv, ref.vest)
+
+
+def _check_records(got, want):
+    g, w = po.unpack_restart(got), po.unpack_restart(want)
+    for k in ("tag", "type", "mask", "image"):
+        assert np.array_equal(g[k], w[k]), k
+    for k in ("x", "v", "rho", "e", "cv", "vest") + (("cg", "rmass") if "cg" in w else ()):
+        assert rel_err(g[k], w[k]) < TOL, k
+    assert np.all(got[:, 0] == want[:, 0])
+
+
+@pytest.mark.gpu
+def test_engine_restart_c2(gpu, sph_amd):
+    from test_gpu_engine import engine_for
+    s, ph = drifting_c2()
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(12)
+    eng = engine_for(sph_amd, s, ph)
+    eng.setup()
+    eng.run(12)
+    rec = eng.write_restart()
+    _check_records(rec, _oracle_records(ref))
+    # round trip: read into a fresh engine, write again -> the same bytes
+    eng2 = engine_for(sph_amd, s, ph)
+    eng2.read_restart(rec)
+    assert np.array_equal(eng2.write_restart(), rec)
+    # continue: read_restart + setup + run == the oracle restarted from the same state
+    d = po.unpack_restart(rec)
+    s2 = s.copy()
+    s2.x, s2.v, s2.rho, s2.e = d["x"].copy(), d["v"].copy(), d["rho"].copy(), d["e"].copy()
+    ref2 = po.RefRun(s2, ph)
+    ref2.vest = d["vest"].copy()   # (unpack_restart restores vest; borders carry it at setup)
+    ref2.setup()
+    ref2.run(5)
+    eng2.setup()
+    eng2.run(5)
+    g = eng2.get_atoms()
+    assert rel_err(g["x"], ref2.s.x) < TOL and rel_err(g["v"], ref2.s.v) < TOL
+    assert rel_err(g["f"], ref2.f) < TOL and rel_err(g["rho"], ref2.s.rho) < TOL
+
+
+@pytest.mark.gpu
+def test_engine_restart_c5(gpu, sph_amd):
+    from c5_util import mp_engine
+    s = bubble_system(8)
+    ph = bubble_physics(8, prob=0.5, Tt=-1.0)
+    ref = po.MpRefRun(s, ph)
+    ref.setup()
+    ref.run(3)
+    eng = mp_engine(sph_amd, s, ph)
+    eng.setup()
+    eng.run(3)
+    rec = eng.write_restart()
+    assert rec.shape == (ref.s.n, 21) and ref.ninserted >= 1
+    _check_records(rec, _oracle_records(ref, mp=True))
+    eng2 = mp_engine(sph_amd, s, bubble_physics(8, pc=False))
+    eng2.read_restart(rec)
+    assert np.array_equal(eng2.write_restart(), rec)

@@ -524,6 +524,21 @@ class Engine:
         buf = np.ascontiguousarray(buf, dtype=np.float64)
         _chk(self.L.sph_engine_read_restart(self.h, buf.shape[0], buf))
 
+    def dump_custom(self, fp, step, columns, boxlo, boxhi, boundary="pp pp pp"):
+        """One 'dump custom' snapshot of the owned atoms (write_dump_custom) from the engine
+        state; per-atom columns by name (see write_dump_custom)."""
+        g = self.get_atoms()
+        try:
+            g.update(self.get_atoms_multiphase())
+        except Exception:
+            pass
+        try:
+            rec = unpack_restart_records(self.write_restart())
+            g["image"] = rec["image_xyz"]
+        except Exception:
+            pass
+        write_dump_custom(fp, step, g, columns, boxlo, boxhi, boundary)
+
     def setup(self):
         _chk(self.L.sph_engine_setup(self.h))
 
@@ -583,3 +598,66 @@ class Engine:
         s = EngineStats()
         _chk(self.L.sph_engine_stats_get(self.h, C.byref(s)))
         return s.as_dict()
+
+
+# ------------------------------------------------------------------------------------------
+# dump custom / restart records on the host
+# ------------------------------------------------------------------------------------------
+def unpack_restart_records(buf):
+    """Fields of (n, 17 | 21) restart records (include/sph_hip.h, sph_engine_write_restart);
+    image_xyz = the unpacked image counts (lmptype.h: 10 bits per dimension, 512 = zero)."""
+    buf = np.asarray(buf)
+    mp = buf.shape[1] == 21
+    ints = (lambda c: buf[:, c].astype(np.int64)) if mp else (lambda c: buf[:, c].view(np.int64))
+    img = ints(7)
+    d = {"x": buf[:, 1:4], "tag": ints(4), "type": ints(5), "image": img,
+         "image_xyz": np.stack([(img & 1023) - 512, ((img >> 10) & 1023) - 512,
+                                ((img >> 20) & 1023) - 512], 1)}
+    return d
+
+
+def write_dump_custom(fp, step, atoms, columns, boxlo, boxhi, boundary="pp pp pp"):
+    """LAMMPS 'dump custom' text (dump_custom.cpp: header_item :351-362, ints '%d ', floats
+    '%g ' per value then a newline, write_text).  atoms: get_atoms()-style dict ("tag" 0-based
+    -> id = tag + 1).  Columns: id type x y z xs ys zs xu yu zu ix iy iz vx vy vz fx fy fz, and
+    the USER-SPH per-atom computes by what they return: rho (compute meso_rho/atom), e
+    (meso_e/atom), t (meso_t/atom = e / cv), cv, rmass, drho, de."""
+    lo, hi = np.asarray(boxlo, float), np.asarray(boxhi, float)
+    prd = hi - lo
+    n = atoms["x"].shape[0]
+    img = atoms.get("image", np.zeros((n, 3), np.int64))
+    cols = []
+    for c in columns:
+        if c == "id":
+            cols.append((atoms["tag"] + 1, True))
+        elif c == "type":
+            cols.append((atoms["type"], True))
+        elif c in ("x", "y", "z"):
+            cols.append((atoms["x"][:, "xyz".index(c)], False))
+        elif c in ("xs", "ys", "zs"):   # pack_xs: (x - boxlo) * (1/prd)
+            k = "xyz".index(c[0])
+            cols.append(((atoms["x"][:, k] - lo[k]) * (1.0 / prd[k]), False))
+        elif c in ("xu", "yu", "zu"):
+            k = "xyz".index(c[0])
+            cols.append((atoms["x"][:, k] + img[:, k] * prd[k], False))
+        elif c in ("ix", "iy", "iz"):
+            cols.append((img[:, "xyz".index(c[1])], True))
+        elif c in ("vx", "vy", "vz", "fx", "fy", "fz"):
+            cols.append((atoms[c[0]][:, "xyz".index(c[1])], False))
+        elif c == "t":
+            cols.append((atoms["e"] / atoms["cv"], False))
+        else:
+            cols.append((atoms[c], False))
+    close = isinstance(fp, str)
+    f = open(fp, "a") if close else fp
+    f.write(f"ITEM: TIMESTEP\n{int(step)}\nITEM: NUMBER OF ATOMS\n{n}\n")
+    f.write(f"ITEM: BOX BOUNDS {boundary}\n")
+    for k in range(3):
+        f.write("%g %g\n" % (lo[k], hi[k]))
+    f.write("ITEM: ATOMS " + " ".join(columns) + "\n")
+    order = np.argsort(atoms["tag"], kind="stable")
+    for i in order:
+        f.write("".join(("%d " % int(a[i])) if is_int else ("%g " % float(a[i]))
+                        for a, is_int in cols) + "\n")
+    if close:
+        f.close()

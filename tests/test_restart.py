@@ -128,3 +128,26 @@ def test_engine_restart_c5(gpu, sph_amd):
     eng2 = mp_engine(sph_amd, s, bubble_physics(8, pc=False))
     eng2.read_restart(rec)
     assert np.array_equal(eng2.write_restart(), rec)
+
+
+def test_dump_custom_format():
+    """dump_custom.cpp header_item (:351-362) and write_text ('%d ' / '%g ' per value)"""
+    import io
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "sph_amd_cpu", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "lammps-sph-multiphase_amd", "__init__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    atoms = dict(x=np.array([[0.5, 1.0, 0.0], [3.0, 2.0, 0.0]]), tag=np.array([1, 0]),
+                 type=np.array([2, 1]), rho=np.array([1000.0, 999.5]), e=np.array([0.0, 1e-3]),
+                 f=np.array([[0.1, -2.0, 0.0], [1.5, 0.25, 0.0]]))
+    buf = io.StringIO()
+    m.write_dump_custom(buf, 100, atoms, ["id", "type", "xs", "ys", "zs", "rho", "e", "fx", "fy"],
+                        [0.0, 0.0, -0.001], [4.001, 8.001, 0.001], "ff ff pp")
+    want = ("ITEM: TIMESTEP\n100\nITEM: NUMBER OF ATOMS\n2\nITEM: BOX BOUNDS ff ff pp\n"
+            "0 4.001\n0 8.001\n-0.001 0.001\nITEM: ATOMS id type xs ys zs rho e fx fy\n"
+            "1 1 0.749813 0.249969 0.5 999.5 0.001 1.5 0.25 \n"
+            "2 2 0.124969 0.124984 0.5 1000 0 0.1 -2 \n")
+    assert buf.getvalue() == want

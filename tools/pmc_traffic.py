@@ -52,8 +52,10 @@ def main(root, meta):
             fa, wa = sum(f) / len(f), sum(w) / len(w)
             per[str(g)] = {"fetch_bytes": fa, "write_bytes": wa, "launches": len(f),
                            "traffic_bytes": 2.0 * fa + wa}
-            tot += 2.0 * fa + wa
-        out[k] = {"grids": per, "traffic_bytes": tot if ok else None}
+            tot += (2.0 * fa + wa) * len(f)
+        # per step: all launches' bytes over the count of the largest-grid (main) launch
+        nmain = per[str(max(grids))]["launches"] if ok and grids else 0
+        out[k] = {"grids": per, "traffic_bytes": tot / nmain if ok and nmain else None}
     print(json.dumps(out, indent=1))
 
 

@@ -831,7 +831,7 @@ struct sph_engine {
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,   \
-                     list_perm_pi, (stride > 0 && list_tbits) ? 1 : 0)
+                     list_perm_pi, mp ? 2 : ((stride > 0 && list_tbits) ? 1 : 0))
       if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
       else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
@@ -992,10 +992,7 @@ struct sph_engine {
     bin_q();
     blk = false;
     if (need_csr || !want_blk()) list_q(need_csr);
-    if (mp) {  // the half list's orientation of every pair, as of this build
-      if (nlocal)
-        hipLaunchKernelGGL(k_mp_orient, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, nlocal,
-                           off.p, nbr.p, xf.p);
+    if (mp) {  // (the CSR rows carry each pair's half-list orientation, k_neigh3)
       ov_ready = false;
       return;
     }

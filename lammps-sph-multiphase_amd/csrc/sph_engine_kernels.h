@@ -413,6 +413,19 @@ __device__ __forceinline__ double slab_gap(double v, int b, int c, double lo, do
 // record loads.  Hits are compacted in candidate order.  Modes: count | CSR fill | strided
 // fill (fixed-stride rows, the row's count in cnt, a row longer than stride raises *ovf);
 // perm_g > 0 stores a strided row chunk-transposed (tpos, stride a multiple of 4*perm_g).
+// the half list's owner of pair (i, j) (half_from_full_newton, neigh_derive.cpp:83-150):
+// an owned j if i < j, a ghost j if it lies above i in z, then y, then x
+__device__ __forceinline__ bool half_keep(int i, int j, int nlocal, const double4 &xi,
+                                          const double4 &xj) {
+  if (j < nlocal) return i < j;
+  if (xj.z < xi.z) return false;
+  if (xj.z == xi.z) {
+    if (xj.y < xi.y) return false;
+    if (xj.y == xi.y && xj.x < xi.x) return false;
+  }
+  return true;
+}
+
 template <int G, int U, bool FILL, bool NT1>
 __global__ void __launch_bounds__(256)
 k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
@@ -503,11 +516,17 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
-        // tbits (strided rows, several types): the neighbour's type rides in the entry's
-        // bits 28-30 (SPH_TBIT_SHIFT), so the pair passes need no type gather
-        if (hit && qq < cap)
-          row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] =
-              (int)xj[u].w | (tbits ? (tj[u] - 1) << SPH_TBIT_SHIFT : 0);
+        // tbits 1 (strided rows, several types): the neighbour's type rides in the entry's
+        // bits 28-30 (SPH_TBIT_SHIFT), so the pair passes need no type gather; tbits 2 (the
+        // multiphase engine's CSR rows): bit 31 = the pair is i's in the half list
+        // (k_mp_gather), frozen at this build as the reference's half list is
+        if (hit && qq < cap) {
+          const int j = (int)xj[u].w;
+          int ent = j;
+          if (tbits == 1) ent |= (tj[u] - 1) << SPH_TBIT_SHIFT;
+          if (tbits == 2 && half_keep(i, j, nlocal, xi, xj[u])) ent |= (int)0x80000000u;
+          row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] = ent;
+        }
         pos += __popcll(m);
       } else {
         n += hit ? 1 : 0;
@@ -537,16 +556,6 @@ static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__
 // (neigh_derive.cpp:124-131), and reverse-communicates the ghost's share.  The engine
 // reproduces that exactly for the setup step: derive the half list from the full one,
 // walk it with Newton-3 scatter, then fold ghost sums into their owners.
-__device__ __forceinline__ bool half_keep(int i, int j, int nlocal, const double4 &xi,
-                                          const double4 &xj) {
-  if (j < nlocal) return i < j;
-  if (xj.z < xi.z) return false;
-  if (xj.z == xi.z) {
-    if (xj.y < xi.y) return false;
-    if (xj.y == xi.y && xj.x < xi.x) return false;
-  }
-  return true;
-}
 
 template <bool FILL>
 static __global__ void k_half_from_full(int nlocal, const int *__restrict__ off,

@@ -19,8 +19,9 @@
 namespace sph {
 
 // Engine full lists carry the half list's orientation of each pair, frozen at the build as
-// the reference's half list is (k_mp_orient), in bit 31 of the entry: mask with MP_NMASK
-// (LAMMPS' NEIGHMASK idiom).  Lists from the pair-style layer never set it.
+// the reference's half list is, in bit 31 of the entry: mask with MP_NMASK
+// (LAMMPS' NEIGHMASK idiom; written by k_neigh3's fill).  Lists from the pair-style layer
+// never set it.
 constexpr int MP_NMASK = 0x7fffffff;
 
 struct MpCoefs {
@@ -128,10 +129,13 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
   }
 }
 
-// p = B (pow(rho/rho0, gamma) - rbackground), pair_sph_taitwater_multiphase.cpp:289-292
+// p = B (pow(rho/rho0, gamma) - rbackground), pair_sph_taitwater_multiphase.cpp:289-292.
+// pow(x, 1) == x exactly (C99 F.9.4.4), and gamma = 1 is the bubble_growth value: the
+// library pow runs only for other exponents
 __device__ __forceinline__ double mp_pressure(double B, double rho0, double gamma, double rbg,
                                               double rho) {
-  return B * (pow(rho / rho0, gamma) - rbg);
+  const double x = rho / rho0;
+  return B * ((gamma == 1.0 ? x : pow(x, gamma)) - rbg);
 }
 
 
@@ -397,27 +401,6 @@ __global__ void __launch_bounds__(256) k_mp_half(MpArgs a) {
 // whose image pair belongs to j's owner (evaluated there with the owner fresh and i's ghost
 // copy stale) -> j fresh, i stale.  fo[i].xyz and de[i] of the owned rows are overwritten
 // (fo.w = drho = 0: none of the styles has a drho term).
-__device__ __forceinline__ bool mp_half_keep(int i, int j, int nlocal, const double4 &xi,
-                                             const double4 &xj) {
-  if (j < nlocal) return i < j;
-  if (xj.z < xi.z) return false;
-  if (xj.z == xi.z) {
-    if (xj.y < xi.y) return false;
-    if (xj.y == xi.y && xj.x < xi.x) return false;
-  }
-  return true;
-}
-// set bit 31 of the full-list entries whose pair the half list gives to the row atom
-static __global__ void k_mp_orient(int n, int nlocal, const int *__restrict__ off,
-                                   int *__restrict__ nbr, const double4 *__restrict__ xf) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const double4 xi = xf[i];
-  for (int k = off[i]; k < off[i + 1]; k++) {
-    const int j = nbr[k];
-    if (mp_half_keep(i, j, nlocal, xi, xf[j])) nbr[k] = j | ~MP_NMASK;
-  }
-}
 template <class T>
 __device__ __forceinline__ T mp_sel(bool c, const T &a, const T &b) {
   return c ? a : b;
@@ -445,7 +428,7 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
     const double4 xj = a.xf[j], v4j = a.vel[j];
     const int tj = a.ty[j];
     const double mj = a.rm[j];
-    const bool own = jr < 0;  // (bit 31: the pair is i's in the half list, k_mp_orient)
+    const bool own = jr < 0;  // (bit 31: the pair is i's in the half list, k_neigh3)
     const bool gj = j >= a.nlocal;
     const bool fi = !(gj && !own), fj = !gj || !own;  // fresh or stale values (see above)
     const double rhoi = fi ? rFi : rSi;

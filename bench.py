@@ -439,6 +439,25 @@ def c2_pair_main(args, sph):
         ms["taitwater_list_reused"] = ctx.last_kernel_ms()
         return ms, time.perf_counter() - t0
 
+    # the calling pattern of a LAMMPS run with the sph/<style>/hip shim: every compute()
+    # restages the atoms (sph_hip_atoms) and stages its NeighList keyed by the build
+    # (sph_hip_list_keyed, key = neighbor->ncalls); a rebuild every `every` steps
+    nl_full, nl_half = sph.NeighList(foff, fnb), sph.NeighList(hoff, hnb)
+    every = 10
+
+    def lammps_step(k):
+        t0 = time.perf_counter()
+        key = k // every
+        ctx.atoms(N, 0, x, t, vest=v, rho=rho, e=e)
+        ctx.list_neighlist(sph.SPH_LIST_FULL, nl_full, key)
+        ctx.rhosum(r)
+        kms = ctx.last_kernel_ms()
+        ctx.atoms_rho(rho)     # (same step: the shim restages rho only)
+        ctx.list_neighlist(sph.SPH_LIST_HALF, nl_half, key)
+        ctx.taitwater(f, drho, de)
+        kms += ctx.last_kernel_ms()
+        return time.perf_counter() - t0, kms
+
     for _ in range(args.warmup):
         step()
     ctx.set_timing(True)
@@ -448,6 +467,12 @@ def c2_pair_main(args, sph):
         wall += w
         for k, val in ms.items():
             acc[k] = acc.get(k, 0.0) + val / args.steps
+    lw, lk = 0.0, 0.0
+    nls = max(args.steps, every) // every * every   # whole rebuild periods
+    for k in range(nls):
+        w, km = lammps_step(k)
+        lw += w
+        lk += km
     n_full, n_half = foff[-1] / N, hoff[-1] / N
     by = {"rhosum": 40 + 4 * n_half, "taitwater": 104 + 4 * n_half}
     by["taitwater_list_reused"] = by["taitwater"]
@@ -465,7 +490,15 @@ def c2_pair_main(args, sph):
                                "= 3.3; the taitwater call after a list upload includes the "
                                "reverse half-list build",
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "wall_ms_per_step_incl_pcie": wall / args.steps * 1e3},
+                   "wall_ms_per_step_incl_pcie": wall / args.steps * 1e3,
+                   "lammps_pattern": {
+                       "what": "per step: sph_hip_atoms + sph_hip_list_keyed(FULL) + rhosum, "
+                               "sph_hip_atoms_rho + sph_hip_list_keyed(HALF) + taitwater; lists "
+                               f"rebuilt every {every} steps (key = build)",
+                       "steps": nls,
+                       "wall_ms_per_step_incl_pcie": lw / nls * 1e3,
+                       "kernel_ms_per_step": lk / nls,
+                       "wall_over_kernel": lw * 1e3 / max(lk, 1e-12)}},
         "roofline": {"bound": "hbm", "kernel": "taitwater (half list: forward + reverse "
                                                "gather)",
                      "achieved": kern["taitwater"]["achieved_GBs"], "peak": PEAK_HBM_GBS,

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define SPH_HIP_ABI_VERSION 1
+#define SPH_HIP_ABI_VERSION 2
 
 #define SPH_HIP_OK 0
 #define SPH_HIP_EINVAL (-1)   /* bad argument / not configured */
@@ -94,12 +94,28 @@ int sph_hip_heatconduction_coeff(sph_hip_ctx *ctx, const double *alpha, const do
    not read them. */
 int sph_hip_atoms(sph_hip_ctx *ctx, int nlocal, int nghost, const double *x,
                   const double *vest, const double *rho, const double *e, const int *type);
+/* Restage rho only (nall values; x, vest, e, type, rmass, cv as last staged): the second
+   and later pair computes of one step under hybrid/overlay, after forward_comm_pair of the
+   density (the shim keys it on ntimestep + neighbor->ncalls + nlocal/nghost). */
+int sph_hip_atoms_rho(sph_hip_ctx *ctx, const double *rho);
 
 /* Stage a LAMMPS NeighList (list->inum, ilist, numneigh, firstneigh; NEIGHMASK bits are
    stripped).  kind = SPH_LIST_FULL (gather-only kernels, nothing written to ghosts) or
-   SPH_LIST_HALF (Newton-3 scatter onto j with fp64 atomics, like the reference). */
+   SPH_LIST_HALF (the reference's Newton-3 semantics: the j share of every pair, ghosts
+   included when newton_pair is on, is gathered through the reverse of the staged half list,
+   built once per upload; SPH_MPREV=0 scatters it with fp64 atomics instead).  Entries are
+   checked on the device (0 <= j < nall, ilist owned): SPH_HIP_EINVAL otherwise. */
 int sph_hip_list(sph_hip_ctx *ctx, int kind, int inum, const int *ilist,
                  const int *numneigh, const int *const *firstneigh);
+/* sph_hip_list with reuse (the device mirror keyed by the list build):
+   key >= 0 identifies the build (LAMMPS: neighbor->ncalls).  The context keeps one staged
+   list per kind, so hybrid/overlay sub-styles that alternate FULL and HALF lists each keep
+   theirs; a call whose (kind, key, inum) matches the staged list of that kind returns
+   without touching the host list (no copy, upload or check; the reverse list is kept).
+   Restaging atoms with a different nlocal/nghost drops every staged list.  key < 0 always
+   uploads (= sph_hip_list). */
+int sph_hip_list_keyed(sph_hip_ctx *ctx, int kind, int64_t key, int inum, const int *ilist,
+                       const int *numneigh, const int *const *firstneigh);
 /* Same, from a CSR list (row i = neigh[off[i]..off[i+1]) for owned atom i). */
 int sph_hip_list_csr(sph_hip_ctx *ctx, int kind, int inum, const int64_t *off,
                      const int *neigh);

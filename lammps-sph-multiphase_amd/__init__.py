@@ -107,6 +107,8 @@ EXPORTS = {
     "sph_hip_heatconduction_coeff": (_i, [_vp, _dp, _dp, _dp]),
     "sph_hip_atoms": (_i, [_vp, _i, _i, _dp, _vp, _vp, _vp, _ip]),
     "sph_hip_list": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "sph_hip_list_keyed": (_i, [_vp, _i, C.c_int64, _i, _vp, _vp, _vp]),
+    "sph_hip_atoms_rho": (_i, [_vp, _dp]),
     "sph_hip_list_csr": (_i, [_vp, _i, _i, _lp, _ip]),
     "sph_hip_rhosum": (_i, [_vp, _dp]),
     "sph_hip_taitwater": (_i, [_vp, _dp, _dp, _dp, _vp]),
@@ -196,6 +198,22 @@ class PhaseChangeParams(C.Structure):
 # ------------------------------------------------------------------------------------------
 # 1. Pair-style layer
 # ------------------------------------------------------------------------------------------
+class NeighList:
+    """A LAMMPS NeighList (ilist, numneigh, firstneigh) over one CSR array, built without a
+    per-row Python loop: firstneigh[i] points into `neigh` at off[i] (row i of owned atom i,
+    ilist = identity).  What the shim passes to sph_hip_list[_keyed]."""
+
+    def __init__(self, off, neigh):
+        off = np.asarray(off, dtype=np.int64)
+        self.neigh = np.ascontiguousarray(neigh if len(neigh) else np.zeros(1), dtype=np.int32)
+        self.inum = len(off) - 1
+        self.ilist = np.arange(self.inum, dtype=np.int32)
+        self.numneigh = np.diff(off).astype(np.int32)
+        self.ptrs = (self.neigh.ctypes.data + 4 * off[:-1]).astype(np.uint64)
+        if self.inum == 0:
+            self.ptrs = np.zeros(1, np.uint64)
+
+
 class PairContext:
     """One sph_hip_ctx: what the LAMMPS sph/<style>/hip Pair classes drive."""
 
@@ -249,14 +267,29 @@ class PairContext:
         neigh = np.ascontiguousarray(neigh if len(neigh) else np.zeros(1), dtype=np.int32)
         _chk(self.L.sph_hip_list_csr(self.h, kind, len(off) - 1, off, neigh))
 
-    def list_lammps(self, kind, ilist, numneigh, firstneigh_rows):
-        """LAMMPS NeighList form: ilist, numneigh (per atom), list of per-atom int32 rows."""
+    def list_lammps(self, kind, ilist, numneigh, firstneigh_rows, key=None):
+        """LAMMPS NeighList form: ilist, numneigh (per atom), list of per-atom int32 rows.
+        key (the list build, e.g. neighbor->ncalls): sph_hip_list_keyed, which reuses the
+        staged list of this kind when the key matches."""
         ilist = np.ascontiguousarray(ilist, dtype=np.int32)
         numneigh = np.ascontiguousarray(numneigh, dtype=np.int32)
         rows = [np.ascontiguousarray(r, dtype=np.int32) for r in firstneigh_rows]
         ptrs = (C.c_void_p * max(len(rows), 1))(*[r.ctypes.data for r in rows])
-        _chk(self.L.sph_hip_list(self.h, kind, len(ilist), ilist.ctypes.data,
-                                 numneigh.ctypes.data, C.cast(ptrs, C.c_void_p)))
+        if key is None:
+            _chk(self.L.sph_hip_list(self.h, kind, len(ilist), ilist.ctypes.data,
+                                     numneigh.ctypes.data, C.cast(ptrs, C.c_void_p)))
+        else:
+            _chk(self.L.sph_hip_list_keyed(self.h, kind, int(key), len(ilist), ilist.ctypes.data,
+                                           numneigh.ctypes.data, C.cast(ptrs, C.c_void_p)))
+
+    def atoms_rho(self, rho):
+        """Restage rho only (sph_hip_atoms_rho)."""
+        _chk(self.L.sph_hip_atoms_rho(self.h, np.ascontiguousarray(rho, dtype=np.float64)))
+
+    def list_neighlist(self, kind, nl, key=-1):
+        """Stage a NeighList (sph_hip_list_keyed; key < 0: always upload)."""
+        _chk(self.L.sph_hip_list_keyed(self.h, kind, int(key), nl.inum, nl.ilist.ctypes.data,
+                                       nl.numneigh.ctypes.data, nl.ptrs.ctypes.data))
 
     def rhosum(self, rho):
         _chk(self.L.sph_hip_rhosum(self.h, rho))

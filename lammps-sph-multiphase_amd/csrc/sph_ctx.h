@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdint>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "sph_kernels.h"
@@ -23,6 +25,15 @@ inline bool sph_rev_on() {
   return v;
 }
 
+// a neighbor list parked in the context while another kind is active (sph_hip_list_keyed)
+struct StagedList {
+  int kind = -1, inum = 0;
+  int64_t key = -1;
+  DBuf<int> ilist, off, nbr, rkey, rnbr, rown, roff;
+  std::vector<int> hoff, hilist;
+  bool rev_ok = false;
+};
+
 struct sph_hip_ctx {
   int device = 0, dim = 3, ntypes = 1, newton = 1;
   hipStream_t stream = nullptr;
@@ -31,10 +42,11 @@ struct sph_hip_ctx {
   bool have_rho = false, have_tait = false, have_heat = false;
   int tait_visc = SPH_VISC_MONAGHAN;
   int nlocal = 0, nghost = 0;
+  bool have_atoms = false;
   int list_kind = -1, inum = 0;
   DBuf<double4> xf, vr, fo;
-  DBuf<double> en, de, rho_out, virial;
-  DBuf<int> ty, ilist, off, nbr;
+  DBuf<double> en, de, rho_out, virial, raw;  // (raw: LAMMPS arrays as uploaded)
+  DBuf<int> ty, ilist, off, nbr, lbad;
   // multiphase styles (atom_style meso/multiphase): per-atom rmass and cv, own coefficients
   DBuf<double> rm, cv;
   DBuf<double4> cg, cgin;
@@ -53,6 +65,58 @@ struct sph_hip_ctx {
   std::vector<double> h1;
   std::vector<int> hoff, hnbr, hilist;
   bool coef_dirty = true;
+  // the active list's build key (-1: not reusable) and the parked lists, one per kind
+  int64_t list_key = -1;
+  StagedList parked[2];
+  void swap_active(StagedList &p) {
+    std::swap(list_kind, p.kind);
+    std::swap(inum, p.inum);
+    std::swap(list_key, p.key);
+    std::swap(ilist, p.ilist);
+    std::swap(off, p.off);
+    std::swap(nbr, p.nbr);
+    std::swap(rkey, p.rkey);
+    std::swap(rnbr, p.rnbr);
+    std::swap(rown, p.rown);
+    std::swap(roff, p.roff);
+    std::swap(hoff, p.hoff);
+    std::swap(hilist, p.hilist);
+    std::swap(rev_ok, p.rev_ok);
+  }
+  // make the kind-k list the active one: the active list is parked under its own kind,
+  // the kind-k slot's list (if any) becomes active; a slot's stale buffers are kept for reuse
+  void select_list(int k) {
+    if (list_kind == k) return;
+    if (list_kind >= 0) swap_active(parked[list_kind]);
+    swap_active(parked[k]);
+    if (parked[k].kind != k) {  // (what came back is not a kind-k list: an empty slot)
+      parked[k].kind = -1;
+      parked[k].key = -1;
+      parked[k].rev_ok = false;
+    }
+    if (list_kind != k) {
+      list_kind = k;
+      list_key = -1;
+      inum = 0;
+      rev_ok = false;
+    }
+  }
+  // every staged list stale (the atom set changed): restage before the next style call
+  void drop_lists() {
+    list_kind = -1;
+    list_key = -1;
+    rev_ok = false;
+    for (auto &p : parked) {
+      p.kind = -1;
+      p.key = -1;
+      p.rev_ok = false;
+    }
+  }
+  void release_lists() {
+    for (auto &p : parked)
+      for (DBuf<int> *b : {&p.ilist, &p.off, &p.nbr, &p.rkey, &p.rnbr, &p.rown, &p.roff})
+        b->release();
+  }
   // optional device timing of each style call's kernels (sph_hip_set_timing)
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

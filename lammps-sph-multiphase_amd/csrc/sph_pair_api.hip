@@ -7,6 +7,7 @@
 
 #include <cstdarg>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #include "sph_coef.h"
@@ -122,6 +123,9 @@ int sph_hip_destroy(sph_hip_ctx *c) {
   c->ilist.release();
   c->off.release();
   c->nbr.release();
+  c->release_lists();
+  c->lbad.release();
+  c->raw.release();
   c->rm.release();
   c->cv.release();
   c->cg.release();
@@ -170,6 +174,28 @@ int sph_hip_heatconduction_coeff(sph_hip_ctx *c, const double *alpha, const doub
   SPH_API_END
 }
 
+// LAMMPS' per-atom arrays (x, vest: nall*3; rho, e: nall; NULL = zeros) -> the gather
+// records, with the type range checked on the way (bad |= 1)
+static __global__ void k_pack_atoms(int nall, const double *__restrict__ x,
+                                    const double *__restrict__ v, const double *__restrict__ rho,
+                                    const double *__restrict__ e, const int *__restrict__ ty,
+                                    int ntypes, double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                    double *__restrict__ en, int *__restrict__ bad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nall) return;
+  xf[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
+  vr[i] = make_double4(v ? v[3 * i] : 0.0, v ? v[3 * i + 1] : 0.0, v ? v[3 * i + 2] : 0.0,
+                       rho ? rho[i] : 0.0);
+  en[i] = e ? e[i] : 0.0;
+  const int t = ty[i];
+  if (t < 1 || t > ntypes) atomicOr(bad, 1);
+}
+static __global__ void k_set_rho(int nall, const double *__restrict__ rho,
+                                 double4 *__restrict__ vr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nall) vr[i].w = rho[i];
+}
+
 int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const double *vest,
                   const double *rho, const double *e, const int *type) {
   SPH_API_BEGIN
@@ -177,69 +203,135 @@ int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const
               "sph_hip_atoms: bad argument");
   SPH_HIP_TRY(hipSetDevice(c->device));
   const size_t nall = (size_t)nlocal + nghost;
+  if (nlocal != c->nlocal || nghost != c->nghost) c->drop_lists();  // (indices refer to nall)
   c->nlocal = nlocal;
   c->nghost = nghost;
   c->have_mp_atoms = false;  // rmass/cv must be restaged for the new atom set
-  if (nall == 0) return SPH_HIP_OK;
-  for (size_t i = 0; i < nall; i++)
-    SPH_REQUIRE(type[i] >= 1 && type[i] <= c->ntypes, SPH_HIP_EINVAL,
-                "atom %zu has type %d outside [1,%d]", i, type[i], c->ntypes);
+  c->have_atoms = false;
+  if (nall == 0) {
+    c->have_atoms = true;
+    return SPH_HIP_OK;
+  }
+  // raw arrays up (one copy each), packed into the gather records on the device
   c->xf.reserve(nall);
   c->vr.reserve(nall);
   c->en.reserve(nall);
   c->ty.reserve(nall);
-  c->h4.resize(nall);
-  for (size_t i = 0; i < nall; i++)
-    c->h4[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
-  SPH_HIP_TRY(hipMemcpyAsync(c->xf.p, c->h4.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
+  c->raw.reserve(8 * nall);
+  c->lbad.reserve(1);
+  double *const rx = c->raw.p, *const rv = rx + 3 * nall, *const rr = rv + 3 * nall,
+               *const re = rr + nall;
+  SPH_HIP_TRY(hipMemcpyAsync(rx, x, 3 * nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (vest) SPH_HIP_TRY(hipMemcpyAsync(rv, vest, 3 * nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (rho) SPH_HIP_TRY(hipMemcpyAsync(rr, rho, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (e) SPH_HIP_TRY(hipMemcpyAsync(re, e, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
   SPH_HIP_TRY(hipMemcpyAsync(c->ty.p, type, nall * sizeof(int), hipMemcpyHostToDevice, c->stream));
-  std::vector<double4> hv(nall);
-  for (size_t i = 0; i < nall; i++)
-    hv[i] = make_double4(vest ? vest[3 * i] : 0.0, vest ? vest[3 * i + 1] : 0.0,
-                         vest ? vest[3 * i + 2] : 0.0, rho ? rho[i] : 0.0);
-  SPH_HIP_TRY(hipMemcpyAsync(c->vr.p, hv.data(), nall * sizeof(double4), hipMemcpyHostToDevice, c->stream));
-  c->h1.assign(nall, 0.0);
-  if (e)
-    for (size_t i = 0; i < nall; i++) c->h1[i] = e[i];
-  SPH_HIP_TRY(hipMemcpyAsync(c->en.p, c->h1.data(), nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  // staging vectors must outlive the async copies
+  SPH_HIP_TRY(hipMemsetAsync(c->lbad.p, 0, sizeof(int), c->stream));
+  hipLaunchKernelGGL(k_pack_atoms, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, c->stream,
+                     (int)nall, rx, vest ? rv : nullptr, rho ? rr : nullptr, e ? re : nullptr,
+                     c->ty.p, c->ntypes, c->xf.p, c->vr.p, c->en.p, c->lbad.p);
+  int bad = 0;
+  SPH_HIP_TRY(hipMemcpyAsync(&bad, c->lbad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  if (bad)
+    for (size_t i = 0; i < nall; i++)  // (the culprit, for the message)
+      SPH_REQUIRE(type[i] >= 1 && type[i] <= c->ntypes, SPH_HIP_EINVAL,
+                  "atom %zu has type %d outside [1,%d]", i, type[i], c->ntypes);
+  c->have_atoms = true;
+  SPH_API_END
+}
+
+int sph_hip_atoms_rho(sph_hip_ctx *c, const double *rho) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && rho, SPH_HIP_EINVAL, "sph_hip_atoms_rho: bad argument");
+  SPH_REQUIRE(c->have_atoms, SPH_HIP_EINVAL, "sph_hip_atoms_rho: no atoms staged");
+  SPH_HIP_TRY(hipSetDevice(c->device));
+  const size_t nall = (size_t)c->nlocal + c->nghost;
+  if (nall == 0) return SPH_HIP_OK;
+  c->raw.reserve(8 * nall);
+  SPH_HIP_TRY(hipMemcpyAsync(c->raw.p, rho, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_set_rho, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, c->stream,
+                     (int)nall, c->raw.p, c->vr.p);
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   SPH_API_END
 }
 
-static void upload_list(sph_hip_ctx *c, int kind, int inum) {
+// bad[0] |= 1 for a neighbor index outside [0, nall), |= 2 for an ilist entry that is not
+// an owned atom (the kernels index atom arrays with both: checked once per upload, on the
+// device, instead of a host loop over every entry)
+static __global__ void k_list_check(long tot, const int *__restrict__ nbr, int nall, int inum,
+                                    const int *__restrict__ ilist, int nlocal,
+                                    int *__restrict__ bad) {
+  int f = 0;
+  for (long k = blockIdx.x * (long)blockDim.x + threadIdx.x; k < tot;
+       k += (long)gridDim.x * blockDim.x) {
+    const int j = nbr[k];
+    if (j < 0 || j >= nall) f |= 1;
+  }
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < inum; r += gridDim.x * blockDim.x) {
+    const int i = ilist[r];
+    if (i < 0 || i >= nlocal) f |= 2;
+  }
+  if (f) atomicOr(bad, f);
+}
+
+static void upload_list(sph_hip_ctx *c, int kind, int inum, int64_t key) {
   const size_t tot = (size_t)c->hoff[inum];
   SPH_REQUIRE(tot < (size_t)0x7fffffff, SPH_HIP_EOVERFLOW, "neighbor list too long (%zu)", tot);
-  const size_t nall = (size_t)c->nlocal + c->nghost;
-  for (size_t k = 0; k < tot; k++)
-    SPH_REQUIRE(c->hnbr[k] >= 0 && (size_t)c->hnbr[k] < nall, SPH_HIP_EINVAL,
-                "neighbor index %d outside [0,%zu)", c->hnbr[k], nall);
-  for (int r = 0; r < inum; r++)
-    SPH_REQUIRE(c->hilist[r] >= 0 && c->hilist[r] < c->nlocal, SPH_HIP_EINVAL,
-                "ilist[%d] = %d is not an owned atom", r, c->hilist[r]);
+  const int nall = c->nlocal + c->nghost;
+  c->list_key = -1;  // (until the upload is checked)
   c->off.reserve(inum + 1);
   c->nbr.reserve(tot > 0 ? tot : 1);
   c->ilist.reserve(inum > 0 ? inum : 1);
+  c->lbad.reserve(1);
   SPH_HIP_TRY(hipMemcpyAsync(c->off.p, c->hoff.data(), (inum + 1) * sizeof(int), hipMemcpyHostToDevice, c->stream));
   if (tot) SPH_HIP_TRY(hipMemcpyAsync(c->nbr.p, c->hnbr.data(), tot * sizeof(int), hipMemcpyHostToDevice, c->stream));
   if (inum) SPH_HIP_TRY(hipMemcpyAsync(c->ilist.p, c->hilist.data(), inum * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  SPH_HIP_TRY(hipMemsetAsync(c->lbad.p, 0, sizeof(int), c->stream));
+  if (tot || inum) {
+    const long work = std::max<long>((long)tot, inum);
+    const unsigned grid = (unsigned)std::min<long>((work + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_list_check, dim3(grid), dim3(256), 0, c->stream, (long)tot, c->nbr.p,
+                       nall, inum, c->ilist.p, c->nlocal, c->lbad.p);
+  }
+  int bad = 0;
+  SPH_HIP_TRY(hipMemcpyAsync(&bad, c->lbad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   c->list_kind = kind;
   c->inum = inum;
   c->rev_ok = false;
+  if (bad) {
+    c->list_kind = -1;  // (nothing may run on it)
+    SPH_REQUIRE(!(bad & 1), SPH_HIP_EINVAL, "neighbor index outside [0,%d)", nall);
+    SPH_REQUIRE(false, SPH_HIP_EINVAL, "ilist holds an index that is not an owned atom");
+  }
+  c->list_key = key;
 }
 
 int sph_hip_list(sph_hip_ctx *c, int kind, int inum, const int *ilist, const int *numneigh,
                  const int *const *firstneigh) {
+  return sph_hip_list_keyed(c, kind, -1, inum, ilist, numneigh, firstneigh);
+}
+
+int sph_hip_list_keyed(sph_hip_ctx *c, int kind, int64_t key, int inum, const int *ilist,
+                       const int *numneigh, const int *const *firstneigh) {
   SPH_API_BEGIN
-  SPH_REQUIRE(c && (inum == 0 || (ilist && numneigh && firstneigh)), SPH_HIP_EINVAL,
+  SPH_REQUIRE(c && inum >= 0 && (inum == 0 || (ilist && numneigh && firstneigh)), SPH_HIP_EINVAL,
               "sph_hip_list: bad argument");
   SPH_REQUIRE(kind == SPH_LIST_FULL || kind == SPH_LIST_HALF, SPH_HIP_EINVAL, "bad list kind");
   SPH_HIP_TRY(hipSetDevice(c->device));
+  c->select_list(kind);
+  size_t tot = 0;
+  for (int r = 0; r < inum; r++) tot += (size_t)numneigh[ilist[r]];
+  // reuse: same build, same rows and entry count (two lists of one kind from one build --
+  // a pair style's and a fix's full list -- are copies of each other in LAMMPS)
+  if (key >= 0 && c->list_key == key && c->inum == inum && !c->hoff.empty() &&
+      (size_t)c->hoff[inum] == tot)
+    return SPH_HIP_OK;
   const int NEIGHMASK = 0x3FFFFFFF;  // src/lmptype.h / neighbor.h: SBBITS = 30
   c->hoff.resize(inum + 1);
   c->hilist.assign(ilist, ilist + inum);
-  size_t tot = 0;
+  tot = 0;
   for (int r = 0; r < inum; r++) {
     c->hoff[r] = (int)tot;
     tot += (size_t)numneigh[ilist[r]];
@@ -251,7 +343,7 @@ int sph_hip_list(sph_hip_ctx *c, int kind, int inum, const int *ilist, const int
     const int *jl = firstneigh[i];
     for (int k = 0; k < numneigh[i]; k++) c->hnbr[c->hoff[r] + k] = jl[k] & NEIGHMASK;
   }
-  upload_list(c, kind, inum);
+  upload_list(c, kind, inum, key);
   SPH_API_END
 }
 
@@ -261,13 +353,14 @@ int sph_hip_list_csr(sph_hip_ctx *c, int kind, int inum, const int64_t *off, con
               "sph_hip_list_csr: bad argument");
   SPH_REQUIRE(kind == SPH_LIST_FULL || kind == SPH_LIST_HALF, SPH_HIP_EINVAL, "bad list kind");
   SPH_HIP_TRY(hipSetDevice(c->device));
+  c->select_list(kind);
   c->hoff.resize(inum + 1);
   c->hilist.resize(inum);
   for (int r = 0; r <= inum; r++) c->hoff[r] = (int)off[r];
   for (int r = 0; r < inum; r++) c->hilist[r] = r;
   const size_t tot = (size_t)off[inum];
   c->hnbr.assign(neigh, neigh + tot);
-  upload_list(c, kind, inum);
+  upload_list(c, kind, inum, -1);
   SPH_API_END
 }
 

@@ -17,6 +17,7 @@
 #include "force.h"
 #include "memory.h"
 #include "neigh_list.h"
+#include "neighbor.h"
 #include "sph_hip.h"
 #include "update.h"
 
@@ -24,6 +25,15 @@ using namespace LAMMPS_NS;
 
 namespace {
 sph_hip_ctx *g_ctx = NULL;
+// what the context's atoms were staged at: a later compute of the same step (hybrid/overlay
+// sub-styles after forward_comm_pair) restages rho only.  Borders run only with a list
+// build, so (ntimestep, neighbor->ncalls, nlocal, nghost) pins the atom set and positions.
+struct StageKey {
+  bigint step, ncalls;
+  int nlocal, nghost;
+  bool mp;
+};
+StageKey g_key = {-1, -1, -1, -1, false};
 }
 
 sph_hip_ctx *LAMMPS_NS::sph_hip_rank_ctx(LAMMPS *lmp) {
@@ -50,19 +60,30 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
   Atom *atom = lmp->atom;
   const int nlocal = atom->nlocal, nghost = atom->nghost;
   const int nall = nlocal + nghost;
-  // x and vest are memory->create 2-D arrays: contiguous nmax*3 backing (memory.h:124-137)
+  const StageKey key = {lmp->update->ntimestep, lmp->neighbor->ncalls, nlocal, nghost,
+                        multiphase};
+  if (key.step == g_key.step && key.ncalls == g_key.ncalls && key.nlocal == g_key.nlocal &&
+      key.nghost == g_key.nghost && (g_key.mp || !multiphase) && nall && atom->rho) {
+    sph_hip_check(lmp, sph_hip_atoms_rho(ctx, atom->rho), "sph_hip_atoms_rho");
+  } else {
+    // x and vest are memory->create 2-D arrays: contiguous nmax*3 backing (memory.h:124-137)
+    sph_hip_check(lmp,
+                  sph_hip_atoms(ctx, nlocal, nghost, nall ? &atom->x[0][0] : NULL,
+                                (nall && atom->vest) ? &atom->vest[0][0] : NULL, atom->rho,
+                                atom->e, atom->type),
+                  "sph_hip_atoms");
+    if (multiphase)
+      sph_hip_check(lmp, sph_hip_atoms_multiphase(ctx, atom->rmass, atom->cv),
+                    "sph_hip_atoms_multiphase");
+    g_key = key;
+  }
+  // the list build is the key (neighbor->ncalls, neighbor.cpp:1423): between rebuilds the
+  // staged device copy of this kind is reused -- no host copy, no upload, and a half list
+  // keeps its reverse list; sub-styles of hybrid/overlay on the other kind keep theirs
   sph_hip_check(lmp,
-                sph_hip_atoms(ctx, nlocal, nghost, nall ? &atom->x[0][0] : NULL,
-                              (nall && atom->vest) ? &atom->vest[0][0] : NULL, atom->rho,
-                              atom->e, atom->type),
-                "sph_hip_atoms");
-  if (multiphase)
-    sph_hip_check(lmp, sph_hip_atoms_multiphase(ctx, atom->rmass, atom->cv),
-                  "sph_hip_atoms_multiphase");
-  sph_hip_check(lmp,
-                sph_hip_list(ctx, kind, list->inum, list->ilist, list->numneigh,
-                             list->firstneigh),
-                "sph_hip_list");
+                sph_hip_list_keyed(ctx, kind, (int64_t)lmp->neighbor->ncalls, list->inum,
+                                   list->ilist, list->numneigh, list->firstneigh),
+                "sph_hip_list_keyed");
 }
 
 namespace {

@@ -50,7 +50,7 @@ def test_bindings_cover_header(sph_amd):
 
 
 def test_abi_version(sph_amd):
-    assert sph_amd.load().sph_hip_abi_version() == 1
+    assert sph_amd.load().sph_hip_abi_version() == 2
 
 
 def test_no_silent_cpu_fallback(sph_amd):

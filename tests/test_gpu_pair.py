@@ -150,3 +150,64 @@ def test_edge_cases(gpu, sph_amd):
     assert ei.value.code == -1
     with pytest.raises(sph_amd.HipError):
         ctx.list_csr(sph_amd.SPH_LIST_FULL, np.array([0, 1], np.int64), np.array([7], np.int32))
+
+
+def test_keyed_list_reuse(gpu, sph_amd):
+    """sph_hip_list_keyed (the LAMMPS shim's call, key = neighbor->ncalls): a FULL and a HALF
+    list of one build are both kept; calls with a known key skip the host rows entirely
+    (corrupted rows give bit-identical results), a new key re-uploads, and restaging atoms
+    with another ghost count drops every staged list (SURVEY 8(b) device mirrors)."""
+    s = c2_system(6)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    n, nall = s.n, P["g"].nall
+
+    def rows_of(off, nb, bad=False):
+        numneigh = np.diff(off).astype(np.int32)
+        rows = [np.zeros(int(numneigh[i]), np.int32) if bad else nb[off[i]:off[i + 1]].astype(np.int32)
+                for i in range(n)]
+        return np.arange(n, dtype=np.int32), numneigh, rows
+
+    def rho_full(key, bad=False):
+        ctx.list_lammps(sph_amd.SPH_LIST_FULL, *rows_of(P["foff"], P["fnb"], bad), key=key)
+        return ctx.rhosum(np.zeros(nall)).copy()
+
+    def tait_half(key, bad=False):
+        ctx.list_lammps(sph_amd.SPH_LIST_HALF, *rows_of(P["hoff"], P["hnb"], bad), key=key)
+        f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+        ctx.taitwater(f, drho, de)
+        return f
+
+    ctx = _ctx(sph_amd, s, ph, P)
+    rho1 = rho_full(5)
+    f1 = tait_half(5)
+    assert rel_err(rho1[:n], po.rhosum(3, P["g"], 1, s.mass, ph.rhosum_cut, P["foff"], P["fnb"])) < 1e-13
+    wf, _, _ = oracle_forces(s, ph, P, reverse=False)
+    assert rel_err(f1, wf) < TOL
+    # same build: both kinds reused, the (corrupted) host rows are never read
+    assert np.array_equal(rho_full(5, bad=True), rho1)
+    assert np.array_equal(tait_half(5, bad=True), f1)
+    # a new build re-uploads
+    assert np.array_equal(rho_full(6), rho1)
+    with pytest.raises(sph_amd.HipError):
+        ctx.list_lammps(sph_amd.SPH_LIST_FULL, np.arange(n, dtype=np.int32),
+                        np.ones(n, np.int32), [np.array([nall + 3], np.int32)] * n, key=7)
+    # rho-only restage (the later computes of one step): equal to a full restage
+    g = P["g"]
+    rho2 = P["rho_all"] * (1.0 + 0.01 * np.sin(np.arange(nall)))
+    ctx.atoms_rho(rho2)
+    f_rho = tait_half(5)
+    ref = sph_amd.PairContext(s.dim, s.ntypes, 1)
+    ref.atoms(g.nlocal, g.nghost, g.x, g.type, vest=P["vest_all"], rho=rho2, e=P["e_all"])
+    ref.taitwater_coeff(ph.rho0, ph.c0, ph.c0 * ph.c0 * ph.rho0 / 7.0, ph.visc, ph.tait_cut,
+                        s.mass, morris=ph.morris)
+    ref.list_csr(sph_amd.SPH_LIST_HALF, P["hoff"], P["hnb"])
+    f_ref, d_ref, e_ref = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    ref.taitwater(f_ref, d_ref, e_ref)
+    assert rel_err(f_rho, f_ref) < 1e-14 and not np.array_equal(f_rho, f1)
+    ref.close()
+    # another atom count drops the staged lists: a style call needs a restaged list
+    ctx.atoms(g.nlocal, g.nghost - 1, g.x[:-1], g.type[:-1], vest=P["vest_all"][:-1],
+              rho=P["rho_all"][:-1], e=P["e_all"][:-1])
+    with pytest.raises(sph_amd.HipError):
+        ctx.rhosum(np.zeros(nall))

@@ -7,7 +7,7 @@ import sys
 
 
 FAMILIES = ["k_blk_force", "k_blk_rhosum", "k_blk_build", "k_row2_force", "k_row2_rhosum",
-            "k_bin_force", "k_bin_rhosum", "k_bin_neigh", "k_force", "k_rhosum", "k_neigh"]
+            "k_bin_force", "k_bin_rhosum", "k_bin_neigh", "k_blk_neigh", "k_force", "k_rhosum", "k_neigh"]
 
 
 def family(name):

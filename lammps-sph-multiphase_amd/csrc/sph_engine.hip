@@ -124,6 +124,7 @@ struct sph_engine {
   MpCoefs *dm = nullptr;
   DBuf<double> rm, cvv, rho_tmp, dmass, xbuf, xbuf2, rhoS, rhoF;
   DBuf<double4> cg, cgS, cgF;
+  DBuf<double4> recA, recK, recF, recS;  // k_mp_gather's packed records (k_mp_pack_rec)
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
   sph_phasechange_params pcp{};
@@ -1326,7 +1327,12 @@ struct sph_engine {
       }
       if (cdue) {
         a.cg = cg.p;
+        recA.reserve(nall);  // (free until the force pass packs its records)
+        hipLaunchKernelGGL(k_mp_pack_sigma, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vr.p,
+                           rm.p, recA.p);
+        a.xs = recA.p;
         hipLaunchKernelGGL(k_mp_colorgradient<8>, mp_rows(n), dim3(256), 0, s, a);
+        a.xs = nullptr;
       }
     }
     // the fresh version: the owned atoms' new values, forwarded to the ghosts
@@ -1354,6 +1360,17 @@ struct sph_engine {
     h.cgF = cF;
     h.fo = fo.p;
     h.de = de.p;
+    recA.reserve(nall);
+    recK.reserve(nall);
+    recF.reserve(nall);
+    recS.reserve(nall);
+    hipLaunchKernelGGL(k_mp_pack_rec, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vel.p,
+                       rm.p, en.p, cvv.p, rF, rhoS.p, cF, cgS.p, mpc.heat_on ? 1 : 0, recA.p,
+                       recK.p, recF.p, recS.p);
+    h.pA = recA.p;
+    h.pK = recK.p;
+    h.pF = recF.p;
+    h.pS = recS.p;
     const int sel = (mpc.tait_on ? 1 : 0) | (mpc.st_on ? 2 : 0) | (mpc.heat_on ? 4 : 0);
     switch (sel) {
 #define SPH_MPG(k, T, S, H) \
@@ -1753,7 +1770,7 @@ int sph_engine_destroy(sph_engine *e) {
                   &e->xbuf2})
     b->release();
   for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
-  for (auto *b : {&e->cg, &e->cgS, &e->cgF}) b->release();
+  for (auto *b : {&e->cg, &e->cgS, &e->cgF, &e->recA, &e->recK, &e->recF, &e->recS}) b->release();
   if (e->dm) (void)hipFree(e->dm);
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,

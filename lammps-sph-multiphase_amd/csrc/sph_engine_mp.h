@@ -65,6 +65,35 @@ static __global__ void k_mp_snap(int n, const double4 *__restrict__ vr,
   rho[i] = vr[i].w;
   cgo[i] = cg[i];
 }
+// k_mp_gather's per-atom records, so a neighbour costs four loads instead of ten scattered
+// ones: A = (x, y, z, rmass), K = (v, T = e/cv [heat]), F / S = (colorgradient, rho) in the
+// fresh / stale version (the gather picks one per pair, see k_mp_gather)
+static __global__ void k_mp_pack_rec(int nall, const double4 *__restrict__ xf,
+                                     const double4 *__restrict__ vel, const double *__restrict__ rm,
+                                     const double *__restrict__ en, const double *__restrict__ cv,
+                                     const double *__restrict__ rhoF, const double *__restrict__ rhoS,
+                                     const double4 *__restrict__ cgF, const double4 *__restrict__ cgS,
+                                     int heat, double4 *__restrict__ A, double4 *__restrict__ K,
+                                     double4 *__restrict__ F, double4 *__restrict__ S) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nall) return;
+  const double4 x = xf[i], v = vel[i], cf = cgF[i], cs = cgS[i];
+  A[i] = make_double4(x.x, x.y, x.z, rm[i]);
+  K[i] = make_double4(v.x, v.y, v.z, heat ? en[i] / cv[i] : 0.0);  // (sph_energy2t)
+  F[i] = make_double4(cf.x, cf.y, cf.z, rhoF[i]);
+  S[i] = make_double4(cs.x, cs.y, cs.z, rhoS[i]);
+}
+
+// colorgradient's records: (x, y, z, sigma = rho / rmass), pair_sph_colorgradient.cpp:139, 173
+static __global__ void k_mp_pack_sigma(int nall, const double4 *__restrict__ xf,
+                                       const double4 *__restrict__ vr,
+                                       const double *__restrict__ rm, double4 *__restrict__ xs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nall) return;
+  const double4 x = xf[i];
+  xs[i] = make_double4(x.x, x.y, x.z, vr[i].w / rm[i]);
+}
+
 // the fresh version of the ghosts from their owners (one brick)
 static __global__ void k_mp_fwd_fresh(int nghost, int nlocal, const int *__restrict__ gowner,
                                       double *__restrict__ rho, double4 *__restrict__ cg) {

@@ -95,6 +95,11 @@ struct MpArgs {
   const double4 *vel;
   const double *rhoS, *rhoF;
   const double4 *cgS, *cgF;
+  // ... packed per atom (k_mp_pack_rec): (x, rmass), (v, T), (cg, rho) fresh / stale
+  const double4 *pA, *pK, *pF, *pS;
+  // colorgradient: (x, y, z, sigma = rho / rmass) per atom, rho as it stands (nullptr: the
+  // kernel reads xf, vr, rm)
+  const double4 *xs;
 };
 
 template <int G>
@@ -205,13 +210,13 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
   const MpCoefs *c = a.mc;
   const int nt1 = c->ntypes + 1;
   const int i = a.ilist ? a.ilist[row] : row;
-  const double4 xi = a.xf[i];
+  const double4 xi = a.xs ? a.xs[i] : a.xf[i];
   const int it = a.ty[i];
-  const double sigmai = a.vr[i].w / a.rm[i];
+  const double sigmai = a.xs ? xi.w : a.vr[i].w / a.rm[i];
   double gx = 0.0, gy = 0.0, gz = 0.0;
   for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
     const int j = a.nbr[k] & MP_NMASK;
-    const double4 xj = a.xf[j];
+    const double4 xj = a.xs ? a.xs[j] : a.xf[j];
     const int jt = a.ty[j];
     const int p = it * nt1 + jt;
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
@@ -222,7 +227,7 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
     double wfd;
     if (a.dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih;
     else wfd = quintic_dw(2, r * ih) * ih * ih * ih;
-    const double sigmaj = a.vr[j].w / a.rm[j];
+    const double sigmaj = a.xs ? xj.w : a.vr[j].w / a.rm[j];
     const double dphi = -wfd * c->calpha[p] / (sigmaj * sigmaj) * sigmai;
     gx += dphi * (dx / r);
     gy += dphi * (dy / r);
@@ -414,25 +419,27 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
   const MpCoefs *c = a.mc;
   const int dim = a.dim;
   const int i = a.ilist ? a.ilist[row] : row;
-  const double4 xi = a.xf[i], v4i = a.vel[i];
+  // packed records (k_mp_pack_rec): .w of A = rmass, of K = T, of F / S = rho
+  const double4 xi = a.pA[i], v4i = a.pK[i];
   const int ti = a.ty[i];
-  const double mi = a.rm[i];
-  const double Ti = HEAT ? a.en[i] / a.cv[i] : 0.0;  // sph_energy2t
-  const double rFi = a.rhoF[i], rSi = a.rhoS[i];
-  const double4 cFi = SURF ? a.cgF[i] : make_double4(0, 0, 0, 0);
-  const double4 cSi = SURF ? a.cgS[i] : make_double4(0, 0, 0, 0);
+  const double mi = xi.w;
+  const double Ti = v4i.w;
+  const double4 cFi = a.pF[i], cSi = a.pS[i];
+  const double rFi = cFi.w, rSi = cSi.w;
   double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
   for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
     const int jr = a.nbr[k];
     const int j = jr & MP_NMASK;
-    const double4 xj = a.xf[j], v4j = a.vel[j];
-    const int tj = a.ty[j];
-    const double mj = a.rm[j];
     const bool own = jr < 0;  // (bit 31: the pair is i's in the half list, k_neigh3)
     const bool gj = j >= a.nlocal;
     const bool fi = !(gj && !own), fj = !gj || !own;  // fresh or stale values (see above)
+    const double4 xj = a.pA[j];
+    const double4 v4j = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
+    const double4 cj = (fj ? a.pF : a.pS)[j];  // (colorgradient, rho) of j as used here
+    const int tj = a.ty[j];
+    const double mj = xj.w;
     const double rhoi = fi ? rFi : rSi;
-    const double rhoj = fj ? a.rhoF[j] : a.rhoS[j];
+    const double rhoj = cj.w;
     const double sg = own ? 1.0 : -1.0;
     // the pair's row atom (p) and neighbour (q) in the half list
     const double4 xp = mp_sel(own, xi, xj), xq = mp_sel(own, xj, xi);
@@ -452,7 +459,6 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
     }
     if (SURF) {
       const double4 ci = fi ? cFi : cSi;
-      const double4 cj = fj ? a.cgF[j] : a.cgS[j];
       const double4 cp = mp_sel(own, ci, cj), cq = mp_sel(own, cj, ci);
       double3 F;
       if (mp_surf_pair(c, dim, xp, tp, mp / rp, cp, st_abs(dim, cp), xq, tq, mq / rq, cq, F)) {
@@ -462,7 +468,7 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
       }
     }
     if (HEAT) {
-      const double Tj = a.en[j] / a.cv[j];
+      const double Tj = v4j.w;
       double d;
       // de_p += deltaE m_q, de_q -= deltaE m_p (pair_sph_heatconduction_phasechange.cpp:132-136)
       if (mp_heat_pair(c, dim, xp, tp, rp, own ? Ti : Tj, xq, tq, rq, own ? Tj : Ti, d))

@@ -168,6 +168,7 @@ struct sph_hip_ctx {
   }
   void upload_mp() {
     if (!mp_dirty) return;
+    mp_inverses(hm);
     SPH_HIP_TRY(hipMemcpyAsync(dm, &hm, sizeof(MpCoefs), hipMemcpyHostToDevice, stream));
     mp_dirty = false;
   }

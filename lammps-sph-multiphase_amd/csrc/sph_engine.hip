@@ -1748,6 +1748,7 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     SPH_HIP_TRY(hipMemcpy(e->dc, &e->hc, sizeof(Coefs), hipMemcpyHostToDevice));
     if (e->mp) {
       SPH_HIP_TRY(hipMalloc(&e->dm, sizeof(MpCoefs)));
+      mp_inverses(e->hm);
       SPH_HIP_TRY(hipMemcpy(e->dm, &e->hm, sizeof(MpCoefs), hipMemcpyHostToDevice));
     }
     SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));

@@ -38,7 +38,30 @@ struct MpCoefs {
   double calpha[NT2], ccut[NT2], ccutsq[NT2];
   // surfacetension: h = cut[it][jt]
   double scut[NT2], scutsq[NT2];
+  // 1/h of every style and 1/rho0 (mp_inverses: the reference's own 1.0/h, taken once)
+  double rcut_inv[NT2], tcut_inv[NT2], hcut_inv[NT2], ccut_inv[NT2], scut_inv[NT2];
+  double rho0_inv[MAXT + 1];
 };
+
+// the reciprocal tables of MpCoefs from its cut / rho0 tables (host, before every upload)
+inline void mp_inverses(MpCoefs &m) {
+  auto inv = [](double h) { return h != 0.0 ? 1.0 / h : 0.0; };
+  for (int k = 0; k < NT2; k++) {
+    m.rcut_inv[k] = inv(m.rcut[k]);
+    m.tcut_inv[k] = inv(m.tcut[k]);
+    m.hcut_inv[k] = inv(m.hcut[k]);
+    m.ccut_inv[k] = inv(m.ccut[k]);
+    m.scut_inv[k] = inv(m.scut[k]);
+  }
+  for (int t = 0; t <= MAXT; t++) m.rho0_inv[t] = inv(m.rho0[t]);
+}
+
+// 1/b for the pair terms' divisions: v_rcp_f64 seed + one Newton step (~1 ulp; the fp64
+// IEEE division sequence costs ~3x the issue slots, and the 1e-10 parity bar is kept)
+__device__ __forceinline__ double mp_rcp(double b) {
+  const double y = __builtin_amdgcn_rcp(b);
+  return fma(y, fma(-b, y, 1.0), y);
+}
 
 // Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r).  The reference's pow(x, n) with
 // small integer n are evaluated as products (a few ulp apart from libm pow; the golden
@@ -121,7 +144,7 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
     if (rsq < c->rcutsq[it * nt1 + jt]) {
-      const double ih = 1.0 / c->rcut[it * nt1 + jt];
+      const double ih = c->rcut_inv[it * nt1 + jt];
       const double r = sqrt(rsq) * ih;
       acc += (dim == 3) ? quintic_w(3, r) * ih * ih * ih : quintic_w(2, r) * ih * ih;
     }
@@ -138,8 +161,8 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
 // pow(x, 1) == x exactly (C99 F.9.4.4), and gamma = 1 is the bubble_growth value: the
 // library pow runs only for other exponents
 __device__ __forceinline__ double mp_pressure(double B, double rho0, double gamma, double rbg,
-                                              double rho) {
-  const double x = rho / rho0;
+                                              double rho) {  // (rho0 = 1/rho0)
+  const double x = rho * rho0;  // (rho0: 1/rho0 from the table)
   return B * ((gamma == 1.0 ? x : pow(x, gamma)) - rbg);
 }
 
@@ -157,18 +180,18 @@ __device__ __forceinline__ bool mp_tait_pair(const MpCoefs *c, int dim, double4 
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
   const double rsq = dx * dx + dy * dy + dz * dz;
   if (!(rsq < c->tcutsq[p])) return false;
-  const double ih = 1.0 / c->tcut[p];
+  const double ih = c->tcut_inv[p];
   const double r = sqrt(rsq);
   double wfd;
-  if (dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih / r;
-  else wfd = quintic_dw(2, r * ih) * ih * ih * ih / r;
+  if (dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih * mp_rcp(r);
+  else wfd = quintic_dw(2, r * ih) * ih * ih * ih * mp_rcp(r);
   const double rhoi = vi.w, rhoj = vj.w;
-  const double Vi = mi / rhoi, Vj = mj / rhoj;
+  const double Vi = mi * mp_rcp(rhoi), Vj = mj * mp_rcp(rhoj);
   const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
-  const double pi = mp_pressure(c->B[it], c->rho0[it], c->gamma[it], c->rbg[it], rhoi);
+  const double pi = mp_pressure(c->B[it], c->rho0_inv[it], c->gamma[it], c->rbg[it], rhoi);
   // reference quirk kept: p_j with gamma[itype] (pair_sph_taitwater_multiphase.cpp:148)
-  const double pj = mp_pressure(c->B[jt], c->rho0[jt], c->gamma[it], c->rbg[jt], rhoj);
-  const double pij = (rhoj * pi + rhoi * pj) / (rhoi + rhoj);
+  const double pj = mp_pressure(c->B[jt], c->rho0_inv[jt], c->gamma[it], c->rbg[jt], rhoj);
+  const double pij = (rhoj * pi + rhoi * pj) * mp_rcp(rhoi + rhoj);
   const double velx = vi.x - vj.x, vely = vi.y - vj.y, velz = vi.z - vj.z;
   const double fvisc = (Vi2 + Vj2) * c->tvisc[p] * wfd;
   const double fpair = -(Vi2 + Vj2) * pij * wfd;
@@ -185,20 +208,21 @@ __device__ __forceinline__ bool mp_heat_pair(const MpCoefs *c, int dim, double4 
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
   const double rsq = dx * dx + dy * dy + dz * dz;
   if (!(rsq < c->hcutsq[p])) return false;
-  const double ih = 1.0 / c->hcut[p];
+  const double ih = c->hcut_inv[p];
+  const double r = sqrt(rsq);
   double wfd;
   if (dim == 3) {
-    wfd = quintic_dw(3, sqrt(rsq) * ih);
-    wfd = wfd * ih * ih * ih * ih / sqrt(rsq);
+    wfd = quintic_dw(3, r * ih);
+    wfd = wfd * ih * ih * ih * ih * mp_rcp(r);
   } else {
-    wfd = quintic_dw(2, sqrt(rsq) * ih);
-    wfd = wfd * ih * ih * ih / sqrt(rsq);
+    wfd = quintic_dw(2, r * ih);
+    wfd = wfd * ih * ih * ih * mp_rcp(r);
   }
   double Ti = Ti0, Tj = Tj0;
   const int ff = c->hfix[p];
   if (ff == it && Ti < Tj) Ti = c->htc[p];
   if (ff == jt && Tj < Ti) Tj = c->htc[p];
-  deltaE = 2.0 * c->halpha[p] * (Ti - Tj) * wfd / (rhoi * rhoj);
+  deltaE = 2.0 * c->halpha[p] * (Ti - Tj) * wfd * mp_rcp(rhoi * rhoj);
   return true;
 }
 
@@ -223,15 +247,16 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
     const double rsq = dx * dx + dy * dy + dz * dz;
     if (!(rsq < c->ccutsq[p])) continue;
     const double r = sqrt(rsq);
-    const double ih = 1.0 / c->ccut[p];
+    const double ih = c->ccut_inv[p];
     double wfd;
     if (a.dim == 3) wfd = quintic_dw(3, r * ih) * ih * ih * ih * ih;
     else wfd = quintic_dw(2, r * ih) * ih * ih * ih;
     const double sigmaj = a.xs ? xj.w : a.vr[j].w / a.rm[j];
-    const double dphi = -wfd * c->calpha[p] / (sigmaj * sigmaj) * sigmai;
-    gx += dphi * (dx / r);
-    gy += dphi * (dy / r);
-    if (a.dim == 3) gz += dphi * (dz / r);
+    const double dphi = -wfd * c->calpha[p] * mp_rcp(sigmaj * sigmaj) * sigmai;
+    const double ir = mp_rcp(r);
+    gx += dphi * (dx * ir);
+    gy += dphi * (dy * ir);
+    if (a.dim == 3) gz += dphi * (dz * ir);
   }
   gx = group_sum<G>(gx);
   gy = group_sum<G>(gy);
@@ -244,20 +269,21 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
 // :29), written term by term as the reference does.
 __device__ __forceinline__ double3 st_vector(int dim, double4 c, double absc, double3 e) {
   if (!(absc > 1.0e-12)) return make_double3(0.0, 0.0, 0.0);
+  const double ia = mp_rcp(absc);
   if (dim == 2)
     return make_double3(
-        (e.x * ((c.y * c.y + c.x * c.x) / 2 - c.x * c.x) - c.x * e.y * c.y) / absc,
-        (e.y * ((c.y * c.y + c.x * c.x) / 2 - c.y * c.y) - e.x * c.x * c.y) / absc, 0.0);
+        (e.x * ((c.y * c.y + c.x * c.x) / 2 - c.x * c.x) - c.x * e.y * c.y) * ia,
+        (e.y * ((c.y * c.y + c.x * c.x) / 2 - c.y * c.y) - e.x * c.x * c.y) * ia, 0.0);
   return make_double3(
       (e.x * (0.3333333333333333 * c.z * c.z + 0.3333333333333333 * c.y * c.y -
               0.6666666666666666 * c.x * c.x) -
-       1.0 * c.x * e.z * c.z - 1.0 * c.x * e.y * c.y) / absc,
+       1.0 * c.x * e.z * c.z - 1.0 * c.x * e.y * c.y) * ia,
       (e.y * (0.3333333333333333 * c.z * c.z - 0.6666666666666666 * c.y * c.y +
               0.3333333333333333 * c.x * c.x) -
-       1.0 * c.y * e.z * c.z - 1.0 * e.x * c.x * c.y) / absc,
+       1.0 * c.y * e.z * c.z - 1.0 * e.x * c.x * c.y) * ia,
       (e.z * (-0.6666666666666666 * c.z * c.z + 0.3333333333333333 * c.y * c.y +
               0.3333333333333333 * c.x * c.x) -
-       1.0 * e.y * c.y * c.z - 1.0 * e.x * c.x * c.z) / absc);
+       1.0 * e.y * c.y * c.z - 1.0 * e.x * c.x * c.z) * ia);
 }
 __device__ __forceinline__ double st_abs(int dim, double4 c) {
   return dim == 3 ? sqrt(c.x * c.x + c.y * c.y + c.z * c.z) : sqrt(c.x * c.x + c.y * c.y);
@@ -272,11 +298,12 @@ __device__ __forceinline__ bool mp_surf_pair(const MpCoefs *c, int dim, double4 
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
   const double rsq = dx * dx + dy * dy + dz * dz;
   if (!(rsq < c->scutsq[p])) return false;
-  const double ih = 1.0 / c->scut[p];
+  const double ih = c->scut_inv[p];
   const double r = sqrt(rsq);
   const double wfd = (dim == 3) ? quintic_dw(3, r * ih) * ih * ih * ih * ih
                                 : quintic_dw(2, r * ih) * ih * ih * ih;
-  const double3 e = make_double3(dx / r, dy / r, dim == 3 ? dz / r : 0.0);
+  const double ir = mp_rcp(r);
+  const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
   const double3 Si = st_vector(dim, cgi, abscgi, e);
   const double3 Sj = st_vector(dim, cgj, st_abs(dim, cgj), e);
   F = make_double3((Si.x * Vi * Vi + Sj.x * Vj * Vj) * wfd, (Si.y * Vi * Vi + Sj.y * Vj * Vj) * wfd,
@@ -461,7 +488,8 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
       const double4 ci = fi ? cFi : cSi;
       const double4 cp = mp_sel(own, ci, cj), cq = mp_sel(own, cj, ci);
       double3 F;
-      if (mp_surf_pair(c, dim, xp, tp, mp / rp, cp, st_abs(dim, cp), xq, tq, mq / rq, cq, F)) {
+      if (mp_surf_pair(c, dim, xp, tp, mp * mp_rcp(rp), cp, st_abs(dim, cp), xq, tq,
+                       mq * mp_rcp(rq), cq, F)) {
         fx += sg * F.x;
         fy += sg * F.y;
         fz += sg * F.z;

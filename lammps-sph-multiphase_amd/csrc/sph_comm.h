@@ -51,6 +51,14 @@ struct Transport {
     exchange(s1, sb1, d1, r1, rb1, src1, s);
   }
   virtual void barrier(hipStream_t s) = 0;
+  // every other rank r: send scnt[r] to r, receive rcnt[r] from r (scnt/rcnt hold size()
+  // ints; the own entry is ignored); host-synchronous
+  virtual void exchange_counts_all(const int *scnt, int *rcnt, hipStream_t s) = 0;
+  // n exchanges in ONE group: send sb[k] (sbytes[k]) to peer[k] and receive rb[k]
+  // (rbytes[k]) from peer[k]; at most one entry per peer; stream-ordered on s
+  virtual void exchange_multi(int n, const int *peer, const void *const *sb,
+                              const size_t *sbytes, void *const *rb, const size_t *rbytes,
+                              hipStream_t s) = 0;
 };
 
 #define SPH_NCCL_TRY(call)                                                             \
@@ -67,6 +75,7 @@ class RcclTransport : public Transport {
   }
   ~RcclTransport() override {
     if (dcnt_) (void)hipFree(dcnt_);
+    if (dall_) (void)hipFree(dall_);
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   int rank() const override { return me_; }
@@ -121,17 +130,40 @@ class RcclTransport : public Transport {
     SPH_NCCL_TRY(ncclAllReduce(dcnt_, dcnt_, 1, ncclInt32, ncclSum, comm_, s));
     SPH_HIP_TRY(hipStreamSynchronize(s));
   }
+  void exchange_counts_all(const int *scnt, int *rcnt, hipStream_t s) override {
+    if (!dall_) SPH_HIP_TRY(hipMalloc(&dall_, 2 * (size_t)n_ * sizeof(int)));
+    SPH_HIP_TRY(hipMemcpyAsync(dall_, scnt, n_ * sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_NCCL_TRY(ncclGroupStart());
+    for (int r = 0; r < n_; r++) {
+      if (r == me_) continue;
+      SPH_NCCL_TRY(ncclSend(dall_ + r, 1, ncclInt32, r, comm_, s));
+      SPH_NCCL_TRY(ncclRecv(dall_ + n_ + r, 1, ncclInt32, r, comm_, s));
+    }
+    SPH_NCCL_TRY(ncclGroupEnd());
+    SPH_HIP_TRY(hipMemcpyAsync(rcnt, dall_ + n_, n_ * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    rcnt[me_] = 0;
+  }
+  void exchange_multi(int n, const int *peer, const void *const *sb, const size_t *sbytes,
+                      void *const *rb, const size_t *rbytes, hipStream_t s) override {
+    SPH_NCCL_TRY(ncclGroupStart());
+    for (int k = 0; k < n; k++) {
+      if (sbytes[k]) SPH_NCCL_TRY(ncclSend(sb[k], sbytes[k], ncclUint8, peer[k], comm_, s));
+      if (rbytes[k]) SPH_NCCL_TRY(ncclRecv(rb[k], rbytes[k], ncclUint8, peer[k], comm_, s));
+    }
+    SPH_NCCL_TRY(ncclGroupEnd());
+  }
 
  private:
   int n_, me_;
   ncclComm_t comm_ = nullptr;
-  int *dcnt_ = nullptr;
+  int *dcnt_ = nullptr, *dall_ = nullptr;
 };
 
 // Bricks of one process: every brick runs in its own host thread; a swap posts its send
 // buffer, meets the others at a barrier, copies its peer's buffer, meets them again.
 struct LocalWorld {
-  explicit LocalWorld(int n) : n(n), post(n) {}
+  explicit LocalWorld(int n) : n(n), post(n), mpost(n), cpost(n) {}
   struct Post {
     const void *buf = nullptr;
     size_t bytes = 0;
@@ -139,6 +171,8 @@ struct LocalWorld {
   };
   int n;
   std::vector<Post> post;
+  std::vector<std::vector<Post>> mpost;  // exchange_multi: every rank's sends
+  std::vector<std::vector<int>> cpost;   // exchange_counts_all: every rank's counts
   std::mutex m;
   std::condition_variable cv;
   int arrived = 0;
@@ -190,6 +224,38 @@ class LocalTransport : public Transport {
     SPH_HIP_TRY(hipStreamSynchronize(s));
     w_->barrier();
   }
+  void exchange_counts_all(const int *scnt, int *rcnt, hipStream_t s) override {
+    w_->cpost[me_].assign(scnt, scnt + w_->n);
+    w_->barrier();
+    for (int r = 0; r < w_->n; r++) rcnt[r] = r == me_ ? 0 : w_->cpost[r][me_];
+    w_->barrier();
+  }
+  void exchange_multi(int n, const int *peer, const void *const *sb, const size_t *sbytes,
+                      void *const *rb, const size_t *rbytes, hipStream_t s) override {
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // my send buffers are packed
+    auto &mine = w_->mpost[me_];
+    mine.clear();
+    for (int k = 0; k < n; k++) {
+      LocalWorld::Post p;
+      p.buf = sb[k];
+      p.bytes = sbytes[k];
+      p.dest = peer[k];
+      mine.push_back(p);
+    }
+    w_->barrier();
+    for (int k = 0; k < n; k++) {
+      const LocalWorld::Post *q = nullptr;
+      for (const auto &c : w_->mpost[peer[k]])
+        if (c.dest == me_) q = &c;
+      SPH_REQUIRE((q && q->bytes == rbytes[k]) || (!q && rbytes[k] == 0), SPH_HIP_ECOMM,
+                  "local multi exchange mismatch (%d -> %d: %zu bytes expected)", peer[k], me_,
+                  rbytes[k]);
+      if (rbytes[k])
+        SPH_HIP_TRY(hipMemcpyAsync(rb[k], q->buf, rbytes[k], hipMemcpyDeviceToDevice, s));
+    }
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    w_->barrier();  // the senders may reuse their buffers now
+  }
 
  private:
   LocalWorld *w_;
@@ -198,11 +264,14 @@ class LocalTransport : public Transport {
 
 // ---- pack / unpack kernels -------------------------------------------------------------
 // border record (AtomVecMeso::pack_border/unpack_border, atom_vec_meso.cpp:422-600):
-// x (shifted), vest + rho, e, type
+// x (shifted), vest + rho, e, type -- plus the ghost's ORIGIN: the rank and owned index of
+// the atom it images and the accumulated periodic image (a ghost forwarded along a later
+// dimension keeps its origin), from which the per-step forward comm goes straight from
+// owner to ghost in one exchange (sph_engine::build_direct)
 struct BorderRec {
   double4 x, v;
   double e;
-  int type, pad;
+  int type, orank, oidx, img;
 };
 
 __device__ __forceinline__ double4 shift_x(double4 x, int dim, double shift) {
@@ -213,10 +282,13 @@ __device__ __forceinline__ double4 shift_x(double4 x, int dim, double shift) {
 }
 
 static __global__ void k_pack_border(int n, const int *__restrict__ list, int dim, double shift,
+                                     int pbc, int me, int nlocal,
                                      const double4 *__restrict__ xf,
                                      const double4 *__restrict__ vr,
                                      const double *__restrict__ en, const int *__restrict__ ty,
-                                     BorderRec *__restrict__ out) {
+                                     const int *__restrict__ gorank,
+                                     const int *__restrict__ goidx,
+                                     const int *__restrict__ gimg, BorderRec *__restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const int i = list[k];
@@ -225,13 +297,19 @@ static __global__ void k_pack_border(int n, const int *__restrict__ list, int di
   r.v = vr[i];
   r.e = en[i];
   r.type = ty[i];
-  r.pad = 0;
+  const bool own = i < nlocal;
+  r.orank = own ? me : gorank[i - nlocal];
+  r.oidx = own ? i : goidx[i - nlocal];
+  r.img = img_add(own ? 0 : gimg[i - nlocal], dim, pbc);
   out[k] = r;
 }
 
-static __global__ void k_unpack_border(int n, int first, const BorderRec *__restrict__ in,
+static __global__ void k_unpack_border(int n, int first, int nlocal,
+                                       const BorderRec *__restrict__ in,
                                        double4 *__restrict__ xf, double4 *__restrict__ vr,
-                                       double *__restrict__ en, int *__restrict__ ty) {
+                                       double *__restrict__ en, int *__restrict__ ty,
+                                       int *__restrict__ gorank, int *__restrict__ goidx,
+                                       int *__restrict__ gimg) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const BorderRec r = in[k];
@@ -239,6 +317,88 @@ static __global__ void k_unpack_border(int n, int first, const BorderRec *__rest
   vr[first + k] = r.v;
   en[first + k] = r.e;
   ty[first + k] = r.type;
+  const int g = first + k - nlocal;
+  gorank[g] = r.orank;
+  goidx[g] = r.oidx;
+  gimg[g] = r.img;
+}
+
+// ---- direct forward comm (owner -> ghost in one exchange) -----------------------------
+// pack: the listed owned atoms' x (unshifted), vest, rho, e, P/rho^2 (9 doubles); unpack:
+// into ghost slots, each coordinate shifted by its own image (one add per coordinate, as the
+// hop-by-hop forward adds it: every hop shifts exactly one coordinate, atom_vec_meso.cpp:
+// 246-288)
+static __global__ void k_pack_direct(int n, const int *__restrict__ idx,
+                                     const double4 *__restrict__ xf,
+                                     const double4 *__restrict__ vr,
+                                     const double *__restrict__ en, double *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = idx[k];
+  const double4 x = xf[i], v = vr[i];
+  double *o = out + 9 * (size_t)k;
+  o[0] = x.x;
+  o[1] = x.y;
+  o[2] = x.z;
+  o[3] = v.x;
+  o[4] = v.y;
+  o[5] = v.z;
+  o[6] = v.w;
+  o[7] = en[i];
+  o[8] = x.w;
+}
+static __global__ void k_unpack_direct(int n, const int *__restrict__ slot, int nlocal, Box b,
+                                       const int *__restrict__ gimg,
+                                       const double *__restrict__ in, double4 *__restrict__ xf,
+                                       double4 *__restrict__ vr, double *__restrict__ en) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int g = slot[k], img = gimg[g];
+  const double *o = in + 9 * (size_t)k;
+  double4 x = make_double4(o[0], o[1], o[2], o[8]);
+  const int ix = img_get(img, 0), iy = img_get(img, 1), iz = img_get(img, 2);
+  if (ix) x.x = x.x + ix * b.prd[0];
+  if (iy) x.y = x.y + iy * b.prd[1];
+  if (iz) x.z = x.z + iz * b.prd[2];
+  xf[nlocal + g] = x;
+  vr[nlocal + g] = make_double4(o[3], o[4], o[5], o[6]);
+  en[nlocal + g] = o[7];
+}
+// ghosts imaging this rank's own atoms: straight device copies
+static __global__ void k_forward_self(int n, const int *__restrict__ slot, int nlocal, Box b,
+                                      const int *__restrict__ goidx,
+                                      const int *__restrict__ gimg, double4 *__restrict__ xf,
+                                      double4 *__restrict__ vr, double *__restrict__ en) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int g = slot[k], o = goidx[g], img = gimg[g];
+  double4 x = xf[o];
+  const int ix = img_get(img, 0), iy = img_get(img, 1), iz = img_get(img, 2);
+  if (ix) x.x = x.x + ix * b.prd[0];
+  if (iy) x.y = x.y + iy * b.prd[1];
+  if (iz) x.z = x.z + iz * b.prd[2];
+  xf[nlocal + g] = x;
+  vr[nlocal + g] = vr[o];
+  en[nlocal + g] = en[o];
+}
+static __global__ void k_unpack_rho_direct(int n, const int *__restrict__ slot, int nlocal,
+                                           const double2 *__restrict__ in,
+                                           double4 *__restrict__ xf, double4 *__restrict__ vr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int g = nlocal + slot[k];
+  const double2 r = in[k];
+  vr[g].w = r.x;
+  xf[g].w = r.y;
+}
+static __global__ void k_forward_rho_self(int n, const int *__restrict__ slot, int nlocal,
+                                          const int *__restrict__ goidx,
+                                          double4 *__restrict__ xf, double4 *__restrict__ vr) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int g = slot[k], o = goidx[g];
+  vr[nlocal + g].w = vr[o].w;
+  xf[nlocal + g].w = xf[o].w;
 }
 
 // forward comm (AtomVecMeso::pack_comm_vel, atom_vec_meso.cpp:246-360): x (shifted),

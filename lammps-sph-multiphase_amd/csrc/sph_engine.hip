@@ -93,6 +93,11 @@ static int blk_shape_env() {
   return v;
 }
 // (read per engine at sph_engine_create)
+// SPH_DIRECT (default 1): bricks forward the per-step halos owner -> ghost in one exchange
+static bool direct_env() {
+  static bool v = env_int("SPH_DIRECT", 1) != 0;
+  return v;
+}
 static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
 
 namespace {
@@ -140,6 +145,7 @@ struct sph_engine {
   Transport *tr = nullptr;
   struct Swap {
     int dim = 0, dir = 0, sendproc = 0, recvproc = 0, nsend = 0, nrecv = 0, firstrecv = 0;
+    int pbc = 0;
     double lo = 0.0, hi = 0.0, shift = 0.0;
     bool remote = false;
     DBuf<int> list;
@@ -180,6 +186,17 @@ struct sph_engine {
   DBuf<int> ty2, tag2;
   // ghosts
   DBuf<int> gowner, gimg;
+  DBuf<int> gorank, goidx;  // bricks: each ghost's origin rank and owned index (gimg: image)
+  // direct forward comm (build_direct): peers, per-peer record offsets (sends / receives),
+  // send lists (owned indices), receiving ghost slots, ghosts imaging own atoms
+  bool dr_ok = false;
+  std::vector<int> dr_peer;
+  std::vector<size_t> dr_soff, dr_roff;
+  DBuf<int> dr_sidx, dr_rslot, dr_self;
+  int dr_nself = 0;
+  std::vector<const void *> dr_sb;
+  std::vector<void *> dr_rb;
+  std::vector<size_t> dr_sbytes, dr_rbytes;
   // borders scratch
   DBuf<unsigned char> flags;
   DBuf<int> sel, nsel;
@@ -438,6 +455,7 @@ struct sph_engine {
         if (dir == 0 && myloc[d] == 0) pbc = 1;
         if (dir == 1 && myloc[d] == pg[d] - 1) pbc = -1;
         sw.shift = pbc * box.prd[d];
+        sw.pbc = pbc;
         int ns = 0;
         if (sendflag && nlast > 0) {
           flags.reserve(nlast);
@@ -470,7 +488,8 @@ struct sph_engine {
         Swap &sw = *pair[dir];
         if (sw.nsend)
           hipLaunchKernelGGL(k_pack_border, dim3(blocks(sw.nsend)), dim3(BLK), 0, s, sw.nsend,
-                             sw.list.p, d, sw.shift, xf.p, vr.p, en.p, ty.p,
+                             sw.list.p, d, sw.shift, sw.pbc, tr->rank(), nlocal, xf.p, vr.p,
+                             en.p, ty.p, gorank.p, goidx.p, gimg.p,
                              (BorderRec *)(cbs.p + (dir ? so : 0)));
       }
       if (a.remote) {
@@ -481,19 +500,132 @@ struct sph_engine {
         if (rb) SPH_HIP_TRY(hipMemcpyAsync(cbr.p + ro, cbs.p + so, rb, hipMemcpyDeviceToDevice, s));
       }
       const int nr = a.nrecv + b.nrecv;
-      if (nr) ensure_atoms((size_t)nall + nr, true);
+      if (nr) {
+        ensure_atoms((size_t)nall + nr, true);
+        const size_t ngn = (size_t)nall + nr - nlocal;
+        gorank.reserve(ngn, true, s);
+        goidx.reserve(ngn, true, s);
+        gimg.reserve(ngn, true, s);
+      }
       for (int dir = 0; dir < 2; dir++) {
         Swap &sw = *pair[dir];
         if (sw.nrecv)
           hipLaunchKernelGGL(k_unpack_border, dim3(blocks(sw.nrecv)), dim3(BLK), 0, s,
-                             sw.nrecv, sw.firstrecv,
+                             sw.nrecv, sw.firstrecv, nlocal,
                              (const BorderRec *)(cbr.p + (dir ? ro : 0)), xf.p, vr.p, en.p,
-                             ty.p);
+                             ty.p, gorank.p, goidx.p, gimg.p);
       }
       if (mp) mpx_swap_pair(a, b);
       nall += nr;
     }
     nghost = nall - nlocal;
+    build_direct();
+  }
+
+  // Direct forward comm: the per-step halo goes straight from each ghost's owner (its
+  // origin, carried through the border records) in ONE exchange, instead of one exchange
+  // per dimension with earlier dimensions' ghosts forwarded again (CommBrick's
+  // dimension-ordered swaps, comm_brick.cpp:475-530).  Built at every borders: the ghosts
+  // are grouped by origin rank (ghost order kept), every rank sends its peers the owned
+  // indices it needs from them (counts first), and what it receives becomes its send lists.
+  // Ghosts imaging this rank's own atoms are device copies (through the communicator in
+  // loopback mode).  The swaps stay for the reverse comm of the setup step and of fix
+  // phase_change.  SPH_DIRECT=0 keeps the dimension-ordered forward.
+  void build_direct() {
+    dr_ok = false;
+    if (!direct_env() || mp || !tr) return;
+    const int P = tr->size(), me = tr->rank(), ng = nghost;
+    std::vector<int> hr(ng), hi(ng);
+    if (ng) {
+      SPH_HIP_TRY(hipMemcpyAsync(hr.data(), gorank.p, ng * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(hi.data(), goidx.p, ng * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipStreamSynchronize(s));
+    }
+    // counting sort of the ghosts by origin rank (ghost order kept within a rank)
+    std::vector<int> cnt(P + 1, 0);
+    for (int g = 0; g < ng; g++) {
+      SPH_REQUIRE(hr[g] >= 0 && hr[g] < P, SPH_HIP_ERUNTIME, "ghost %d: origin rank %d", g, hr[g]);
+      cnt[hr[g] + 1]++;
+    }
+    std::vector<int> beg(P + 1, 0);
+    for (int r = 0; r < P; r++) beg[r + 1] = beg[r] + cnt[r + 1];
+    std::vector<int> byq(ng), byg(ng);  // owned indices / ghost slots, grouped by origin rank
+    {
+      std::vector<int> pos(beg.begin(), beg.end() - 1);
+      for (int g = 0; g < ng; g++) {
+        const int k = pos[hr[g]]++;
+        byq[k] = hi[g];
+        byg[k] = g;
+      }
+    }
+    std::vector<int> scnt(P, 0), rcnt(P, 0);
+    for (int r = 0; r < P; r++)
+      if (r != me) scnt[r] = beg[r + 1] - beg[r];
+    tr->exchange_counts_all(scnt.data(), rcnt.data(), s);  // rcnt[r]: what r needs from me
+    dr_peer.clear();
+    dr_soff.assign(1, 0);
+    dr_roff.assign(1, 0);
+    std::vector<int> hreq, hslot;
+    hreq.reserve(ng);
+    hslot.reserve(ng);
+    for (int r = 0; r < P; r++) {
+      if (r == me && !loopback) continue;
+      const size_t nin = beg[r + 1] - beg[r], nout = (r == me) ? nin : (size_t)rcnt[r];
+      if (nin == 0 && nout == 0) continue;
+      dr_peer.push_back(r);
+      hreq.insert(hreq.end(), byq.begin() + beg[r], byq.begin() + beg[r + 1]);
+      hslot.insert(hslot.end(), byg.begin() + beg[r], byg.begin() + beg[r + 1]);
+      dr_roff.push_back(dr_roff.back() + nin);
+      dr_soff.push_back(dr_soff.back() + nout);
+    }
+    const int np = (int)dr_peer.size();
+    const size_t S = dr_soff.back(), R = dr_roff.back();
+    DBuf<int> req;
+    req.reserve(R > 0 ? R : 1);
+    dr_sidx.reserve(S > 0 ? S : 1);
+    dr_rslot.reserve(R > 0 ? R : 1);
+    if (R) {
+      SPH_HIP_TRY(hipMemcpyAsync(req.p, hreq.data(), R * sizeof(int), hipMemcpyHostToDevice, s));
+      SPH_HIP_TRY(hipMemcpyAsync(dr_rslot.p, hslot.data(), R * sizeof(int), hipMemcpyHostToDevice, s));
+    }
+    dr_sb.resize(np);
+    dr_rb.resize(np);
+    dr_sbytes.resize(np);
+    dr_rbytes.resize(np);
+    for (int k = 0; k < np; k++) {  // requests out, the peers' requests in (= my send lists)
+      dr_sb[k] = req.p + dr_roff[k];
+      dr_sbytes[k] = (dr_roff[k + 1] - dr_roff[k]) * sizeof(int);
+      dr_rb[k] = dr_sidx.p + dr_soff[k];
+      dr_rbytes[k] = (dr_soff[k + 1] - dr_soff[k]) * sizeof(int);
+    }
+    tr->exchange_multi(np, dr_peer.data(), dr_sb.data(), dr_sbytes.data(), dr_rb.data(),
+                       dr_rbytes.data(), s);
+    dr_nself = loopback ? 0 : beg[me + 1] - beg[me];
+    dr_self.reserve(dr_nself > 0 ? dr_nself : 1);
+    if (dr_nself)
+      SPH_HIP_TRY(hipMemcpyAsync(dr_self.p, byg.data() + beg[me], dr_nself * sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // (req and the host vectors go out of scope)
+    req.release();
+    dr_ok = true;
+  }
+  // one direct forward of rec-byte records: pack the send lists, one exchange, unpack
+  template <class Pack, class Unpack, class Self>
+  void forward_direct(size_t rec, Pack pack, Unpack unpack, Self self) {
+    const int np = (int)dr_peer.size();
+    const size_t S = dr_soff.back(), R = dr_roff.back();
+    cbs.reserve(std::max<size_t>(S * rec, 1));
+    cbr.reserve(std::max<size_t>(R * rec, 1));
+    if (S) pack((int)S, cbs.p);
+    for (int k = 0; k < np; k++) {
+      dr_sb[k] = cbs.p + dr_soff[k] * rec;
+      dr_sbytes[k] = (dr_soff[k + 1] - dr_soff[k]) * rec;
+      dr_rb[k] = cbr.p + dr_roff[k] * rec;
+      dr_rbytes[k] = (dr_roff[k + 1] - dr_roff[k]) * rec;
+    }
+    tr->exchange_multi(np, dr_peer.data(), dr_sb.data(), dr_sbytes.data(), dr_rb.data(),
+                       dr_rbytes.data(), s);
+    if (R) unpack((int)R, cbr.p);
+    if (dr_nself) self();
   }
 
   // the extra multiphase fields of a dimension's two swaps (pack_border_vel / pack_comm_vel
@@ -557,6 +689,25 @@ struct sph_engine {
 
   // Comm::forward_comm (x, vest, rho, e)
   void forward_multi() {
+    if (dr_ok) {
+      forward_direct(
+          9 * sizeof(double),
+          [&](int n, unsigned char *buf) {
+            hipLaunchKernelGGL(k_pack_direct, dim3(blocks(n)), dim3(BLK), 0, s, n, dr_sidx.p,
+                               xf.p, vr.p, en.p, (double *)buf);
+          },
+          [&](int n, unsigned char *buf) {
+            hipLaunchKernelGGL(k_unpack_direct, dim3(blocks(n)), dim3(BLK), 0, s, n,
+                               dr_rslot.p, nlocal, box, gimg.p, (const double *)buf, xf.p, vr.p,
+                               en.p);
+          },
+          [&] {
+            hipLaunchKernelGGL(k_forward_self, dim3(blocks(dr_nself)), dim3(BLK), 0, s,
+                               dr_nself, dr_self.p, nlocal, box, goidx.p, gimg.p, xf.p, vr.p,
+                               en.p);
+          });
+      return;
+    }
     forward_dims(
         9 * sizeof(double),
         [&](Swap &sw, unsigned char *buf) {
@@ -596,6 +747,23 @@ struct sph_engine {
 
   // comm->forward_comm_pair of sph/rhosum: rho (+ the EOS term)
   void forward_rho_multi() {
+    if (dr_ok) {
+      forward_direct(
+          sizeof(double2),
+          [&](int n, unsigned char *buf) {
+            hipLaunchKernelGGL(k_pack_rho, dim3(blocks(n)), dim3(BLK), 0, s, n, dr_sidx.p, xf.p,
+                               vr.p, (double2 *)buf);
+          },
+          [&](int n, unsigned char *buf) {
+            hipLaunchKernelGGL(k_unpack_rho_direct, dim3(blocks(n)), dim3(BLK), 0, s, n,
+                               dr_rslot.p, nlocal, (const double2 *)buf, xf.p, vr.p);
+          },
+          [&] {
+            hipLaunchKernelGGL(k_forward_rho_self, dim3(blocks(dr_nself)), dim3(BLK), 0, s,
+                               dr_nself, dr_self.p, nlocal, goidx.p, xf.p, vr.p);
+          });
+      return;
+    }
     forward_dims(
         sizeof(double2),
         [&](Swap &sw, unsigned char *buf) {
@@ -1773,6 +1941,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
   for (auto *b : {&e->cg, &e->cgS, &e->cgF, &e->recA, &e->recK, &e->recF, &e->recS}) b->release();
   if (e->dm) (void)hipFree(e->dm);
+  for (auto *b : {&e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self}) b->release();
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
                   &e->ccnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,

@@ -56,6 +56,10 @@ inline void mp_inverses(MpCoefs &m) {
   for (int t = 0; t <= MAXT; t++) m.rho0_inv[t] = inv(m.rho0[t]);
 }
 
+// the quintic kernel's dW/dr scaled by h^-(dim+1) (the styles' wfd before any 1/r)
+__device__ __forceinline__ double quintic_dw(int dim, double r);
+__device__ __forceinline__ double mp_qdw(int dim, double r, double ih);
+
 // 1/b for the pair terms' divisions: v_rcp_f64 seed + one Newton step (~1 ulp; the fp64
 // IEEE division sequence costs ~3x the issue slots, and the 1e-10 parity bar is kept)
 __device__ __forceinline__ double mp_rcp(double b) {
@@ -93,6 +97,11 @@ __device__ __forceinline__ double quintic_dw(int dim, double r) {
     wfd = 0.0;
   }
   return norm * wfd;
+}
+
+__device__ __forceinline__ double mp_qdw(int dim, double r, double ih) {
+  return dim == 3 ? quintic_dw(3, r * ih) * ih * ih * ih * ih
+                  : quintic_dw(2, r * ih) * ih * ih * ih;
 }
 
 struct MpArgs {
@@ -454,16 +463,37 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
   const double4 cFi = a.pF[i], cSi = a.pS[i];
   const double rFi = cFi.w, rSi = cSi.w;
   double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
-    const int jr = a.nbr[k];
+  // two entries per lane and round, both entries' records loaded before either is used
+  // (the loop is latency-bound on the index -> record chain otherwise)
+  constexpr int NU = 2;
+  const int kend = a.off[row + 1];
+  for (int k0 = a.off[row] + lane; k0 < kend; k0 += NU * G) {
+    int jrs[NU];
+    double4 xjs[NU], v4js[NU], cjs[NU];
+    int tjs[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) jrs[u] = k0 + u * G < kend ? a.nbr[k0 + u * G] : 0;
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int j = jrs[u] & MP_NMASK;
+      const bool fj = !(j >= a.nlocal) || !(jrs[u] < 0);
+      xjs[u] = a.pA[j];
+      v4js[u] = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
+      cjs[u] = (fj ? a.pF : a.pS)[j];
+      tjs[u] = a.ty[j];
+    }
+#pragma unroll
+  for (int u = 0; u < NU; u++) {
+    if (k0 + u * G >= kend) break;
+    const int jr = jrs[u];
     const int j = jr & MP_NMASK;
     const bool own = jr < 0;  // (bit 31: the pair is i's in the half list, k_neigh3)
     const bool gj = j >= a.nlocal;
-    const bool fi = !(gj && !own), fj = !gj || !own;  // fresh or stale values (see above)
-    const double4 xj = a.pA[j];
-    const double4 v4j = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
-    const double4 cj = (fj ? a.pF : a.pS)[j];  // (colorgradient, rho) of j as used here
-    const int tj = a.ty[j];
+    const bool fi = !(gj && !own);  // fresh or stale values of i (see above; j's: cjs)
+    const double4 xj = xjs[u];
+    const double4 v4j = v4js[u];
+    const double4 cj = cjs[u];  // (colorgradient, rho) of j as used here
+    const int tj = tjs[u];
     const double mj = xj.w;
     const double rhoi = fi ? rFi : rSi;
     const double rhoj = cj.w;
@@ -473,35 +503,56 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
     const int tp = own ? ti : tj, tq = own ? tj : ti;
     const double mp = own ? mi : mj, mq = own ? mj : mi;
     const double rp = own ? rhoi : rhoj, rq = own ? rhoj : rhoi;
-    if (TAIT) {
-      const double4 vi = make_double4(v4i.x, v4i.y, v4i.z, rhoi);
-      const double4 vj = make_double4(v4j.x, v4j.y, v4j.z, rhoj);
-      double3 F;
-      if (mp_tait_pair(c, dim, xp, mp_sel(own, vi, vj), tp, mp, xq, mp_sel(own, vj, vi), tq, mq,
-                       F)) {
-        fx += sg * F.x;
-        fy += sg * F.y;
-        fz += sg * F.z;
-      }
+    // the three styles' pair terms (mp_tait_pair, mp_surf_pair, mp_heat_pair) sharing the
+    // geometry: r, 1/r, and the quintic dW once per distinct cutoff (bubble.lmp: one h)
+    const int pc = tp * (c->ntypes + 1) + tq;
+    const double dx = xp.x - xq.x, dy = xp.y - xq.y, dz = xp.z - xq.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    const bool ct = TAIT && rsq < c->tcutsq[pc], cs = SURF && rsq < c->scutsq[pc],
+               ch = HEAT && rsq < c->hcutsq[pc];
+    if (!(ct || cs || ch)) continue;
+    const double r = sqrt(rsq), ir = mp_rcp(r);
+    const double iht = c->tcut_inv[pc], ihs = c->scut_inv[pc], ihh = c->hcut_inv[pc];
+    const double qt = ct ? mp_qdw(dim, r, iht) : 0.0;
+    const double qs = !cs ? 0.0 : (ct && ihs == iht) ? qt : mp_qdw(dim, r, ihs);
+    const double qh = !ch ? 0.0 : (ct && ihh == iht) ? qt : (cs && ihh == ihs) ? qs
+                                                                            : mp_qdw(dim, r, ihh);
+    if (ct) {  // taitwater/multiphase (pair_sph_taitwater_multiphase.cpp:128-170)
+      const double wfd = qt * ir;
+      const double4 vp = mp_sel(own, v4i, v4j), vq = mp_sel(own, v4j, v4i);
+      const double Vi = mp * mp_rcp(rp), Vj = mq * mp_rcp(rq);
+      const double V2 = Vi * Vi + Vj * Vj;
+      const double pi = mp_pressure(c->B[tp], c->rho0_inv[tp], c->gamma[tp], c->rbg[tp], rp);
+      // reference quirk kept: p_j with gamma[itype] (pair_sph_taitwater_multiphase.cpp:148)
+      const double pj = mp_pressure(c->B[tq], c->rho0_inv[tq], c->gamma[tp], c->rbg[tq], rq);
+      const double pij = (rq * pi + rp * pj) * mp_rcp(rp + rq);
+      const double fvisc = V2 * c->tvisc[pc] * wfd;
+      const double fpair = -V2 * pij * wfd;
+      fx += sg * (dx * fpair + (vp.x - vq.x) * fvisc);
+      fy += sg * (dy * fpair + (vp.y - vq.y) * fvisc);
+      fz += sg * (dz * fpair + (vp.z - vq.z) * fvisc);
     }
-    if (SURF) {
+    if (SURF && cs) {  // surfacetension (pair_sph_surfacetension.cpp:100-190)
       const double4 ci = fi ? cFi : cSi;
       const double4 cp = mp_sel(own, ci, cj), cq = mp_sel(own, cj, ci);
-      double3 F;
-      if (mp_surf_pair(c, dim, xp, tp, mp * mp_rcp(rp), cp, st_abs(dim, cp), xq, tq,
-                       mq * mp_rcp(rq), cq, F)) {
-        fx += sg * F.x;
-        fy += sg * F.y;
-        fz += sg * F.z;
-      }
+      const double Vp = mp * mp_rcp(rp), Vq = mq * mp_rcp(rq);
+      const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
+      const double3 Sp = st_vector(dim, cp, st_abs(dim, cp), e);
+      const double3 Sq = st_vector(dim, cq, st_abs(dim, cq), e);
+      fx += sg * ((Sp.x * Vp * Vp + Sq.x * Vq * Vq) * qs);
+      fy += sg * ((Sp.y * Vp * Vp + Sq.y * Vq * Vq) * qs);
+      if (dim == 3) fz += sg * ((Sp.z * Vp * Vp + Sq.z * Vq * Vq) * qs);
     }
-    if (HEAT) {
-      const double Tj = v4j.w;
-      double d;
-      // de_p += deltaE m_q, de_q -= deltaE m_p (pair_sph_heatconduction_phasechange.cpp:132-136)
-      if (mp_heat_pair(c, dim, xp, tp, rp, own ? Ti : Tj, xq, tq, rq, own ? Tj : Ti, d))
-        dE += sg * d * mj;
+    if (HEAT && ch) {  // heatconduction/phasechange (pair_sph_heatconduction_phasechange.cpp:101-136)
+      double Tp = own ? Ti : v4j.w, Tq = own ? v4j.w : Ti;
+      const int ff = c->hfix[pc];
+      if (ff == tp && Tp < Tq) Tp = c->htc[pc];
+      if (ff == tq && Tq < Tp) Tq = c->htc[pc];
+      const double d = 2.0 * c->halpha[pc] * (Tp - Tq) * (qh * ir) * mp_rcp(rp * rq);
+      // de_p += deltaE m_q, de_q -= deltaE m_p (:132-136)
+      dE += sg * d * mj;
     }
+  }
   }
   fx = group_sum<G>(fx);
   fy = group_sum<G>(fy);

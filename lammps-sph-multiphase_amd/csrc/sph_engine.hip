@@ -130,6 +130,9 @@ struct sph_engine {
   DBuf<double> rm, cvv, rho_tmp, dmass, xbuf, xbuf2, rhoS, rhoF;
   DBuf<double4> cg, cgS, cgF;
   DBuf<double4> recA, recK, recF, recS;  // k_mp_gather's packed records (k_mp_pack_rec)
+  // fix phase_change scratch, kept across calls (no allocation per step)
+  DBuf<int> pc_flag, pc_cand, pc_otag, pc_idx;
+  DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec;
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
   sph_phasechange_params pcp{};
@@ -226,6 +229,7 @@ struct sph_engine {
   int blk_sh = 0, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
   DBuf<int> ulist, ucnt, bl;
   DBuf<unsigned short> snbr;
+  DBuf<int> nbs;  // fixed-stride scratch rows of a CSR build (list_q)
   DBuf<int> mx, ccnt;  // scratch scalars; full-list row counts of the current build
   DBuf<long long> blen;
   // cub scratch
@@ -991,15 +995,16 @@ struct sph_engine {
     off.reserve(n + 1);
     constexpr int G = 8;
     dim3 grid(grid_for_rows(n, G)), block(BLK);
-    auto launch = [&](bool fill, int stride) {
+    auto launch = [&](bool fill, int stride, int *dst = nullptr) {
       if (n == 0) return;
       const bool t = nt1();
       int *const cnt_out = (!fill || stride > 0) ? ccnt.p : (int *)nullptr;
+      int *const rows = dst ? dst : nbr.p;
 #define SPH_N3(F, T)                                                                           \
   hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xi_src, ty.p, \
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
-                     F ? nbr.p : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,   \
+                     F ? rows : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,    \
                      list_perm_pi, mp ? 2 : ((stride > 0 && list_tbits) ? 1 : 0))
       if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
       else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
@@ -1026,7 +1031,19 @@ struct sph_engine {
     }
     strided = false;
     list_tbits = false;
-    launch(false, 0);
+    // CSR: when an earlier build sized the rows, ONE fill pass into fixed-stride scratch rows
+    // (counts as a by-product) compacted into CSR after the scan -- instead of a count pass
+    // and a fill pass (the C5 stack rebuilds every step); a row past the stride falls back
+    bool filled = false;
+    if (list_stride > 0 && (long)n * list_stride < 0x7fffffffL) {  // (64-bit row offsets)
+      list_perm_g = 0;
+      list_perm_pi = 0;
+      nbs.reserve((size_t)n * list_stride);
+      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
+      launch(true, list_stride, nbs.p);
+      filled = read_scalar(mx.p) == 0;
+    }
+    if (!filled) launch(false, 0);
     hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, ccnt.p, off.p);
     size_t tb2 = 0;
     SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, off.p, off.p, n + 1, s));
@@ -1044,7 +1061,13 @@ struct sph_engine {
     const int tot = hm[0];
     SPH_REQUIRE(tot >= 0, SPH_HIP_EOVERFLOW, "neighbor list exceeds 2^31 entries");
     nbr.reserve(tot > 0 ? tot : 1);
-    launch(true, 0);
+    if (filled) {
+      if (n)
+        hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)(((long)n * 32 + BLK - 1) / BLK)),
+                           dim3(BLK), 0, s, n, list_stride, ccnt.p, off.p, nbs.p, nbr.p);
+    } else {
+      launch(true, 0);
+    }
     // stride of later single-pass builds: this build's longest row + 25% + 16, 64-aligned
     // (whole chunks of the transposed layout, 16-B aligned rows)
     list_stride = ((hm[1] + hm[1] / 4 + 16) + 63) & ~63;
@@ -1603,8 +1626,8 @@ struct sph_engine {
       p.top[k] = myloc[k] == pg[k] - 1;
     }
     const PcDev pd{cfg.dim, p.from_type, p.to_type, p.Tc, p.to_mass, p.cutoff};
-    DBuf<int> flag, cand, otag, rows, idx;
-    DBuf<double> rec, gat, Wd, vals, nrec;
+    DBuf<int> &flag = pc_flag, &cand = pc_cand, &otag = pc_otag, &idx = pc_idx;
+    DBuf<double> &rec = pc_rec, &gat = pc_gat, &Wd = pc_Wd, &vals = pc_vals, &nrec = pc_nrec;
     flag.reserve(n);
     hipLaunchKernelGGL(k_pc_flags, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
                        ty.p, en.p, cvv.p, pd, flag.p);
@@ -1681,7 +1704,7 @@ struct sph_engine {
     hipLaunchKernelGGL(k_pc_append, dim3(blocks(nins)), dim3(BLK), 0, s, nins, nrec.p, n,
                        p.to_type, tag_next, xf.p, vr.p, vel.p, en.p, rm.p, cvv.p, cg.p, ty.p,
                        tag.p, fo.p, de.p);
-    SPH_HIP_TRY(hipStreamSynchronize(s));  // (the scratch buffers are freed on return)
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host staging vectors go out of scope)
     nlocal = n + nins;
     nghost = 0;
     tag_next += nins;
@@ -1941,7 +1964,10 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
   for (auto *b : {&e->cg, &e->cgS, &e->cgF, &e->recA, &e->recK, &e->recF, &e->recS}) b->release();
   if (e->dm) (void)hipFree(e->dm);
-  for (auto *b : {&e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self}) b->release();
+  for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->pc_flag,
+                  &e->pc_cand, &e->pc_otag, &e->pc_idx})
+    b->release();
+  for (auto *b : {&e->pc_rec, &e->pc_gat, &e->pc_Wd, &e->pc_vals, &e->pc_nrec}) b->release();
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
                   &e->ccnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,

@@ -548,6 +548,19 @@ static __global__ void k_copy_counts(int n, const int *__restrict__ cnt, int *__
   if (i == n) off[i] = 0;
 }
 
+// fixed-stride rows (row i at i*stride, cnt[i] entries) -> CSR rows at off[i]; 32 lanes a
+// row (128-B runs per access)
+static __global__ void k_compact_rows(int n, int stride, const int *__restrict__ cnt,
+                                      const int *__restrict__ off, const int *__restrict__ src,
+                                      int *__restrict__ dst) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (int)(t >> 5), lane = (int)(t & 31);
+  if (i >= n) return;
+  const int c = cnt[i], o = off[i];
+  const int *const r = src + (size_t)i * stride;
+  for (int k = lane; k < c; k += 32) dst[o + k] = __builtin_nontemporal_load(r + k);
+}
+
 // ---- setup-step forces with the reference's half-list ownership --------------------------
 // On the first run after atoms are created, ghosts carry the vest they had at borders()
 // (zero for new atoms) while owned atoms already have vest = v (Verlet::setup calls

@@ -1013,12 +1013,15 @@ struct sph_engine {
     mx.reserve(8);
     // single pass into fixed-stride rows when a previous build sized them and nothing
     // needs the CSR form (the setup's half-list pass)
-    if (!csr && list_stride > 0 && row2_fits((long)nall, (long)n * list_stride)) {
+    // (the multiphase passes index rows with 64-bit offsets: plain rows, any size)
+    const bool sfits = mp ? (long)n * list_stride < 0x7fffffffL
+                          : row2_fits((long)nall, (long)n * list_stride);
+    if (!csr && list_stride > 0 && sfits) {
       // rows stored chunk-transposed for the row2 kernels' 16-B index loads; with several
       // types the neighbour's type rides in the entry's top bits
-      list_perm_g = row2_iv() ? row2_iv_g() : 0;
-      list_perm_pi = row2_pi() ? 1 : 0;
-      list_tbits = !nt1() && tbits_env();
+      list_perm_g = (row2_iv() && !mp) ? row2_iv_g() : 0;
+      list_perm_pi = (row2_pi() && !mp) ? 1 : 0;
+      list_tbits = !nt1() && tbits_env() && !mp;
       nbr.reserve((size_t)n * list_stride);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, sizeof(int), s));
       launch(true, list_stride);
@@ -1176,15 +1179,16 @@ struct sph_engine {
   // from the bins (no global-index list on a plain rebuild); the row path's strided list
   // if a block overflows its LDS image.
   void build_all(bool need_csr) {
-    need_csr = need_csr || mp;  // (the multiphase passes walk the CSR full and half lists)
+    // (the multiphase passes walk global-index full rows carrying each pair's half-list
+    // orientation, k_neigh3: CSR at setup, fixed-stride rows once the setup sized them)
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p, vel.p);
     if (multi()) exchange_multi();
     if (cfg.sort) sort_owned();
     borders();
     bin_q();
     blk = false;
-    if (need_csr || !want_blk()) list_q(need_csr);
-    if (mp) {  // (the CSR rows carry each pair's half-list orientation, k_neigh3)
+    if (need_csr || !want_blk() || mp) list_q(need_csr);
+    if (mp) {
       ov_ready = false;
       return;
     }
@@ -1487,6 +1491,8 @@ struct sph_engine {
     de.reserve(n > 0 ? n : 1, true, s);
     if (n == 0) return;
     MpArgs a{};
+    a.stride = strided ? list_stride : 0;  // (else CSR: off)
+    a.cnt = ccnt.p;
     a.inum = n;
     a.nlocal = n;
     a.newton = 1;
@@ -1638,7 +1644,7 @@ struct sph_engine {
     otag.reserve(ncand);
     hipLaunchKernelGGL(k_pc_candidates<8>, mp_rows(ncand), dim3(256), 0, s, ncand, cand.p,
                        (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p, 4,
-                       ty.p, rm.p, pd, rec.p);
+                       ty.p, rm.p, pd, rec.p, strided ? list_stride : 0, ccnt.p);
     hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
                        vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
     std::vector<int> hc(ncand), ht(ncand);
@@ -1693,7 +1699,8 @@ struct sph_engine {
     // comm, rmass -= dmass and e renormalised, then the new atoms
     hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
     hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
-                       (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p);
+                       (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p,
+                       strided ? list_stride : 0, ccnt.p);
     reverse1(dmass.p);
     hipLaunchKernelGGL(k_pc_finish, dim3(blocks(n)), dim3(BLK), 0, s, n, dmass.p, rm.p, en.p);
     ensure_atoms((size_t)n + nins, true);  // (over the ghost slots: the rebuild follows)

@@ -132,6 +132,22 @@ struct MpArgs {
   // colorgradient: (x, y, z, sigma = rho / rmass) per atom, rho as it stands (nullptr: the
   // kernel reads xf, vr, rm)
   const double4 *xs;
+  // stride > 0: fixed-stride rows (row r at r*stride, cnt[r] entries) instead of CSR off
+  int stride;
+  const int *cnt;
+};
+// a list row's entries [beg, end): CSR (off) or fixed-stride rows (stride, cnt)
+struct MpRow {
+  int beg, end;
+  __device__ __forceinline__ MpRow(const int *off, const int *cnt, int stride, int row) {
+    if (stride > 0) {
+      beg = row * stride;
+      end = beg + cnt[row];
+    } else {
+      beg = off[row];
+      end = off[row + 1];
+    }
+  }
 };
 
 template <int G>
@@ -146,7 +162,8 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
   const int it = a.ty[i];
   const int dim = a.dim;
   double acc = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  for (int k = rw.beg + lane; k < rw.end; k += G) {
     const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xf[j];
     const int jt = a.ty[j];
@@ -247,7 +264,8 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
   const int it = a.ty[i];
   const double sigmai = a.xs ? xi.w : a.vr[i].w / a.rm[i];
   double gx = 0.0, gy = 0.0, gz = 0.0;
-  for (int k = a.off[row] + lane; k < a.off[row + 1]; k += G) {
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  for (int k = rw.beg + lane; k < rw.end; k += G) {
     const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xs ? a.xs[j] : a.xf[j];
     const int jt = a.ty[j];
@@ -466,8 +484,9 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
   // two entries per lane and round, both entries' records loaded before either is used
   // (the loop is latency-bound on the index -> record chain otherwise)
   constexpr int NU = 2;
-  const int kend = a.off[row + 1];
-  for (int k0 = a.off[row] + lane; k0 < kend; k0 += NU * G) {
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  const int kend = rw.end;
+  for (int k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
     int jrs[NU];
     double4 xjs[NU], v4js[NU], cjs[NU];
     int tjs[NU];

@@ -57,7 +57,8 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
                 const int *__restrict__ off, const int *__restrict__ nbr,
                 const double4 *__restrict__ xf, const double4 *__restrict__ vr,
                 const double *__restrict__ vel, int vstride, const int *__restrict__ ty,
-                const double *__restrict__ rm, PcDev p, double *__restrict__ rec) {
+                const double *__restrict__ rm, PcDev p, double *__restrict__ rec,
+                int lstride = 0, const int *__restrict__ lcnt = nullptr) {
   const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (k >= ncand) return;
@@ -67,7 +68,8 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
   const double cut2 = p.cutoff * p.cutoff;
   int around = 0;
   double W = 0.0, sv0 = 0.0, sv1 = 0.0, sv2 = 0.0, se0 = 0.0, se1 = 0.0, se2 = 0.0;
-  for (int q = off[row] + lane; q < off[row + 1]; q += G) {
+  const MpRow rw(off, lcnt, lstride, row);
+  for (int q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type) continue;
     const double4 xj = xf[j];
@@ -115,7 +117,7 @@ k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wt
            const int *__restrict__ ilist, const int *__restrict__ off,
            const int *__restrict__ nbr, const double4 *__restrict__ xf,
            const int *__restrict__ ty, const double *__restrict__ rm, PcDev p,
-           double *__restrict__ dmass) {
+           double *__restrict__ dmass, int lstride = 0, const int *__restrict__ lcnt = nullptr) {
   const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (k >= nins) return;
@@ -123,7 +125,8 @@ k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wt
   const int i = ilist ? ilist[row] : row;
   const double4 xi = xf[i];
   const double W = Wtot[k];
-  for (int q = off[row] + lane; q < off[row + 1]; q += G) {
+  const MpRow rw(off, lcnt, lstride, row);
+  for (int q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type || !(rm[j] > 0.5 * p.to_mass)) continue;
     const double4 xj = xf[j];

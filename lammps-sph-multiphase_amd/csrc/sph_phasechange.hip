@@ -79,7 +79,7 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
   hipLaunchKernelGGL(k_pc_candidates<PCG>,
                      dim3((unsigned)(((long long)ncand * PCG + 255) / 256)), dim3(256), 0,
                      c->stream, ncand, cand.p, c->ilist.p, c->off.p, c->nbr.p, c->xf.p,
-                     c->vr.p, vel.p, 3, c->ty.p, c->rm.p, pd, rec.p);
+                     c->vr.p, vel.p, 3, c->ty.p, c->rm.p, pd, rec.p, 0, (const int *)nullptr);
   SPH_HIP_TRY(hipGetLastError());
   std::vector<int> hcand(ncand);
   std::vector<double> hrec((size_t)8 * ncand);
@@ -139,7 +139,7 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     SPH_HIP_TRY(hipMemsetAsync(dm.p, 0, nall * sizeof(double), c->stream));
     hipLaunchKernelGGL(k_pc_dmass<PCG>, dim3((unsigned)(((long long)nins * PCG + 255) / 256)),
                        dim3(256), 0, c->stream, nins, rows.p, Wd.p, c->ilist.p, c->off.p,
-                       c->nbr.p, c->xf.p, c->ty.p, c->rm.p, pd, dm.p);
+                       c->nbr.p, c->xf.p, c->ty.p, c->rm.p, pd, dm.p, 0, (const int *)nullptr);
     SPH_HIP_TRY(hipGetLastError());
     SPH_HIP_TRY(hipMemcpyAsync(dmass, dm.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     SPH_HIP_TRY(hipStreamSynchronize(c->stream));

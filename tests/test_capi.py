@@ -91,3 +91,20 @@ int main(void){
     C = sph_amd.EngineConfig
     assert vals == [ctypes.sizeof(C), C.tait_on.offset, C.heat_cut.offset, C.sort.offset,
                     ctypes.sizeof(sph_amd.EngineStats)]
+
+
+def test_neighlist_row_pointers(sph_amd):
+    """NeighList (what the shim hands to sph_hip_list_keyed): firstneigh[i] points at row i
+    of the CSR array, numneigh = row lengths, ilist = identity -- no per-row Python arrays."""
+    off = np.array([0, 3, 3, 7, 8], dtype=np.int64)
+    nb = np.arange(8, dtype=np.int32) + 100
+    nl = sph_amd.NeighList(off, nb)
+    assert nl.inum == 4
+    assert list(nl.numneigh) == [3, 0, 4, 1]
+    assert list(nl.ilist) == [0, 1, 2, 3]
+    for i in range(4):
+        row = np.ctypeslib.as_array(ctypes.cast(int(nl.ptrs[i]), ctypes.POINTER(ctypes.c_int32)),
+                                    shape=(int(nl.numneigh[i]) or 1,))
+        assert list(row[:nl.numneigh[i]]) == list(nb[off[i]:off[i + 1]])
+    empty = sph_amd.NeighList(np.zeros(1, np.int64), np.zeros(0, np.int32))
+    assert empty.inum == 0 and len(empty.ptrs) == 1

@@ -23,13 +23,13 @@ CORE="pair.cpp memory.cpp error.cpp comm.cpp comm_brick.cpp neighbor.cpp neigh_f
       neigh_half_bin.cpp neigh_half_nsq.cpp neigh_half_multi.cpp neigh_half_respa.cpp
       neigh_derive.cpp neigh_stencil.cpp neigh_list.cpp neigh_request.cpp neigh_bond.cpp
       neigh_gran.cpp neigh_full.cpp neigh_respa.cpp atom_vec.cpp citeme.cpp fix.cpp
-      group.cpp"
+      group.cpp random_park.cpp region.cpp region_block.cpp"
 SPH="atom_vec_meso.cpp atom_vec_meso_multiphase.cpp pair_sph_rhosum.cpp
      pair_sph_taitwater.cpp pair_sph_taitwater_morris.cpp pair_sph_heatconduction.cpp
      pair_sph_rhosum_multiphase.cpp pair_sph_taitwater_multiphase.cpp
      pair_sph_heatconduction_phasechange.cpp pair_sph_colorgradient.cpp
      pair_sph_surfacetension.cpp sph_kernel_quintic.cpp sph_energy_equation.cpp
-     fix_meso.cpp fix_meso_stationary.cpp"
+     fix_meso.cpp fix_meso_stationary.cpp fix_phase_change.cpp"
 
 # the reference's own serial build: g++ -O3 at the compiler's default C++ dialect (src/MAKE/
 # Makefile.serial:9-10); the dialect matters -- under C++98 pow(double,int) is __builtin_powi

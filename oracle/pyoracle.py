@@ -63,6 +63,60 @@ def phasechange(p: "PcParams", seed, nlocal, x, v, vest, cg, e, rmass, rho, cv, 
     return sd.value, n, rec[:min(n, cap)].copy(), par[:min(n, cap)].copy(), dmass
 
 
+def pc_params_from_args(args, dim, boxlo, boxhi, dt) -> "PcParams":
+    """FixPhaseChange's argument list (fix_phase_change.cpp:46-87, options :358-390) ->
+    PcParams for one process owning the whole box."""
+    a = [str(v) for v in args]
+    p = PcParams()
+    p.dim = int(dim)
+    p.Tc, p.Tt, p.Hwv, p.dr, p.to_mass, p.cutoff = (float(v) for v in a[3:9])
+    p.from_type, p.to_type = int(a[9]), int(a[10])
+    m = 13
+    if a[m] == "ENERGY":
+        p.energy_chance, p.rate, m = 1, float(a[m + 1]), m + 2
+    else:
+        p.energy_chance, p.change_chance, m = 0, float(a[m]), m + 1
+    p.maxattempt = 10
+    while m < len(a):
+        if a[m] == "attempt":
+            p.maxattempt = int(a[m + 1])
+        m += 2
+    p.dt = float(dt)
+    for k in range(3):
+        p.sublo[k], p.subhi[k], p.boxhi[k] = float(boxlo[k]), float(boxhi[k]), float(boxhi[k])
+        p.top[k] = 1
+    return p
+
+
+def pre_exchange_ref(p: "PcParams", seed, g: "Ghosted", arrays: dict, off, neigh, extra=64):
+    """FixPhaseChange::pre_exchange with the reference's memory behaviour (oracle
+    orc_pre_exchange_ref).  arrays: x, v, vest, cg, e, rmass, rho, cv, type over the g.nall
+    atoms (LAMMPS order).  Returns (seed, new nlocal, arrays after the call, cut to the new
+    nlocal)."""
+    nmax = g.nall + extra
+    a = {}
+    for k in ("x", "v", "vest", "cg"):
+        b = np.zeros((nmax, 3))
+        b[:g.nall] = arrays[k]
+        a[k] = b
+    for k in ("e", "rmass", "rho", "cv"):
+        b = np.zeros(nmax)
+        b[:g.nall] = arrays[k]
+        a[k] = b
+    t = np.zeros(nmax, dtype=np.int32)
+    t[:g.nall] = arrays["type"]
+    a["type"] = t
+    sd = C.c_int(int(seed))
+    dm = np.zeros(nmax)
+    n = lib().orc_pre_exchange_ref(C.byref(p), C.byref(sd), g.nlocal, g.nghost, nmax, a["x"],
+                                   a["v"], a["vest"], a["cg"], a["e"], a["rmass"], a["rho"],
+                                   a["cv"], a["type"], off, _nz(neigh), len(g.swap_first) - 1,
+                                   g.swap_first, _nz(g.src), dm)
+    if n < 0:
+        return pre_exchange_ref(p, seed, g, arrays, off, neigh, extra * 4)
+    return sd.value, n, {k: v[:n].copy() for k, v in a.items()}
+
+
 def build_oracle() -> str:
     src = os.path.join(HERE, "sph_oracle.c")
     if (not os.path.exists(ORACLE_SO)) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
@@ -82,6 +136,14 @@ def lib():
         L.orc_pbc.argtypes = [P, _i, _dp]
         L.orc_borders.argtypes = [P, _d, _i, _dp, _ip, _i, _ip, _ip]
         L.orc_borders.restype = _i
+        L.orc_borders_ex.argtypes = [P, _d, _i, _dp, _ip, _i, _ip, _ip, _ip, _ip,
+                                     C.POINTER(_i)]
+        L.orc_borders_ex.restype = _i
+        L.orc_reverse_swaps.argtypes = [_i, _i, _ip, _ip, _dp]
+        L.orc_pre_exchange_ref.argtypes = [C.POINTER(PcParams), C.POINTER(_i), _i, _i, _i,
+                                           _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _lp,
+                                           _ip, _i, _ip, _ip, _dp]
+        L.orc_pre_exchange_ref.restype = _i
         L.orc_forward_comm.argtypes = [P, _i, _i, _ip, _ip, _dp, C.c_void_p, C.c_void_p,
                                        C.c_void_p]
         L.orc_reverse_comm.argtypes = [_i, _i, _ip, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -167,6 +229,15 @@ def ref():
                                         _ip, _dp]
         R.ref_surfacetension.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
                                          _lp, _ip, _dp]
+        R.ref_pc_new.argtypes = [_i, _i, _dp, _dp, _l, _d, _i, C.POINTER(C.c_char_p)]
+        R.ref_pc_new.restype = C.c_void_p
+        R.ref_pc_pre_exchange.argtypes = [C.c_void_p, _l, _i, _i, _i, _dp, _dp, _dp, _dp,
+                                          _dp, _dp, _dp, _dp, _ip, _lp, _ip, _i, _ip, _ip,
+                                          C.POINTER(_l)]
+        R.ref_pc_pre_exchange.restype = _i
+        R.ref_pack_restart.argtypes = [_i, _i, _dp, _ip, _ip, _ip, _ip, _dp, _dp, _dp, _dp,
+                                       _dp, _dp, _dp, _i, _dp]
+        R.ref_pack_restart.restype = _i
         for n in ("ref_kernel_quintic2d", "ref_kernel_quintic3d", "ref_dw_quintic2d",
                   "ref_dw_quintic3d"):
             getattr(R, n).argtypes = [_d]
@@ -275,6 +346,8 @@ class Ghosted:
     type: np.ndarray
     owner: np.ndarray        # (nghost,)
     image: np.ndarray        # (nghost,3)
+    src: np.ndarray | None = None         # (nghost,) sendlist entry each ghost came from
+    swap_first: np.ndarray | None = None  # (nswap+1,) first ghost of each CommBrick swap
 
     @property
     def nall(self) -> int:
@@ -298,12 +371,17 @@ def borders(sysm: System, cutghost: float, x: np.ndarray | None = None) -> Ghost
         own = np.zeros(nmax, dtype=np.int32)
         img = np.zeros(3 * nmax, dtype=np.int32)
         d = sysm.domain()
-        ng = L.orc_borders(C.byref(d), cutghost, n, xa, ta, nmax, own, img)
+        src = np.zeros(nmax, dtype=np.int32)
+        sf = np.zeros(8, dtype=np.int32)
+        ns = C.c_int(0)
+        ng = L.orc_borders_ex(C.byref(d), cutghost, n, xa, ta, nmax, own, img, src, sf,
+                              C.byref(ns))
         if ng >= 0:
             break
         nmax *= 2
     return Ghosted(n, ng, xa[:n + ng].copy(), ta[:n + ng].copy(), own[:ng].copy(),
-                   img[:3 * ng].reshape(-1, 3).copy())
+                   img[:3 * ng].reshape(-1, 3).copy(), src[:ng].copy(),
+                   sf[:ns.value + 1].copy())
 
 
 def cutneighsq(ntypes: int, cutmax: np.ndarray, skin: float):
@@ -779,38 +857,50 @@ class MpRefRun:
 
     def _phase_change(self):
         """FixPhaseChange::pre_exchange (fix_phase_change.cpp:167-352) on the last build's
-        full list: owned x as integrated, ghosts as last communicated."""
+        full list: owned x as integrated, ghosts as last communicated.  self.pc_exact (the
+        default): orc_pre_exchange_ref, the reference's own memory behaviour (created atoms
+        over ghost slots, reverse comm along the swaps; pinned to the reference by
+        tests/test_phasechange_golden.py).  Otherwise the port semantics (orc_phasechange:
+        every candidate on the atoms as found)."""
         s, g, L = self.s, self.g, lib()
         n = s.n
         p = pc_params(s, self.ph.pc, self.ph.dt)
-        x_all = np.ascontiguousarray(np.concatenate([s.x, g.x[n:]]))
-        v_all = np.ascontiguousarray(np.concatenate([s.v, self.v_all[n:]]))
-        vest_all = np.ascontiguousarray(np.concatenate([self.vest, self.vest_all[n:]]))
-        e_all = np.ascontiguousarray(np.concatenate([s.e, self.e_all[n:]]))
-        rm_all = np.ascontiguousarray(np.concatenate([s.rmass, self.rm_all[n:]]))
-        rho_all = np.ascontiguousarray(np.concatenate([s.rho, self.rho_all[n:]]))
-        cv_all = np.ascontiguousarray(np.concatenate([s.cv, self.cv_all[n:]]))
-        cg_all = np.ascontiguousarray(np.concatenate([self.cg, self.cg_all[n:]]))
-        seed, nins, rec, par, dmass = phasechange(p, self.seed, n, x_all, v_all, vest_all,
-                                                  cg_all, e_all, rm_all, rho_all, cv_all,
-                                                  g.type, self.foff, self.fnb)
-        self.seed = seed
-        s.e[:] = e_all[:n]
-        reverse_comm(g, None, dmass, None)        # comm->reverse_comm_fix (:324)
-        L.orc_phasechange_finish(n, dmass, s.rmass, s.e)
+        arrays = dict(x=np.concatenate([s.x, g.x[n:]]), v=np.concatenate([s.v, self.v_all[n:]]),
+                      vest=np.concatenate([self.vest, self.vest_all[n:]]),
+                      cg=np.concatenate([self.cg, self.cg_all[n:]]),
+                      e=np.concatenate([s.e, self.e_all[n:]]),
+                      rmass=np.concatenate([s.rmass, self.rm_all[n:]]),
+                      rho=np.concatenate([s.rho, self.rho_all[n:]]),
+                      cv=np.concatenate([s.cv, self.cv_all[n:]]), type=g.type)
+        arrays = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+        if getattr(self, "pc_exact", True):
+            self.seed, nnew, out = pre_exchange_ref(p, self.seed, g, arrays, self.foff, self.fnb)
+            nins = nnew - n
+            s.x, s.v, s.e, s.rmass = out["x"], out["v"], out["e"], out["rmass"]
+            s.rho, s.cv, s.type = out["rho"], out["cv"], out["type"]
+            self.vest, self.cg = out["vest"], out["cg"]
+        else:
+            e_all = arrays["e"]
+            seed, nins, rec, par, dmass = phasechange(
+                p, self.seed, n, arrays["x"], arrays["v"], arrays["vest"], arrays["cg"], e_all,
+                arrays["rmass"], arrays["rho"], arrays["cv"], g.type, self.foff, self.fnb)
+            self.seed = seed
+            s.e[:] = e_all[:n]
+            L.orc_reverse_swaps(n, len(g.swap_first) - 1, g.swap_first, _nz(g.src), dmass)
+            L.orc_phasechange_finish(n, dmass, s.rmass, s.e)
+            if nins:
+                to = int(self.ph.pc["to_type"])
+                s.x = np.concatenate([s.x, rec[:, 0:3]])
+                s.v = np.concatenate([s.v, rec[:, 3:6]])
+                self.vest = np.concatenate([self.vest, rec[:, 6:9]])
+                s.e = np.concatenate([s.e, rec[:, 9]])
+                s.rmass = np.concatenate([s.rmass, rec[:, 10]])
+                s.rho = np.concatenate([s.rho, rec[:, 11]])
+                s.cv = np.concatenate([s.cv, rec[:, 12]])
+                s.type = np.concatenate([s.type, np.full(nins, to, dtype=np.int32)])
+                self.cg = np.concatenate([self.cg, np.zeros((nins, 3))])   # create_atom
         if nins:
-            to = int(self.ph.pc["to_type"])
-            s.x = np.concatenate([s.x, rec[:, 0:3]])
-            s.v = np.concatenate([s.v, rec[:, 3:6]])
-            self.vest = np.concatenate([self.vest, rec[:, 6:9]])
-            s.e = np.concatenate([s.e, rec[:, 9]])
-            s.rmass = np.concatenate([s.rmass, rec[:, 10]])
-            s.rho = np.concatenate([s.rho, rec[:, 11]])
-            s.cv = np.concatenate([s.cv, rec[:, 12]])
-            s.type = np.concatenate([s.type, np.full(nins, to, dtype=np.int32)])
-            self.cg = np.concatenate([self.cg, np.zeros((nins, 3))])   # create_atom
-            for k in ("f",):
-                setattr(self, k, np.concatenate([getattr(self, k), np.zeros((nins, 3))]))
+            self.f = np.concatenate([self.f, np.zeros((nins, 3))])
             self.drho = np.concatenate([self.drho, np.zeros(nins)])
             self.de = np.concatenate([self.de, np.zeros(nins)])
             self.ninserted += nins

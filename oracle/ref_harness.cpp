@@ -49,6 +49,10 @@
 #include "group.h"
 #include "fix_meso.h"
 #include "fix_meso_stationary.h"
+#include "fix_phase_change.h"
+#include "modify.h"
+#include "region.h"
+#include "region_block.h"
 
 using namespace LAMMPS_NS;
 
@@ -81,6 +85,28 @@ struct HNeighbor : public Neighbor {
 
 struct HComm : public CommBrick {
   HComm(LAMMPS *l) : CommBrick(l) { nswap = 0; }
+  using CommBrick::grow_list;
+  using CommBrick::grow_send;
+  using CommBrick::maxsend;
+  using CommBrick::maxsendlist;
+  // self swaps as CommBrick::borders leaves them on one process (comm_brick.cpp:696-864):
+  // swap s received ghosts [first[s], first[s+1]) (offsets past nlocal), each copied from
+  // src[g] (its sendlist entry: an owned atom or a ghost of an earlier swap)
+  void set_self_swaps(int nlocal, int ns, const int *first, const int *src) {
+    if (ns > maxswap) grow_swap(ns);
+    nswap = ns;
+    int most = 0;
+    for (int s = 0; s < ns; s++) {
+      const int n = first[s + 1] - first[s];
+      sendproc[s] = recvproc[s] = me;
+      sendnum[s] = recvnum[s] = n;
+      firstrecv[s] = nlocal + first[s];
+      if (n > maxsendlist[s]) grow_list(s, n);
+      for (int k = 0; k < n; k++) sendlist[s][k] = src[first[s] + k];
+      if (n > most) most = n;
+    }
+    if (most > maxsend) grow_send(most, 0);
+  }
 };
 
 struct HRhoSum : public PairSPHRhoSum {
@@ -669,6 +695,140 @@ int ref_fix_meso(int stationary, int phase, int nlocal, int ntypes, double dt, c
   return 0;
 }
 
+
+// ---- FixPhaseChange (fix_phase_change.cpp), constructed from its own argument list -------
+// A persistent one-process universe: the fix keeps its RanPark stream across
+// ref_pc_pre_exchange calls exactly as it does across a LAMMPS run.  The fix's region is a
+// real RegBlock ("block EDGE x6 units box" = the box, region_block.cpp:26-92), found through
+// Domain::find_region (restated at the bottom of this file: domain.cpp needs the generated
+// style_region.h).  Atom::tag_extend and Atom::map_* (atom.cpp, not built) are kept out of
+// reach with tag_enable = map_style = 0: tags are the caller's bookkeeping.
+struct PCWorld {
+  World *w;
+  Fix *fix;
+  NeighList *list;
+};
+
+void *ref_pc_new(int dim, int ntypes, const double *boxlo, const double *boxhi, long step0,
+                 double dt, int narg, const char **args) {
+  PCWorld *pw = new PCWorld;
+  pw->w = new World(dim, ntypes, 0, 0, 1, 1);
+  World &w = *pw->w;
+  LAMMPS *lmp = w.lmp;
+  Domain *d = lmp->domain;
+  d->box_exist = 1;
+  for (int k = 0; k < 3; k++) {
+    d->boxlo[k] = d->sublo[k] = boxlo[k];
+    d->boxhi[k] = d->subhi[k] = boxhi[k];
+    d->prd[k] = boxhi[k] - boxlo[k];
+    w.comm->procgrid[k] = 1;
+    w.comm->myloc[k] = 0;
+  }
+  lmp->update->ntimestep = step0;
+  lmp->update->dt = dt;
+  lmp->modify = zalloc<Modify>();
+  lmp->group = new Group(lmp);
+  lmp->atom->tag_enable = 0;
+  lmp->atom->map_style = 0;
+  char rid[] = "box", rst[] = "block", edge[] = "EDGE", un[] = "units", bx[] = "box";
+  char *rarg[10] = {rid, rst, edge, edge, edge, edge, edge, edge, un, bx};
+  d->maxregion = 1;
+  d->nregion = 1;
+  d->regions = (Region **)calloc(1, sizeof(Region *));
+  d->regions[0] = new RegBlock(lmp, 10, rarg);
+  pw->fix = new FixPhaseChange(lmp, narg, const_cast<char **>(args));
+  pw->list = NULL;
+  return pw;
+}
+
+// One Modify::pre_exchange of the fix at `step` on nlocal owned + nghost ghost atoms (in
+// LAMMPS' index order, ghosts right after the owned atoms) in arrays with room for nmax
+// atoms; the FULL list rows cover the owned atoms.  Arrays are updated in place; returns
+// atom->nlocal afterwards (created atoms sit at [nlocal, return)).
+int ref_pc_pre_exchange(void *h, long step, int nlocal, int nghost, int nmax, double *x,
+                        double *v, double *vest, double *cg, double *e, double *rmass,
+                        double *rho, double *cv, int *type, const long *off, const int *neigh,
+                        int nswap, const int *swap_first, const int *ghost_src,
+                        long *next_reneighbor) {
+  PCWorld *pw = static_cast<PCWorld *>(h);
+  World &w = *pw->w;
+  Atom *a = w.lmp->atom;
+  a->nlocal = nlocal;
+  a->nghost = nghost;
+  w.nall = nlocal + nghost;
+  w.avec->grow(nmax);
+  for (int i = 0; i < w.nall; i++) {
+    for (int k = 0; k < 3; k++) {
+      a->x[i][k] = x[3 * i + k];
+      a->v[i][k] = v[3 * i + k];
+      a->vest[i][k] = vest[3 * i + k];
+      a->colorgradient[i][k] = cg[3 * i + k];
+      a->f[i][k] = 0.0;
+    }
+    a->e[i] = e[i];
+    a->rmass[i] = rmass[i];
+    a->rho[i] = rho[i];
+    a->cv[i] = cv[i];
+    a->type[i] = type[i];
+    a->mask[i] = 1;
+    a->tag[i] = 0;
+    a->drho[i] = 0.0;
+    a->de[i] = 0.0;
+  }
+  if (pw->list) free_list(pw->list);
+  pw->list = make_list(w, nlocal, off, neigh);
+  pw->fix->init_list(0, pw->list);
+  w.comm->set_self_swaps(nlocal, nswap, swap_first, ghost_src);
+  w.lmp->update->ntimestep = step;
+  pw->fix->pre_exchange();
+  const int n = a->nlocal;
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 3; k++) {
+      x[3 * i + k] = a->x[i][k];
+      v[3 * i + k] = a->v[i][k];
+      vest[3 * i + k] = a->vest[i][k];
+      cg[3 * i + k] = a->colorgradient[i][k];
+    }
+    e[i] = a->e[i];
+    rmass[i] = a->rmass[i];
+    rho[i] = a->rho[i];
+    cv[i] = a->cv[i];
+    type[i] = a->type[i];
+  }
+  if (next_reneighbor) *next_reneighbor = pw->fix->next_reneighbor;
+  return n;
+}
+
+// ---- per-atom restart records: AtomVecMeso::pack_restart (atom_vec_meso.cpp:729-757) and
+// AtomVecMesoMultiPhase::pack_restart (atom_vec_meso_multiphase.cpp:887-916), one call per
+// atom into rec[i*stride...]; returns the record length the routine reported.
+int ref_pack_restart(int multiphase, int n, const double *x, const int *tag, const int *type,
+                     const int *mask, const int *image, const double *v, const double *rho,
+                     const double *cg, const double *rmass, const double *e, const double *cv,
+                     const double *vest, int stride, double *rec) {
+  World w(3, 8, n, 0, 1, multiphase);
+  Atom *a = w.lmp->atom;
+  int len = 0;
+  for (int i = 0; i < n; i++) {
+    for (int k = 0; k < 3; k++) {
+      a->x[i][k] = x[3 * i + k];
+      a->v[i][k] = v[3 * i + k];
+      a->vest[i][k] = vest[3 * i + k];
+      if (multiphase) a->colorgradient[i][k] = cg[3 * i + k];
+    }
+    a->tag[i] = tag[i];
+    a->type[i] = type[i];
+    a->mask[i] = mask[i];
+    a->image[i] = image[i];
+    a->rho[i] = rho[i];
+    a->e[i] = e[i];
+    a->cv[i] = cv[i];
+    if (multiphase) a->rmass[i] = rmass[i];
+  }
+  for (int i = 0; i < n; i++) len = w.avec->pack_restart(i, rec + (size_t)i * stride);
+  return len;
+}
+
 double ref_kernel_quintic3d(double r);
 double ref_dw_quintic3d(double r);
 }
@@ -678,3 +838,11 @@ extern "C" double ref_kernel_quintic3d(double r) { return sph_kernel_quintic3d(r
 extern "C" double ref_dw_quintic3d(double r) { return sph_dw_quintic3d(r); }
 extern "C" double ref_kernel_quintic2d(double r) { return sph_kernel_quintic2d(r); }
 extern "C" double ref_dw_quintic2d(double r) { return sph_dw_quintic2d(r); }
+
+// Domain::find_region (domain.cpp:1436-1441), restated: domain.cpp itself needs the
+// generated style_region.h, so it is not part of the reference build here.
+int LAMMPS_NS::Domain::find_region(char *name) {
+  for (int iregion = 0; iregion < nregion; iregion++)
+    if (strcmp(name, regions[iregion]->id) == 0) return iregion;
+  return -1;
+}

@@ -43,13 +43,27 @@ void orc_pbc(const orc_domain *d, int nlocal, double *x) {
    ------------------------------------------------------------------------------------ */
 int orc_borders(const orc_domain *d, double cutghost, int nlocal, double *x, int *type,
                 int nmax, int *ghost_owner, int *ghost_image) {
-  int nall = nlocal;
+  return orc_borders_ex(d, cutghost, nlocal, x, type, nmax, ghost_owner, ghost_image, NULL,
+                        NULL, NULL);
+}
+
+/* The same, also recording CommBrick's swap structure for a reverse comm done the
+   reference's way (comm_brick.cpp:513-571, 999-1030): ghost_src[g] = the index the ghost
+   was copied from (sendlist entry, owned or an earlier ghost), swap_first[s] = the first
+   ghost of swap s (firstrecv - nlocal), swap_first[nswap] = nghost.  Non-periodic
+   dimensions still count their two (empty) swaps, as CommBrick does. */
+int orc_borders_ex(const orc_domain *d, double cutghost, int nlocal, double *x, int *type,
+                   int nmax, int *ghost_owner, int *ghost_image, int *ghost_src,
+                   int *swap_first, int *nswap) {
+  int nall = nlocal, iswap = 0;
   const int ndim = (d->dim == 2) ? 2 : 3;
   for (int dim = 0; dim < ndim; dim++) {
-    if (!d->periodic[dim]) continue;
     const double prd = d->boxhi[dim] - d->boxlo[dim];
     const int nlast = nall;
     for (int ineed = 0; ineed < 2; ineed++) {
+      if (swap_first) swap_first[iswap] = nall - nlocal;
+      iswap++;
+      if (!d->periodic[dim]) continue;
       double lo, hi, shift;
       int pbc;
       if (ineed == 0) {
@@ -83,12 +97,24 @@ int orc_borders(const orc_domain *d, double cutghost, int nlocal, double *x, int
             ghost_image[3 * g + 2] = ghost_image[3 * gi + 2];
           }
           ghost_image[3 * g + dim] += pbc;
+          if (ghost_src) ghost_src[g] = i;
           nall++;
         }
       }
     }
   }
+  if (swap_first) swap_first[iswap] = nall - nlocal;
+  if (nswap) *nswap = iswap;
   return nall - nlocal;
+}
+
+/* Fix::pack_reverse_comm / unpack_reverse_comm through CommBrick::reverse_comm_fix
+   (comm_brick.cpp:999-1030) for self swaps: swaps in reverse order, each adding its
+   ghosts' values onto the atoms they were copied from (an earlier ghost or the owner). */
+void orc_reverse_swaps(int nlocal, int nswap, const int *swap_first, const int *ghost_src,
+                       double *a) {
+  for (int s = nswap - 1; s >= 0; s--)
+    for (int g = swap_first[s]; g < swap_first[s + 1]; g++) a[ghost_src[g]] += a[nlocal + g];
 }
 
 /* AtomVecMeso::pack_comm/unpack_comm, src/USER-SPH/atom_vec_meso.cpp:246-360.
@@ -1101,4 +1127,126 @@ void orc_phasechange_finish(int nlocal, const double *dmass, double *rmass, doub
     rmass[i] -= dmass[i];
     e[i] = e[i] * mold / rmass[i];
   }
+}
+
+/* FixPhaseChange::pre_exchange, fix_phase_change.cpp:167-352, restated WITH the reference's
+   memory behaviour on one process (the port's orc_phasechange above evaluates every
+   candidate on the atoms as found instead).  The arrays have room for nmax atoms: owned
+   [0, nlocal), ghosts [nlocal, nlocal+nghost).  The k-th atom created by this call goes to
+   index nlocal + k through AtomVecMesoMultiPhase::create_atom
+   (atom_vec_meso_multiphase.cpp:968-997) -- over a ghost slot that later candidates' full
+   lists may still name, and with drho (= the fix's dmass, :193) of that slot zeroed.  Then
+   the ghosts' dmass goes back along CommBrick's swaps (reverse_comm_fix), the donors lose
+   mass and have their energy renormalised (:325-332).  dmass is scratch of nmax.  Returns
+   the new nlocal (owned + created), or -1 when nmax is too small for the created atoms
+   (the reference would grow the arrays there). */
+int orc_pre_exchange_ref(const orc_pc_params *p, int *seed, int nlocal, int nghost, int nmax,
+                         double *x, double *v, double *vest, double *cg, double *e,
+                         double *rmass, double *rho, double *cv, int *type, const long *off,
+                         const int *neigh, int nswap, const int *swap_first,
+                         const int *ghost_src, double *dmass) {
+  const int nall = nlocal + nghost;
+  int ncur = nlocal;
+  for (int i = 0; i < nall; i++) dmass[i] = 0.0;   /* force->newton on (:196-201) */
+  for (int i = 0; i < nlocal; i++) {
+    const double Ti = e[i] / cv[i];
+    int isphasechange;
+    if ((Ti < p->Tc) || (type[i] != p->to_type)) {
+      isphasechange = 0;
+    } else if (p->energy_chance) {
+      const double threshold = (e[i] - p->Tc * cv[i]) / p->Hwv * p->dt * p->rate;
+      isphasechange = (orc_park_uniform(seed) < threshold) && pc_around(p, i, x, type, off, neigh);
+    } else {
+      isphasechange = (orc_park_uniform(seed) < p->change_chance) && (Ti > p->Tt) &&
+                      pc_around(p, i, x, type, off, neigh);
+    }
+    if (!isphasechange) continue;
+    double coord[3];
+    int ok = 0, natempt = 0;
+    double delta = p->dr;
+    do {
+      pc_newpos(p->dim, seed, x + 3 * i, cg + 3 * i, delta, coord);
+      ok = pc_mine(p, coord);
+      delta = 0.75 * delta;
+      natempt++;
+    } while (!ok && natempt < p->maxattempt);
+    if (!ok) {
+      delta = p->dr;
+      natempt = 0;
+      do {
+        pc_newpos_simple(seed, x + 3 * i, delta, coord);
+        ok = pc_mine(p, coord);
+        delta = 0.75 * delta;
+        natempt++;
+      } while (!ok && natempt < p->maxattempt);
+    }
+    if (!ok) continue;
+    /* insert_one_atom -> create_atom(to_type, coord) at m = ncur (:455-462) */
+    if (ncur >= nmax) return -1;
+    const int m = ncur++;
+    type[m] = p->to_type;
+    for (int k = 0; k < 3; k++) {
+      x[3 * m + k] = coord[k];
+      v[3 * m + k] = 0.0;
+      cg[3 * m + k] = 0.0;
+      vest[3 * m + k] = 0.0;
+    }
+    rho[m] = 0.0;
+    rmass[m] = 0.0;
+    e[m] = 0.0;
+    cv[m] = 1.0;
+    dmass[m] = 0.0;
+    /* weights and mass taken, over the atoms now in the list's slots (:242-300) */
+    double wtotal = 0.0;
+    for (long jj = off[i]; jj < off[i + 1]; jj++) {
+      const int j = neigh[jj];
+      if (type[j] == p->from_type && rmass[j] > 0.5 * p->to_mass) {
+        const double delx = x[3 * i] - x[3 * j];
+        const double dely = x[3 * i + 1] - x[3 * j + 1];
+        const double delz = x[3 * i + 2] - x[3 * j + 2];
+        const double rsq = delx * delx + dely * dely + delz * delz;
+        wtotal += (p->dim == 3) ? orc_kernel_quintic3d(sqrt(rsq) * p->cutoff)
+                                : orc_kernel_quintic2d(sqrt(rsq) * p->cutoff);
+      }
+    }
+    double dmom[3] = {0, 0, 0}, dmomest[3] = {0, 0, 0};
+    for (long jj = off[i]; jj < off[i + 1]; jj++) {
+      const int j = neigh[jj];
+      if (type[j] == p->from_type && rmass[j] > 0.5 * p->to_mass) {
+        const double delx = x[3 * i] - x[3 * j];
+        const double dely = x[3 * i + 1] - x[3 * j + 1];
+        const double delz = x[3 * i + 2] - x[3 * j + 2];
+        const double rsq = delx * delx + dely * dely + delz * delz;
+        const double wfd = (p->dim == 3) ? orc_kernel_quintic3d(sqrt(rsq) * p->cutoff)
+                                         : orc_kernel_quintic2d(sqrt(rsq) * p->cutoff);
+        const double dmass_aux = p->to_mass * wfd / wtotal;
+        dmass[j] += dmass_aux;
+        dmom[0] += v[3 * j] * dmass_aux;
+        dmom[1] += v[3 * j + 1] * dmass_aux;
+        dmom[2] += v[3 * j + 2] * dmass_aux;
+        dmomest[0] += vest[3 * j] * dmass_aux;
+        dmomest[1] += vest[3 * j + 1] * dmass_aux;
+        dmomest[2] += vest[3 * j + 2] * dmass_aux;
+      }
+    }
+    /* the new atom (:302-318): m = atom->nlocal - 1 */
+    rmass[m] = p->to_mass;
+    rho[m] = rho[i];
+    cv[m] = cv[i];
+    for (int k = 0; k < 3; k++) {
+      v[3 * m + k] = dmom[k] / p->to_mass;
+      vest[3 * m + k] = dmomest[k] / p->to_mass;
+    }
+    const double energy_aux = 0.5 * (e[i] - p->Hwv);
+    e[i] = energy_aux;
+    e[m] = energy_aux;
+  }
+  orc_reverse_swaps(nlocal, nswap, swap_first, ghost_src, dmass);   /* :324 */
+  for (int i = 0; i < nlocal; i++) {
+    const double mold = rmass[i];
+    rmass[i] -= dmass[i];
+    e[i] = e[i] * mold / rmass[i];
+    dmass[i] = 0;
+  }
+  return ncur;
 }

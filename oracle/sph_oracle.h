@@ -55,6 +55,14 @@ void orc_pbc(const orc_domain *d, int nlocal, double *x);
    Returns nghost, or -1 if nmax would be exceeded. */
 int orc_borders(const orc_domain *d, double cutghost, int nlocal, double *x, int *type,
                 int nmax, int *ghost_owner, int *ghost_image);
+/* orc_borders plus CommBrick's swap structure: ghost_src[g] = sendlist entry the ghost was
+   copied from, swap_first[0..nswap] = first ghost of each swap (nullable outputs) */
+int orc_borders_ex(const orc_domain *d, double cutghost, int nlocal, double *x, int *type,
+                   int nmax, int *ghost_owner, int *ghost_image, int *ghost_src,
+                   int *swap_first, int *nswap);
+/* CommBrick::reverse_comm_fix over self swaps (comm_brick.cpp:999-1030), one double/atom */
+void orc_reverse_swaps(int nlocal, int nswap, const int *swap_first, const int *ghost_src,
+                       double *a);
 
 /* ghost <- owner (+ image*prd on x), for x, rho, e, vest (AtomVecMeso::pack_comm). any of
    rho/e/vest may be NULL. */
@@ -199,6 +207,14 @@ int orc_phasechange(const orc_pc_params *p, int *seed, int nlocal, int nall, con
                     int cap, double *new_atoms, int *parent);
 /* after reverse comm of dmass: rmass -= dmass, e renormalised (fix_phase_change.cpp:327-334) */
 void orc_phasechange_finish(int nlocal, const double *dmass, double *rmass, double *e);
+/* The whole pre_exchange with the reference's memory behaviour (created atoms written over
+   ghost slots, reverse comm along CommBrick's swaps); see sph_oracle.c.  Returns the new
+   nlocal or -1. */
+int orc_pre_exchange_ref(const orc_pc_params *p, int *seed, int nlocal, int nghost, int nmax,
+                         double *x, double *v, double *vest, double *cg, double *e,
+                         double *rmass, double *rho, double *cv, int *type, const long *off,
+                         const int *neigh, int nswap, const int *swap_first,
+                         const int *ghost_src, double *dmass);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,24 @@ def test_layouts_roundtrip():
     assert np.array_equal(d["image"], img)
 
 
+def test_layouts_match_reference_pack_restart():
+    """tests/golden/restart_records.npz holds records written by the reference's own
+    pack_restart routines (make_restart.py): the restated layouts -- which the engine's
+    write_restart is checked against below -- reproduce them bit for bit."""
+    import os
+    d = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                  "restart_records.npz")))
+    m = po.pack_restart_meso(d["x"], d["tag"], d["type"], d["image"], d["v"], d["rho"], d["e"],
+                             d["cv"], d["vest"], mask=d["mask"])
+    assert np.array_equal(m.view(np.int64), d["rec_meso"].view(np.int64))
+    p = po.pack_restart_multiphase(d["x"], d["tag"], d["type"], d["image"], d["v"], d["rho"],
+                                   d["cg"], d["rmass"], d["e"], d["cv"], d["vest"],
+                                   mask=d["mask"])
+    assert np.array_equal(p.view(np.int64), d["rec_multiphase"].view(np.int64))
+    u = po.unpack_restart(d["rec_multiphase"])
+    assert np.array_equal(u["image"], d["image"]) and np.array_equal(u["tag"], d["tag"])
+
+
 def test_oracle_images_unwrap_continuously():
     s, ph = drifting_c2()
     ref = po.RefRun(s, ph)

@@ -181,6 +181,12 @@ def device_count() -> int:
     return load().sph_hip_device_count()
 
 
+def phasechange_finish(nlocal, dmass, rmass, e):
+    """sph_hip_phasechange_finish: rmass -= dmass, e renormalised (fix_phase_change.cpp:
+    325-332), in place on the owned atoms."""
+    _chk(load().sph_hip_phasechange_finish(int(nlocal), dmass, rmass, e))
+
+
 def _ptr(a):
     return None if a is None else a.ctypes.data
 

@@ -147,7 +147,7 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
             int *__restrict__ ulist, int *__restrict__ ucnt, int *__restrict__ rcnt,
             unsigned short *__restrict__ snbr, int *__restrict__ ovf, int *__restrict__ umax,
             int cq, int bexp) {
-  // bexp (study, SPH_BEXP; outputs meaningless): 1 = no candidate loads, 2 = no row
+  // bexp (study builds only, SPH_BEXP; outputs meaningless): 1 = no candidate loads, 2 = no row
   // tests, 4 = no slot-row stores, 8 = no union stores
   constexpr int TPR = BLK_TPR, BLK_BT = R * TPR;
   constexpr int W = MC / 32;
@@ -725,7 +725,11 @@ static __global__ void k_blk_large(int nb, const int *__restrict__ ucnt, int um,
 // ---- host-side launch helpers ----------------------------------------------------------
 // Block shapes (rows per block R, lanes per row G, slots per lane and chunk U); SPH_BLK
 // picks one (tuning).  R*G threads per pair-pass workgroup.
+#ifdef SPH_STUDY
 #define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4) X(2, 32, 16, 2)
+#else
+#define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4)
+#endif
 constexpr int BLK_NCH = 8;  // slot chunks preloaded per row (rows up to BLK_NCH*U*G entries)
 struct BlkShape {
   int R, G, U;
@@ -849,9 +853,11 @@ inline void blk_force_n(int visc, int mode, hipStream_t s, const BlkArgs &k, con
   switch (mode) {
     case M_TAIT:
       if (mor) blk_force_t<R, G, U, NCH, 1, M_TAIT, NT1>(s, k, a);
+#ifdef SPH_STUDY  // (outputs meaningless: study builds only, make STUDY=1)
       else if (NT1 && k.exp == 1) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 1>(s, k, a);
       else if (NT1 && k.exp == 2) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 2>(s, k, a);
       else if (NT1 && k.exp == 3) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 3>(s, k, a);
+#endif
       else blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1>(s, k, a);
       break;
     case M_TAIT | M_HEAT:

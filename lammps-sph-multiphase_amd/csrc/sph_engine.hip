@@ -32,24 +32,33 @@ static int env_int(const char *name, int dflt) {
   const char *s = getenv(name);
   return s ? atoi(s) : dflt;
 }
+// Study knobs (tools/kernel_sweep.py, tools/build_sweep.py) exist only in study builds
+// (make STUDY=1 -> -DSPH_STUDY); the production library ignores the variables, so no
+// environment setting can change its results or run a variant whose outputs are
+// meaningless.
+#ifdef SPH_STUDY
+static int study_int(const char *name, int dflt) { return env_int(name, dflt); }
+#else
+static int study_int(const char *, int dflt) { return dflt; }
+#endif
 // SPH_ROW2TILE: shape index of SPH_ROW2_TILES (default 3 = 8 lanes x 4 pairs, the fastest
 // with lane-pair gathers on C2 1M: profiles/r01/sweep_row2.log)
 int row2_tile() {
-  static int t = env_int("SPH_ROW2TILE", 3);
+  static int t = study_int("SPH_ROW2TILE", 3);
   return t;
 }
 }  // namespace sph
 // SPH_MORTON_DIV (default 4, the fastest of 1/2/4/8 on C2 1M for the row path): cells per
 // bin edge of the owned atoms' sort key (Morton for the row path, Hilbert for the block path)
 static int morton_div() {
-  static int v = std::max(1, env_int("SPH_MORTON_DIV", 4));
+  static int v = std::max(1, study_int("SPH_MORTON_DIV", 4));
   return v;
 }
 // Row path (kernel_path 1) knobs.  SPH_LP (default 1): lane-pair gathers in the row2
 // kernels; SPH_IV (default 1): the strided list is stored chunk-transposed so each lane's
 // four indices of a chunk are one 16-B load (sph_row2_kernels.h).
 static bool row2_lp() {
-  static bool v = env_int("SPH_LP", 1) != 0;
+  static bool v = study_int("SPH_LP", 1) != 0;
   return v;
 }
 // SPH_TIGHT (default 0): with a strided list, the rhosum pass writes this step's in-cut
@@ -57,22 +66,22 @@ static bool row2_lp() {
 // Measured on C2 1M: taitwater 0.57 -> 0.46 ms but rhosum 0.31 -> 0.48 ms (the stores
 // count in vmcnt, so the loop waits for them with the prefetched indices) -> off.
 static bool tight_on() {
-  static bool v = env_int("SPH_TIGHT", 0) != 0;
+  static bool v = study_int("SPH_TIGHT", 0) != 0;
   return v;
 }
 // SPH_PI (default 0): pair-interleaved entry slots with lane-pair gathers (entry_slot).
 // Measured on C2 1M: taitwater 0.562 (off) vs 0.567 ms (on), rhosum equal -> off.
 static bool row2_pi() {
-  static bool v = env_int("SPH_PI", 0) != 0 && row2_lp();
+  static bool v = study_int("SPH_PI", 0) != 0 && row2_lp();
   return v;
 }
 static bool row2_iv() {
-  static bool v = env_int("SPH_IV", 1) != 0;
+  static bool v = study_int("SPH_IV", 1) != 0;
   return v;
 }
 // SPH_EXP: study variants of the pair passes (tools/kernel_sweep.py sets it for the timed
 // passes only, so it is read per launch); 0 in production
-static int row2_exp() { return env_int("SPH_EXP", 0); }
+static int row2_exp() { return study_int("SPH_EXP", 0); }
 // SPH_OVERLAP (default 0): with a brick decomposition, run the pair passes of interior
 // rows (no ghost in the list) on a second stream while the forward / rho halos are in
 // flight, then the boundary rows after them (sph_engine::pair_compute_overlap).  Parity
@@ -83,13 +92,13 @@ static int row2_exp() { return env_int("SPH_EXP", 0); }
 // SPH_TBITS (default 1): with several types, strided list entries carry the neighbour's
 // type in their top bits, so the row2 passes skip the per-neighbour type gather
 static bool tbits_env() {
-  static bool v = env_int("SPH_TBITS", 1) != 0;
+  static bool v = study_int("SPH_TBITS", 1) != 0;
   return v;
 }
 // SPH_BLK (default 0 = 64-row blocks, 8 lanes x 4 slots; the fastest pair passes on C2 1M):
 // block shape of the block-staged path (SPH_BLK_SHAPES)
 static int blk_shape_env() {
-  static int v = env_int("SPH_BLK", 0);
+  static int v = study_int("SPH_BLK", 0);
   return v;
 }
 // (read per engine at sph_engine_create)
@@ -131,7 +140,8 @@ struct sph_engine {
   DBuf<double4> cg, cgS, cgF;
   DBuf<double4> recA, recK, recF, recS;  // k_mp_gather's packed records (k_mp_pack_rec)
   // fix phase_change scratch, kept across calls (no allocation per step)
-  DBuf<int> pc_flag, pc_cand, pc_otag, pc_idx;
+  DBuf<int> pc_flag, pc_cand, pc_otag, pc_idx, pc_minr, pc_one, pc_grank, pc_key, pc_val, gsrc;
+  std::vector<int> gswap_first;  // one brick: first ghost of each swap (+ nghost at the end)
   DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec;
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
@@ -878,6 +888,7 @@ struct sph_engine {
     int nall = nlocal;
     const int ndim = cfg.dim;
     nsel.reserve(1);
+    gswap_first.clear();
     for (int d = 0; d < ndim; d++) {
       if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
       const int nlast = nall;
@@ -903,10 +914,16 @@ struct sph_engine {
         tmp_reserve(tb);
         SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flags.p, sel.p, nsel.p, nlast, s));
         const int ns = read_scalar(nsel.p);
+        gswap_first.push_back(nall - nlocal);
         if (ns == 0) continue;
         ensure_atoms((size_t)nall + ns, true);
         gowner.reserve((size_t)nall + ns - nlocal, true, s);
         gimg.reserve((size_t)nall + ns - nlocal, true, s);
+        if (pc) {  // the swap's sendlist (each ghost's source), for LAMMPS' ghost slot order
+          gsrc.reserve((size_t)nall + ns - nlocal, true, s);
+          SPH_HIP_TRY(hipMemcpyAsync(gsrc.p + (nall - nlocal), sel.p, ns * sizeof(int),
+                                     hipMemcpyDeviceToDevice, s));
+        }
         hipLaunchKernelGGL(k_append_ghosts, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sel.p,
                            nlocal, nall, d, pbc, shift, xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p);
         mpx_copy(ns, sel.p, nall, xbuf);
@@ -914,6 +931,33 @@ struct sph_engine {
       }
     }
     nghost = nall - nlocal;
+    gswap_first.push_back(nghost);
+  }
+
+  // LAMMPS' index order of this brick's ghosts (one process): CommBrick::borders appends each
+  // swap's ghosts in the order of the atoms it scans (comm_brick.cpp:741-800), i.e. by the
+  // LAMMPS index of their source -- tag - 1 for an owned atom (local order = tag order on one
+  // process without sorting), nlocal + slot for a ghost of an earlier swap.  Our swaps hold
+  // the same ghosts in our own (Hilbert) order; sort each swap by that key: grank[g] = the
+  // ghost's LAMMPS slot.  Used only when a created atom may overwrite a slot a candidate reads.
+  void pc_ghost_slots() {
+    pc_grank.reserve(nghost > 0 ? nghost : 1);
+    for (size_t w = 0; w + 1 < gswap_first.size(); w++) {
+      const int first = gswap_first[w], ns = gswap_first[w + 1] - first;
+      if (ns == 0) continue;
+      pc_key.reserve(2 * (size_t)ns);
+      pc_val.reserve(2 * (size_t)ns);
+      hipLaunchKernelGGL(k_pc_swapkeys, dim3(blocks(ns)), dim3(BLK), 0, s, ns, first, gsrc.p,
+                         nlocal, tag.p, pc_grank.p, pc_key.p, pc_val.p);
+      size_t tb = 0;
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pc_key.p, pc_key.p + ns,
+                                                     pc_val.p, pc_val.p + ns, ns, 0, 32, s));
+      tmp_reserve(tb);
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, pc_key.p, pc_key.p + ns,
+                                                     pc_val.p, pc_val.p + ns, ns, 0, 32, s));
+      hipLaunchKernelGGL(k_pc_swaprank, dim3(blocks(ns)), dim3(BLK), 0, s, ns, first,
+                         pc_val.p + ns, pc_grank.p);
+    }
   }
 
   void setup_bins_geometry() {
@@ -1114,7 +1158,7 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
       blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                 dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
-                blk_cq(), env_int("SPH_BEXP", 0));
+                blk_cq(), study_int("SPH_BEXP", 0));
       int hm[5];
       SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
@@ -1642,13 +1686,30 @@ struct sph_engine {
     rec.reserve((size_t)8 * ncand);
     gat.reserve((size_t)9 * ncand);
     otag.reserve(ncand);
-    hipLaunchKernelGGL(k_pc_candidates<8>, mp_rows(ncand), dim3(256), 0, s, ncand, cand.p,
-                       (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p, 4,
-                       ty.p, rm.p, pd, rec.p, strided ? list_stride : 0, ccnt.p);
+    // first pass screens: every ghost ranks 0, so minr < NORANK flags the candidates whose
+    // row holds a from_type ghost at all; only then are LAMMPS' ghost slots worked out
+    pc_minr.reserve(ncand);
+    const int lst = strided ? list_stride : 0;
+    PcRank rk{n, 1, nullptr};
+    auto walk = [&](const PcRank &r) {
+      hipLaunchKernelGGL(k_pc_candidates<8>, mp_rows(ncand), dim3(256), 0, s, ncand, cand.p,
+                         (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p,
+                         4, ty.p, rm.p, pd, rec.p, lst, ccnt.p, r, 0, 0, pc_minr.p);
+    };
+    walk(rk);
+    std::vector<int> hm(ncand);
+    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    if (std::any_of(hm.begin(), hm.end(), [](int v) { return v != PC_NORANK; })) {
+      pc_ghost_slots();
+      rk = PcRank{n, 2, pc_grank.p};
+      walk(rk);
+    }
     hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
                        vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
     std::vector<int> hc(ncand), ht(ncand);
     std::vector<double> hr((size_t)8 * ncand), hg((size_t)9 * ncand);
+    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
     SPH_HIP_TRY(hipMemcpyAsync(hc.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
     SPH_HIP_TRY(hipMemcpyAsync(ht.data(), otag.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
     SPH_HIP_TRY(hipMemcpyAsync(hr.data(), rec.p, hr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -1671,10 +1732,21 @@ struct sph_engine {
       c.cv = g[7];
       c.rho = g[8];
       for (int d = 0; d < 8; d++) c.rec[d] = hr[(size_t)8 * k + d];
+      c.minr = hm[k];
     }
+    auto recompute = [&](size_t q, int dead_a, int dead_w, double *out) {
+      pc_one.reserve(1);
+      SPH_HIP_TRY(hipMemcpyAsync(pc_one.p, &hc[ord[q]], sizeof(int), hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL(k_pc_candidates<8>, dim3(1), dim3(256), 0, s, 1, pc_one.p,
+                         (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p,
+                         4, ty.p, rm.p, pd, Wd.p, lst, ccnt.p, rk, dead_a, dead_w, (int *)nullptr);
+      SPH_HIP_TRY(hipMemcpyAsync(out, Wd.p, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipStreamSynchronize(s));
+    };
+    Wd.reserve(8);
     std::vector<int> ins_k;
-    std::vector<double> ins_rec;
-    pc_replay(p, cfg.dim, pc_seed, cands, ins_k, ins_rec);
+    std::vector<double> ins_rec, ins_W;
+    pc_replay(p, cfg.dim, pc_seed, cands, ins_k, ins_W, ins_rec, recompute);
     const int nins = (int)ins_k.size();
     if (nins == 0) return;
     std::vector<int> hidx(nins);
@@ -1683,7 +1755,7 @@ struct sph_engine {
       const int k = ord[ins_k[q]];
       hidx[q] = hc[k];  // the candidate's row = its atom (identity row list)
       hval[q] = ins_rec[(size_t)13 * q + 9];
-      hW[q] = hr[(size_t)8 * k + 1];
+      hW[q] = ins_W[q];
     }
     idx.reserve(nins);
     vals.reserve(nins);
@@ -1700,7 +1772,7 @@ struct sph_engine {
     hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
     hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
                        (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p,
-                       strided ? list_stride : 0, ccnt.p);
+                       lst, ccnt.p, rk);
     reverse1(dmass.p);
     hipLaunchKernelGGL(k_pc_finish, dim3(blocks(n)), dim3(BLK), 0, s, n, dmass.p, rm.p, en.p);
     ensure_atoms((size_t)n + nins, true);  // (over the ghost slots: the rebuild follows)

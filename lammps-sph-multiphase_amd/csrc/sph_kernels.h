@@ -112,6 +112,12 @@ __device__ __forceinline__ int group_sum_i(int v) {
   for (int m = G >> 1; m > 0; m >>= 1) v += __shfl_xor(v, m, G);
   return v;
 }
+template <int G>
+__device__ __forceinline__ int group_min_i(int v) {
+#pragma unroll
+  for (int m = G >> 1; m > 0; m >>= 1) v = min(v, __shfl_xor(v, m, G));
+  return v;
+}
 
 // Tait EOS pressure term P/rho^2 with gamma = 7, in the reference's operation order
 // (pair_sph_taitwater.cpp:117-120).

@@ -40,10 +40,14 @@ MpArgs mp_args(sph_hip_ctx *c) {
   a.en = c->en.p;
   a.cv = c->cv.p;
   a.mc = c->dm;
+#ifdef SPH_STUDY  // study variants (SPH_MPX), study builds only
   static const int mpx = [] {
     const char *v = getenv("SPH_MPX");
     return v ? atoi(v) : 0;
   }();
+#else
+  const int mpx = 0;
+#endif
   a.exp = mpx;
   return a;
 }

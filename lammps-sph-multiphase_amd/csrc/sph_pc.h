@@ -12,15 +12,25 @@
 //    stream exactly in the reference's order;
 //  * device again: the mass taken from the donors (dmass[j] += to_mass w_j / W) for the
 //    candidates that did change phase, scattered with fp64 atomics onto owned and ghost j.
-// Every candidate is evaluated on the atoms as they were when pre_exchange began.  (The
-// reference creates each new atom at index nlocal inside the candidate loop, over the
-// first ghost slot, which later candidates' list walks then read, and create_atom zeroes
-// that slot's drho = dmass entry: with several insertions per call and a donor ghost in
-// that slot the reference's result depends on this aliasing.  Not reproduced; DESIGN.md.)
+//
+// The reference's memory behaviour is reproduced: it creates the k-th new atom of a call at
+// index nlocal + k (AtomVecMesoMultiPhase::create_atom, atom_vec_meso_multiphase.cpp:968-997),
+// i.e. over the ghost in LAMMPS slot k, before that candidate's donor loops.  So a candidate
+// met after K insertions no longer sees the ghosts of slots < K (isfromphasearound) or <= K
+// (its weights): they now hold to_type atoms; and create_atom zeroes that slot's drho (= the
+// fix's dmass, :193), so every donation to a ghost of slot < nins is lost (the reference then
+// does not conserve mass).  Each kernel takes the slot rank of a ghost through PcRank; the
+// candidate pass reports each candidate's smallest from_type ghost rank, and the replay
+// recomputes, on the device, the (rare) candidates whose row meets an overwritten slot.
+// (to_type == from_type would turn those slots into donors at the new atoms' positions: not
+// supported, an error.)  Tests: tests/test_phasechange_golden.py pins the restatement
+// (oracle orc_pre_exchange_ref) to the reference's own FixPhaseChange.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <functional>
+#include <stdexcept>
 #include <vector>
 
 #include "../../include/sph_hip.h"
@@ -31,6 +41,23 @@ namespace sph {
 struct PcDev {
   int dim, from_type, to_type;
   double Tc, to_mass, cutoff;
+};
+
+constexpr int PC_NORANK = 0x7fffffff;
+
+// LAMMPS slot rank of atom j among the ghosts (owned atoms: none)
+struct PcRank {
+  int nlocal;
+  int mode;           // 0: atoms staged in LAMMPS order (rank = j - nlocal)
+                      // 1: screen -- every ghost ranks 0
+                      // 2: table grank[j - nlocal]
+  const int *grank;
+  __device__ __forceinline__ int operator()(int j) const {
+    if (j < nlocal) return PC_NORANK;
+    if (mode == 0) return j - nlocal;
+    if (mode == 1) return 0;
+    return grank[j - nlocal];
+  }
 };
 
 // candidate flags over rows (ilist: row -> atom, nullptr = identity)
@@ -49,8 +76,10 @@ __device__ __forceinline__ double pc_w(int dim, double r) {
   return quintic_w(dim, r);  // sph_kernel_quintic{2,3}d(sqrt(rsq)*cutoff), :247-251 (A.6-3)
 }
 
-// one record per candidate: {around, W, Sv[3], Svest[3]} over the candidate's list row;
-// vel holds v with vstride doubles per atom (3: packed xyz, 4: double4)
+// one record per candidate: {around, W, Sv[3], Svest[3]} over the candidate's list row,
+// without the from_type ghosts of slot rank < dead_a (around) / < dead_w (weights); minr
+// (nullable) gets the smallest slot rank of the row's from_type atoms.  vel holds v with
+// vstride doubles per atom (3: packed xyz, 4: double4)
 template <int G>
 __global__ void __launch_bounds__(256)
 k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__ ilist,
@@ -58,7 +87,8 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
                 const double4 *__restrict__ xf, const double4 *__restrict__ vr,
                 const double *__restrict__ vel, int vstride, const int *__restrict__ ty,
                 const double *__restrict__ rm, PcDev p, double *__restrict__ rec,
-                int lstride = 0, const int *__restrict__ lcnt = nullptr) {
+                int lstride, const int *__restrict__ lcnt, PcRank rk, int dead_a, int dead_w,
+                int *__restrict__ minr) {
   const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (k >= ncand) return;
@@ -66,17 +96,20 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
   const int i = ilist ? ilist[row] : row;
   const double4 xi = xf[i];
   const double cut2 = p.cutoff * p.cutoff;
-  int around = 0;
+  int around = 0, mr = PC_NORANK;
   double W = 0.0, sv0 = 0.0, sv1 = 0.0, sv2 = 0.0, se0 = 0.0, se1 = 0.0, se2 = 0.0;
   const MpRow rw(off, lcnt, lstride, row);
   for (int q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type) continue;
+    const int r = rk(j);
+    mr = min(mr, r);
     const double4 xj = xf[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
-    if (rsq_ref(dx, dy, dz) <= cut2) around = 1;  // (a decision: the reference's rounding)
-    if (rm[j] > 0.5 * p.to_mass) {
+    // (a decision: the reference's rounding)
+    if (r >= dead_a && rsq_ref(dx, dy, dz) <= cut2) around = 1;
+    if (r >= dead_w && rm[j] > 0.5 * p.to_mass) {
       const double w = pc_w(p.dim, sqrt(rsq) * p.cutoff);
       const double4 vj = vr[j];
       const double *const v = vel + (size_t)vstride * j;
@@ -90,6 +123,7 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
     }
   }
   around = group_sum_i<G>(around);
+  mr = group_min_i<G>(mr);
   W = group_sum<G>(W);
   sv0 = group_sum<G>(sv0);
   sv1 = group_sum<G>(sv1);
@@ -107,17 +141,21 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
     o[5] = se0;
     o[6] = se1;
     o[7] = se2;
+    if (minr) minr[k] = mr;
   }
 }
 
-// dmass[j] += to_mass * w_j / W over the donors of every inserted candidate
+// dmass[j] += to_mass * w_j / W over the donors of every inserted candidate; the k-th
+// inserted candidate's donors exclude the ghosts of slot rank <= k (overwritten before its
+// donor loops), and donations to ghosts of slot rank < nins are dropped (create_atom zeroes
+// their drho later in the call)
 template <int G>
 __global__ void __launch_bounds__(256)
 k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wtot,
            const int *__restrict__ ilist, const int *__restrict__ off,
            const int *__restrict__ nbr, const double4 *__restrict__ xf,
            const int *__restrict__ ty, const double *__restrict__ rm, PcDev p,
-           double *__restrict__ dmass, int lstride = 0, const int *__restrict__ lcnt = nullptr) {
+           double *__restrict__ dmass, int lstride, const int *__restrict__ lcnt, PcRank rk) {
   const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (k >= nins) return;
@@ -129,11 +167,34 @@ k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wt
   for (int q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type || !(rm[j] > 0.5 * p.to_mass)) continue;
+    const int r = rk(j);
+    if (r < nins) continue;  // overwritten before this donor loop (r <= k) or later (r < nins)
     const double4 xj = xf[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
     atomicAdd(&dmass[j], p.to_mass * pc_w(p.dim, sqrt(rsq) * p.cutoff) / W);
   }
+}
+
+// one swap of a brick's ghosts: key = LAMMPS index of the atom each ghost was copied from
+// (owned: tag - 1; ghost of an earlier swap: nlocal + its slot), val = position in the swap
+static __global__ void k_pc_swapkeys(int ns, int first, const int *__restrict__ gsrc,
+                                     int nlocal, const int *__restrict__ tag,
+                                     const int *__restrict__ grank, int *__restrict__ key,
+                                     int *__restrict__ val) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ns) return;
+  const int src = gsrc[first + k];
+  key[k] = src < nlocal ? tag[src] - 1 : nlocal + grank[src - nlocal];
+  val[k] = k;
+}
+
+// after the sort by key: the swap's p-th ghost in LAMMPS order sits in slot first + p
+static __global__ void k_pc_swaprank(int ns, int first, const int *__restrict__ val_sorted,
+                                     int *__restrict__ grank) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ns) return;
+  grank[first + val_sorted[p]] = first + p;
 }
 
 // ---- host side: the random stream, in the reference's order ----------------------------
@@ -196,18 +257,35 @@ inline void pc_newpos(int dim, int &seed, const double *x, const double *cg, dou
 struct PcCand {
   double x[3], cg[3], e, cv, rho;
   double rec[8];  // k_pc_candidates: around, W, Sv[3], Svest[3]
+  int minr;       // smallest slot rank of a from_type ghost in its row (PC_NORANK: none)
 };
 
+// recompute(k, dead_a, dead_w, rec): candidate k's record without the ghosts of slot rank
+// < dead_a (around) / < dead_w (weights); device work, called only for rows that meet a
+// slot a created atom has overwritten
+using PcRecompute = std::function<void(size_t, int, int, double *)>;
+
 // The candidate loop of pre_exchange (:198-321).  For each candidate that changes phase:
-// its index in `c` (ins_k), its new energy e_i = (e_i - Hwv)/2, and the new atom's
-// 13-double record {x[3], v[3], vest[3], e, rmass, rho, cv} (ins_rec).
+// its index in `c` (ins_k), its donors' total weight (ins_W), its new energy
+// e_i = (e_i - Hwv)/2, and the new atom's 13-double record {x[3], v[3], vest[3], e, rmass,
+// rho, cv} (ins_rec).
 inline void pc_replay(const sph_phasechange_params &p, int dim, int &seed,
                       const std::vector<PcCand> &c, std::vector<int> &ins_k,
-                      std::vector<double> &ins_rec) {
+                      std::vector<double> &ins_W, std::vector<double> &ins_rec,
+                      const PcRecompute &recompute) {
   ins_k.clear();
+  ins_W.clear();
   ins_rec.clear();
+  int K = 0;  // atoms created so far: they sit in ghost slots 0..K-1
   for (size_t k = 0; k < c.size(); k++) {
-    const PcCand &a = c[k];
+    PcCand a = c[k];
+    if (a.minr <= K) {  // the row meets slot K (this candidate's own new atom) or an earlier one
+      if (p.from_type == p.to_type)
+        throw std::runtime_error(
+            "fix phase_change with to_type == from_type: a created atom would become a donor "
+            "in a later candidate's list (not supported)");
+      recompute(k, K, K + 1, a.rec);
+    }
     const double Ti = a.e / a.cv;
     const bool around = a.rec[0] != 0.0;
     bool change;
@@ -254,7 +332,9 @@ inline void pc_replay(const sph_phasechange_params &p, int dim, int &seed,
     o[11] = a.rho;
     o[12] = a.cv;
     ins_k.push_back((int)k);
+    ins_W.push_back(W);
     ins_rec.insert(ins_rec.end(), o, o + 13);
+    K++;
   }
 }
 

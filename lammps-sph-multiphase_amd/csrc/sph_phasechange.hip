@@ -41,8 +41,8 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
   PcDev pd{c->dim, p->from_type, p->to_type, p->Tc, p->to_mass, p->cutoff};
   const int inum = c->inum;
   // 1. candidates in row order
-  DBuf<int> flag, cand, ncand_d, rows;
-  DBuf<double> vel, rec, Wd, dm;
+  DBuf<int> flag, cand, ncand_d, rows, minr, one;
+  DBuf<double> vel, rec, Wd, dm, rec1;
   flag.reserve(inum);
   cand.reserve(inum);
   ncand_d.reserve(1);
@@ -62,6 +62,9 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     cand.release();
     ncand_d.release();
     rows.release();
+    minr.release();
+    one.release();
+    rec1.release();
     vel.release();
     rec.release();
     Wd.release();
@@ -73,18 +76,23 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     return SPH_HIP_OK;
   }
   // 2. per-candidate list walk (stream independent)
+  // the staged atoms are in LAMMPS order: ghost j sits in slot j - nlocal (sph_pc.h)
+  const PcRank rk{nlocal, 0, nullptr};
   vel.reserve((size_t)3 * nall);
   rec.reserve((size_t)8 * ncand);
+  minr.reserve(ncand);
   SPH_HIP_TRY(hipMemcpyAsync(vel.p, v, (size_t)3 * nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(k_pc_candidates<PCG>,
                      dim3((unsigned)(((long long)ncand * PCG + 255) / 256)), dim3(256), 0,
                      c->stream, ncand, cand.p, c->ilist.p, c->off.p, c->nbr.p, c->xf.p,
-                     c->vr.p, vel.p, 3, c->ty.p, c->rm.p, pd, rec.p, 0, (const int *)nullptr);
+                     c->vr.p, vel.p, 3, c->ty.p, c->rm.p, pd, rec.p, 0, (const int *)nullptr,
+                     rk, 0, 0, minr.p);
   SPH_HIP_TRY(hipGetLastError());
-  std::vector<int> hcand(ncand);
+  std::vector<int> hcand(ncand), hminr(ncand);
   std::vector<double> hrec((size_t)8 * ncand);
   std::vector<double> he(nall), hcv(nall);
   SPH_HIP_TRY(hipMemcpyAsync(hcand.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  SPH_HIP_TRY(hipMemcpyAsync(hminr.data(), minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipMemcpyAsync(hrec.data(), rec.p, hrec.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipMemcpyAsync(he.data(), c->en.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipMemcpyAsync(hcv.data(), c->cv.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -106,11 +114,25 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     a.cv = hcv[i];
     a.rho = hvr[i].w;
     for (int q = 0; q < 8; q++) a.rec[q] = hrec[(size_t)8 * k + q];
+    a.minr = hminr[k];
   }
+  // a candidate whose row meets a slot already overwritten by a created atom: its walk again
+  // on the device without those slots
+  auto recompute = [&](size_t k, int dead_a, int dead_w, double *out) {
+    one.reserve(1);
+    rec1.reserve(8);
+    SPH_HIP_TRY(hipMemcpyAsync(one.p, &hcand[k], sizeof(int), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_pc_candidates<PCG>, dim3(1), dim3(256), 0, c->stream, 1, one.p,
+                       c->ilist.p, c->off.p, c->nbr.p, c->xf.p, c->vr.p, vel.p, 3, c->ty.p,
+                       c->rm.p, pd, rec1.p, 0, (const int *)nullptr, rk, dead_a, dead_w,
+                       (int *)nullptr);
+    SPH_HIP_TRY(hipMemcpyAsync(out, rec1.p, 8 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  };
   int s = *seed;
   std::vector<int> ins_k;
-  std::vector<double> ins_rec;
-  pc_replay(*p, c->dim, s, cands, ins_k, ins_rec);
+  std::vector<double> ins_rec, ins_Wv;
+  pc_replay(*p, c->dim, s, cands, ins_k, ins_Wv, ins_rec, recompute);
   const int nins = (int)ins_k.size();
   std::vector<int> ins_rows(nins);
   std::vector<double> ins_W(nins);
@@ -125,7 +147,7 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     e[i] = o[9];
     he[i] = o[9];
     ins_rows[q] = hcand[k];
-    ins_W[q] = cands[k].rec[1];
+    ins_W[q] = ins_Wv[q];
   }
   *seed = s;
   *nins_out = nins;
@@ -139,7 +161,8 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     SPH_HIP_TRY(hipMemsetAsync(dm.p, 0, nall * sizeof(double), c->stream));
     hipLaunchKernelGGL(k_pc_dmass<PCG>, dim3((unsigned)(((long long)nins * PCG + 255) / 256)),
                        dim3(256), 0, c->stream, nins, rows.p, Wd.p, c->ilist.p, c->off.p,
-                       c->nbr.p, c->xf.p, c->ty.p, c->rm.p, pd, dm.p, 0, (const int *)nullptr);
+                       c->nbr.p, c->xf.p, c->ty.p, c->rm.p, pd, dm.p, 0, (const int *)nullptr,
+                       rk);
     SPH_HIP_TRY(hipGetLastError());
     SPH_HIP_TRY(hipMemcpyAsync(dmass, dm.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     SPH_HIP_TRY(hipStreamSynchronize(c->stream));

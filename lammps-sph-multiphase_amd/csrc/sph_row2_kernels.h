@@ -512,8 +512,10 @@ inline void row2_force_n(int visc, int mode, hipStream_t s, const Row2Args &b) {
   switch (mode) {
     case M_TAIT:
       if (mor) row2_force_t<G, U, 1, M_TAIT, NT1, LP, IV, 0>(s, b);
+#ifdef SPH_STUDY  // (outputs meaningless: study builds only, make STUDY=1)
       else if (NT1 && b.exp == 1) row2_force_t<G, U, 0, M_TAIT, NT1, LP, IV, 1>(s, b);
       else if (NT1 && b.exp == 2) row2_force_t<G, U, 0, M_TAIT, NT1, LP, IV, 2>(s, b);
+#endif
       else row2_force_t<G, U, 0, M_TAIT, NT1, LP, IV, 0>(s, b);
       break;
     case M_TAIT | M_HEAT:
@@ -542,8 +544,13 @@ inline void row2_force_gu(bool nt1, int visc, int mode, hipStream_t s, const Row
   }
 }
 
-// (G lanes per row, U pairs per lane) shapes; SPH_ROW2TILE picks one (tuning)
+// (G lanes per row, U pairs per lane) shapes; SPH_ROW2TILE picks one in study builds
+// (tuning); the production build has the measured fastest, 8 x 4
+#ifdef SPH_STUDY
 #define SPH_ROW2_TILES(X) X(0, 16, 2) X(1, 8, 2) X(2, 16, 4) X(3, 8, 4) X(4, 4, 4)
+#else
+#define SPH_ROW2_TILES(X) X(3, 8, 4)
+#endif
 
 int row2_tile();
 

@@ -86,7 +86,7 @@ def oracle_forces(sysm, ph: po.Physics, P, newton=1, reverse=True):
     return f, drho, de
 
 
-def bubble_system(nx=10, dim=3, rv=None):
+def bubble_system(nx=10, dim=3, rv=None, slab=False):
     """C5 geometry (examples/USER/sph/bubble_growth/bubble.lmp, vars.lmp, in.phases): unit box,
     lattice sc (sq) dx = 1/nx with origin 0.5, liquid (type 1) everywhere, vapour (type 2)
     inside a sphere at the centre (radius rv, default 1.01 dx: the 8 (4) central sites);
@@ -98,11 +98,16 @@ def bubble_system(nx=10, dim=3, rv=None):
                  -1).reshape(-1, 3)
     g = g[np.lexsort((g[:, 0], g[:, 1], g[:, 2]))]      # create_atoms: x fastest
     x = (g + 0.5) * dx
+    if slab:   # jittered (a perfect lattice makes the colour gradient's transverse components
+        # cancel exactly or not depending on summation order, and create_newpos' b2 = 0/0)
+        x += np.random.default_rng(1234).uniform(-0.1, 0.1, size=x.shape) * dx
     if dim == 2:
         x[:, 2] = 0.0
     c = np.array([0.5, 0.5, 0.5 if dim == 3 else 0.0])
     rv = 1.01 * dx if rv is None else rv
     vap = ((x - c) ** 2).sum(1) < rv * rv
+    if slab:   # vapour in the last x layer: its rows meet LAMMPS' first ghost slots (the
+        vap = x[:, 0] > 1.0 - dx   # x-low layer imaged past x = 1), see sph_pc.h
     t = np.where(vap, 2, 1).astype(np.int32)
     rho = np.where(vap, 0.1, 1.0)
     cv = np.where(vap, 0.06, 0.04)

@@ -146,24 +146,15 @@ def test_phase_change_mass_conservation(po):
     assert (rm > 0).all()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("energy", [0, 1])
-def test_gpu_phase_change_vs_oracle(gpu, sph_amd, energy):
-    d, p = two_phase_box()
-    g = d["g"]
-    if energy:
-        p.energy_chance = 1
-        p.rate = 4.0
-        p.dt = 0.5
-    e_o = d["e"].copy()
-    so, no, ro, po_par, dmo = po.phasechange(p, 4242, g.nlocal, g.x, d["v"], d["vest"], d["cg"],
-                                             e_o, d["rmass"], d["rho"], d["cv"], g.type,
-                                             d["foff"], d["fnb"])
-    assert no > 0
-    ctx = sph_amd.PairContext(3, 2, 1)
-    ctx.atoms(g.nlocal, g.nghost, g.x, g.type, vest=d["vest"], rho=d["rho"], e=d["e"])
-    ctx.atoms_multiphase(d["rmass"], d["cv"])
-    ctx.list_csr(sph_amd.SPH_LIST_FULL, d["foff"], d["fnb"])
+def _pair_layer_call(sph_amd, p, seed, g, arrays, off, nb):
+    """sph_hip_phasechange (the pair-style layer, atoms staged in LAMMPS order) followed by
+    what fix phase_change/hip does around it: create the atoms, reverse comm of dmass along
+    CommBrick's swaps, sph_hip_phasechange_finish."""
+    ctx = sph_amd.PairContext(int(p.dim), 2, 1)
+    ctx.atoms(g.nlocal, g.nghost, arrays["x"], arrays["type"], vest=arrays["vest"],
+              rho=arrays["rho"], e=arrays["e"])
+    ctx.atoms_multiphase(arrays["rmass"], arrays["cv"])
+    ctx.list_csr(sph_amd.SPH_LIST_FULL, off, nb)
     hp = sph_amd.PhaseChangeParams()
     for name, _ in sph_amd.PhaseChangeParams._fields_:
         val = getattr(p, name)
@@ -172,11 +163,61 @@ def test_gpu_phase_change_vs_oracle(gpu, sph_amd, energy):
                 getattr(hp, name)[k] = val[k]
         else:
             setattr(hp, name, val)
-    e_g = d["e"].copy()
-    sg, ng, rg, pg, dmg = ctx.phasechange(hp, 4242, d["v"], d["cg"], e_g)
-    assert (sg, ng) == (so, no)                       # same stream consumption
-    assert np.array_equal(pg, po_par)                 # same atoms changed phase, same order
-    assert np.array_equal(rg[:, :3], ro[:, :3])       # host-side positions: bit-identical
-    assert rel_err(rg, ro) < 1e-10
-    assert rel_err(dmg, dmo) < 1e-10
-    assert rel_err(e_g, e_o) < 1e-12
+    e = arrays["e"].copy()
+    sd, nins, rec, par, dm = ctx.phasechange(hp, seed, arrays["v"], arrays["cg"], e)
+    po.lib().orc_reverse_swaps(g.nlocal, len(g.swap_first) - 1, g.swap_first,
+                               g.src if g.src.size else np.zeros(1, np.int32), dm)
+    rm = arrays["rmass"][:g.nlocal].copy()
+    sph_amd.phasechange_finish(g.nlocal, dm, rm, e)
+    return sd, nins, rec, par, rm, e[:g.nlocal]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("energy", [0, 1])
+def test_gpu_phase_change_vs_oracle(gpu, sph_amd, energy):
+    """Against the restatement with the reference's memory behaviour (created atoms over the
+    ghost slots later candidates read; orc_pre_exchange_ref, pinned to the reference by
+    test_phasechange_golden.py): the same stream, insertions and donors' mass."""
+    d, p = two_phase_box()
+    g = d["g"]
+    if energy:
+        p.energy_chance = 1
+        p.rate = 4.0
+        p.dt = 0.5
+    arrays = dict(x=g.x, v=d["v"], vest=d["vest"], cg=d["cg"], e=d["e"], rmass=d["rmass"],
+                  rho=d["rho"], cv=d["cv"], type=g.type)
+    so, no, out = po.pre_exchange_ref(p, 4242, g, arrays, d["foff"], d["fnb"])
+    assert no > g.nlocal
+    sg, ng, rg, pg, rm, e = _pair_layer_call(sph_amd, p, 4242, g, arrays, d["foff"], d["fnb"])
+    n = g.nlocal
+    assert (sg, ng) == (so, no - n)                   # same stream consumption
+    assert np.array_equal(rg[:, :3], out["x"][n:])    # host-side positions: bit-identical
+    for c, k in ((3, "v"), (6, "vest")):
+        assert rel_err(rg[:, c:c + 3], out[k][n:]) < 1e-10, k
+    assert rel_err(rg[:, 9], out["e"][n:]) < 1e-12
+    assert rel_err(rm, out["rmass"][:n]) < 1e-12
+    assert rel_err(e, out["e"][:n]) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["kat", "slab", "bubble", "slab2d"])
+def test_gpu_phase_change_vs_reference_fixture(gpu, sph_amd, name):
+    """The pair-style layer on the inputs of the reference's own FixPhaseChange calls
+    (tests/golden/pc_*.npz, first call): the same insertions at bit-identical positions,
+    the new atoms' fields and the donors' rmass and energies as the reference left them --
+    including the slab case, where created atoms overwrite ghost donors (sph_pc.h)."""
+    import os
+    from test_phasechange_golden import call_inputs, load
+    d = load(name)
+    p = po.pc_params_from_args(d["args"], int(d["dim"]), d["boxlo"], d["boxhi"], float(d["dt"]))
+    g, arrays, off, nb = call_inputs(d, 0)
+    sg, ng, rg, pg, rm, e = _pair_layer_call(sph_amd, p, int(d["args"][12]), g, arrays, off, nb)
+    n = g.nlocal
+    assert ng == int(d["c0_out_nlocal"]) - n
+    assert np.array_equal(rg[:, :3], d["c0_out_x"][n:])
+    for c, k in ((3, "v"), (6, "vest")):
+        assert rel_err(rg[:, c:c + 3], d["c0_out_" + k][n:]) < 1e-10, k
+    assert rel_err(rg[:, 9], d["c0_out_e"][n:]) < 1e-12
+    assert np.array_equal(rg[:, 10], d["c0_out_rmass"][n:])
+    assert rel_err(rm, d["c0_out_rmass"][:n]) < 1e-12
+    assert rel_err(e, d["c0_out_e"][:n]) < 1e-12

@@ -84,6 +84,13 @@ FixPhaseChangeHIP::FixPhaseChangeHIP(LAMMPS *lmp, int narg, char **arg)
     error->all(FLERR, "Fix phase_change region does not support a bounding box");
   if (domain->regions[iregion]->dynamic_check())
     error->all(FLERR, "Fix phase_change region cannot be dynamic");
+  // the region's extent must lie inside the box (:97-114)
+  Region *r = domain->regions[iregion];
+  const double *lo = domain->triclinic ? domain->boxlo_bound : domain->boxlo;
+  const double *hi = domain->triclinic ? domain->boxhi_bound : domain->boxhi;
+  if (r->extent_xlo < lo[0] || r->extent_xhi > hi[0] || r->extent_ylo < lo[1] ||
+      r->extent_yhi > hi[1] || r->extent_zlo < lo[2] || r->extent_zhi > hi[2])
+    error->all(FLERR, "Phase change region extends outside simulation box");
   rng = seed;  // RanPark(lmp, seed)
   force_reneighbor = 1;
   next_reneighbor = update->ntimestep + 1;
@@ -99,6 +106,7 @@ int FixPhaseChangeHIP::setmask() { return PRE_EXCHANGE; }
 void FixPhaseChangeHIP::init() {
   iregion = domain->find_region(idregion);
   if (iregion == -1) error->all(FLERR, "Region ID for fix phase_change does not exist");
+  sph_hip_new_run();
   // full list, rebuilt whenever re-neighboring occurs (fix_phase_change.cpp:151-156)
   int irequest = neighbor->request((void *)this);
   neighbor->requests[irequest]->pair = 0;

@@ -26,15 +26,23 @@ using namespace LAMMPS_NS;
 namespace {
 sph_hip_ctx *g_ctx = NULL;
 // what the context's atoms were staged at: a later compute of the same step (hybrid/overlay
-// sub-styles after forward_comm_pair) restages rho only.  Borders run only with a list
-// build, so (ntimestep, neighbor->ncalls, nlocal, nghost) pins the atom set and positions.
+// sub-styles after forward_comm_pair) restages rho only.  Within one run borders happen only
+// with a list build, so (ntimestep, neighbor->ncalls, nlocal, nghost) pins the atom set and
+// positions; across runs it does not (Verlet::setup and setup_minimal reset ncalls to 0,
+// verlet.cpp:113, :172, and FixMeso::setup_pre_force rewrites vest), so the key also holds
+// the run epoch that every init (Pair::init -> init_style, Fix::init) advances.
 struct StageKey {
-  bigint step, ncalls;
+  bigint epoch, step, ncalls;
   int nlocal, nghost;
   bool mp;
 };
-StageKey g_key = {-1, -1, -1, -1, false};
+bigint g_epoch = 0;
+StageKey g_key = {-1, -1, -1, -1, -1, false};
+// the device list of a kind is reused while this key is unchanged
+int64_t list_key(LAMMPS *lmp) { return (int64_t)(g_epoch << 40) + (int64_t)lmp->neighbor->ncalls; }
 }
+
+void LAMMPS_NS::sph_hip_new_run() { g_epoch++; }
 
 sph_hip_ctx *LAMMPS_NS::sph_hip_rank_ctx(LAMMPS *lmp) {
   if (!g_ctx) {
@@ -60,10 +68,11 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
   Atom *atom = lmp->atom;
   const int nlocal = atom->nlocal, nghost = atom->nghost;
   const int nall = nlocal + nghost;
-  const StageKey key = {lmp->update->ntimestep, lmp->neighbor->ncalls, nlocal, nghost,
+  const StageKey key = {g_epoch, lmp->update->ntimestep, lmp->neighbor->ncalls, nlocal, nghost,
                         multiphase};
-  if (key.step == g_key.step && key.ncalls == g_key.ncalls && key.nlocal == g_key.nlocal &&
-      key.nghost == g_key.nghost && (g_key.mp || !multiphase) && nall && atom->rho) {
+  if (key.epoch == g_key.epoch && key.step == g_key.step && key.ncalls == g_key.ncalls &&
+      key.nlocal == g_key.nlocal && key.nghost == g_key.nghost && (g_key.mp || !multiphase) &&
+      nall && atom->rho) {
     sph_hip_check(lmp, sph_hip_atoms_rho(ctx, atom->rho), "sph_hip_atoms_rho");
   } else {
     // x and vest are memory->create 2-D arrays: contiguous nmax*3 backing (memory.h:124-137)
@@ -77,12 +86,13 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
                     "sph_hip_atoms_multiphase");
     g_key = key;
   }
-  // the list build is the key (neighbor->ncalls, neighbor.cpp:1423): between rebuilds the
-  // staged device copy of this kind is reused -- no host copy, no upload, and a half list
-  // keeps its reverse list; sub-styles of hybrid/overlay on the other kind keep theirs
+  // the list build is the key (run epoch + neighbor->ncalls, neighbor.cpp:1423): between
+  // rebuilds the staged device copy of this kind is reused -- no host copy, no upload, and a
+  // half list keeps its reverse list; sub-styles of hybrid/overlay on the other kind keep
+  // theirs
   sph_hip_check(lmp,
-                sph_hip_list_keyed(ctx, kind, (int64_t)lmp->neighbor->ncalls, list->inum,
-                                   list->ilist, list->numneigh, list->firstneigh),
+                sph_hip_list_keyed(ctx, kind, list_key(lmp), list->inum, list->ilist,
+                                   list->numneigh, list->firstneigh),
                 "sph_hip_list_keyed");
 }
 
@@ -216,4 +226,56 @@ void PairSPHColorGradientHIP::compute(int eflag, int vflag) {
                     "sph_hip_colorgradient");
   }
   comm->forward_comm_pair(this);
+}
+
+/* pair_sph_surfacetension.cpp:50-192 (no virial tally there either) */
+void PairSPHSurfaceTensionHIP::compute(int eflag, int vflag) {
+  if (eflag || vflag) ev_setup(eflag, vflag);
+  else evflag = vflag_fdotr = 0;
+  sph_hip_ctx *ctx = sph_hip_rank_ctx(lmp);
+  sph_hip_check(lmp, sph_hip_surfacetension_coeff(ctx, tab(cut)), "sph_hip_surfacetension_coeff");
+  sph_hip_stage(lmp, ctx, list, SPH_LIST_HALF, true);
+  if (atom->nlocal + atom->nghost)
+    sph_hip_check(lmp,
+                  sph_hip_surfacetension(ctx, &atom->colorgradient[0][0], &atom->f[0][0]),
+                  "sph_hip_surfacetension");
+}
+
+/* Pair::init -> init_style (pair.cpp:211): the reference style's own request, then a new run
+   epoch for the device mirrors */
+void PairSPHRhoSumHIP::init_style() {
+  PairSPHRhoSum::init_style();
+  sph_hip_new_run();
+}
+void PairSPHTaitwaterHIP::init_style() {
+  PairSPHTaitwater::init_style();
+  sph_hip_new_run();
+}
+void PairSPHTaitwaterMorrisHIP::init_style() {
+  PairSPHTaitwaterMorris::init_style();
+  sph_hip_new_run();
+}
+void PairSPHHeatConductionHIP::init_style() {
+  PairSPHHeatConduction::init_style();
+  sph_hip_new_run();
+}
+void PairSPHRhoSumMultiphaseHIP::init_style() {
+  PairSPHRhoSumMultiphase::init_style();
+  sph_hip_new_run();
+}
+void PairSPHTaitwaterMultiphaseHIP::init_style() {
+  PairSPHTaitwaterMultiphase::init_style();
+  sph_hip_new_run();
+}
+void PairSPHHeatConductionPhaseChangeHIP::init_style() {
+  PairSPHHeatConductionPhaseChange::init_style();
+  sph_hip_new_run();
+}
+void PairSPHColorGradientHIP::init_style() {
+  PairSPHColorGradient::init_style();
+  sph_hip_new_run();
+}
+void PairSPHSurfaceTensionHIP::init_style() {
+  PairSPHSurfaceTension::init_style();
+  sph_hip_new_run();
 }

@@ -15,6 +15,7 @@ PairStyle(sph/rhosum/multiphase/hip,PairSPHRhoSumMultiphaseHIP)
 PairStyle(sph/taitwater/multiphase/hip,PairSPHTaitwaterMultiphaseHIP)
 PairStyle(sph/heatconduction/phasechange/hip,PairSPHHeatConductionPhaseChangeHIP)
 PairStyle(sph/colorgradient/hip,PairSPHColorGradientHIP)
+PairStyle(sph/surfacetension/hip,PairSPHSurfaceTensionHIP)
 
 #else
 
@@ -26,6 +27,7 @@ PairStyle(sph/colorgradient/hip,PairSPHColorGradientHIP)
 #include "pair_sph_heatconduction_phasechange.h"
 #include "pair_sph_rhosum.h"
 #include "pair_sph_rhosum_multiphase.h"
+#include "pair_sph_surfacetension.h"
 #include "pair_sph_taitwater.h"
 #include "pair_sph_taitwater_morris.h"
 #include "pair_sph_taitwater_multiphase.h"
@@ -41,41 +43,51 @@ void sph_hip_stage(class LAMMPS *lmp, sph_hip_ctx *ctx, class NeighList *list, i
                    bool multiphase);
 // turn an ABI status into error->one (src/GPU/pair_lj_cut_gpu.cpp:114-115 precedent)
 void sph_hip_check(class LAMMPS *lmp, int rc, const char *where);
+// a new run/minimize/rerun is being set up (Pair::init -> init_style, Fix::init): atoms and
+// lists staged before it are never reused after it, even at the same timestep and list
+// build count (Verlet::setup resets neighbor->ncalls, verlet.cpp:113)
+void sph_hip_new_run();
 
 class PairSPHRhoSumHIP : public PairSPHRhoSum {
  public:
   PairSPHRhoSumHIP(class LAMMPS *lmp) : PairSPHRhoSum(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHTaitwaterHIP : public PairSPHTaitwater {
  public:
   PairSPHTaitwaterHIP(class LAMMPS *lmp) : PairSPHTaitwater(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHTaitwaterMorrisHIP : public PairSPHTaitwaterMorris {
  public:
   PairSPHTaitwaterMorrisHIP(class LAMMPS *lmp) : PairSPHTaitwaterMorris(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHHeatConductionHIP : public PairSPHHeatConduction {
  public:
   PairSPHHeatConductionHIP(class LAMMPS *lmp) : PairSPHHeatConduction(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHRhoSumMultiphaseHIP : public PairSPHRhoSumMultiphase {
  public:
   PairSPHRhoSumMultiphaseHIP(class LAMMPS *lmp) : PairSPHRhoSumMultiphase(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHTaitwaterMultiphaseHIP : public PairSPHTaitwaterMultiphase {
  public:
   PairSPHTaitwaterMultiphaseHIP(class LAMMPS *lmp) : PairSPHTaitwaterMultiphase(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHHeatConductionPhaseChangeHIP : public PairSPHHeatConductionPhaseChange {
@@ -83,12 +95,21 @@ class PairSPHHeatConductionPhaseChangeHIP : public PairSPHHeatConductionPhaseCha
   PairSPHHeatConductionPhaseChangeHIP(class LAMMPS *lmp)
       : PairSPHHeatConductionPhaseChange(lmp) {}
   void compute(int, int);
+  void init_style();
 };
 
 class PairSPHColorGradientHIP : public PairSPHColorGradient {
  public:
   PairSPHColorGradientHIP(class LAMMPS *lmp) : PairSPHColorGradient(lmp) {}
   void compute(int, int);
+  void init_style();
+};
+
+class PairSPHSurfaceTensionHIP : public PairSPHSurfaceTension {
+ public:
+  PairSPHSurfaceTensionHIP(class LAMMPS *lmp) : PairSPHSurfaceTension(lmp) {}
+  void compute(int, int);
+  void init_style();
 };
 
 }  // namespace LAMMPS_NS

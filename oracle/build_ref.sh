@@ -63,3 +63,33 @@ for o in "${allo[@]}"; do
 done
 g++ -shared -o "$OUT/libsph_ref.so" "${wobjs[@]}" "$OBJ/mpi_stubs.o"
 echo "built $OUT/libsph_ref.so"
+
+# libsph_shim.so: the same reference objects with the drop-in style classes of this repo
+# (lammps-sph-multiphase_amd/lammps/*.cpp: sph/<style>/hip, fix phase_change/hip) linked
+# in, as LAMMPS would link them, and the harness built with -DSPH_SHIM (entry points
+# shim_*): the classes run their compute()/pre_exchange() through libsph_hip.so on the
+# harness-filled universe.  Needs the product library built first (make -C the package).
+PKG=$HERE/../lammps-sph-multiphase_amd
+if [ -f "$PKG/libsph_hip.so" ]; then
+  SHIMF="-I$PKG/lammps -I$HERE/../include"
+  sobjs=()
+  for f in pair_sph_hip fix_phase_change_hip; do
+    o=$OBJ/shim_$f.o; sobjs+=("$o")
+    if [ ! -f "$o" ] || [ "$PKG/lammps/$f.cpp" -nt "$o" ] || [ "$PKG/lammps/$f.h" -nt "$o" ] ||
+       [ "$HERE/../include/sph_hip.h" -nt "$o" ]; then
+      g++ $CXXFLAGS $SHIMF -c "$PKG/lammps/$f.cpp" -o "$o"
+    fi
+  done
+  g++ $CXXFLAGS $SHIMF -DSPH_SHIM -c "$HERE/ref_harness.cpp" -o "$OBJ/shim_harness.o"
+  sall=("${objs[@]}" "${sobjs[@]}" "$OBJ/shim_harness.o")
+  nm -u "${sall[@]}" 2>/dev/null | awk 'NF==2 && $1=="U"{print $2}' | sort -u > "$OBJ/sundef.txt"
+  nm --defined-only "${sall[@]}" 2>/dev/null | awk 'NF==3{print $3}' | sort -u > "$OBJ/sdef.txt"
+  comm -23 "$OBJ/sundef.txt" "$OBJ/sdef.txt" | grep '9LAMMPS_NS' > "$OBJ/sweaken.txt" || true
+  SW=$OBJ/sweak; mkdir -p "$SW"; swobjs=()
+  for o in "${sall[@]}"; do
+    w=$SW/$(basename "$o"); objcopy --weaken-symbols="$OBJ/sweaken.txt" "$o" "$w"; swobjs+=("$w")
+  done
+  g++ -shared -o "$OUT/libsph_shim.so" "${swobjs[@]}" "$OBJ/mpi_stubs.o" -L"$PKG" -lsph_hip \
+      -Wl,-rpath,'$ORIGIN/../../lammps-sph-multiphase_amd'
+  echo "built $OUT/libsph_shim.so"
+fi

@@ -201,49 +201,85 @@ def ref_available() -> bool:
     return os.path.exists(REF_SO)
 
 
+def _bind_harness(path, pre):
+    """ctypes signatures of oracle/ref_harness.cpp's entry points (prefix ref_ or shim_)"""
+    R = C.CDLL(path)
+    g = lambda n: getattr(R, pre + n)  # noqa: E731
+    g("neigh_full").argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _dp, _dp, _d, _dp, _lp,
+                                C.c_void_p, _l]
+    g("neigh_full").restype = _l
+    g("neigh_half_from_full").argtypes = [_i, _i, _dp, _lp, _ip, _lp, C.c_void_p]
+    g("neigh_half_from_full").restype = _l
+    g("fix_meso").argtypes = [_i, _i, _i, _i, _d, _ip, _i, _dp, _dp, _dp, _dp, _dp, _dp, _dp,
+                              _dp, _dp]
+    g("rhosum").argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
+    g("taitwater").argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _dp, _dp,
+                               _lp, _ip, _dp, _dp, _dp]
+    g("taitwater_morris").argtypes = g("taitwater").argtypes
+    g("heatconduction").argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _lp,
+                                    _ip, _dp]
+    g("rhosum_multiphase").argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
+    g("taitwater_multiphase").argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
+                                          _dp, _dp, _dp, _dp, _dp, _lp, _ip, _dp]
+    g("heatconduction_phasechange").argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _dp, _dp,
+                                                _ip, _dp, C.c_void_p, C.c_void_p, _dp, _lp,
+                                                _ip, _dp]
+    g("colorgradient").argtypes = [_i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
+    g("surfacetension").argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _lp, _ip,
+                                    _dp]
+    g("pc_new").argtypes = [_i, _i, _dp, _dp, _l, _d, _i, C.POINTER(C.c_char_p)]
+    g("pc_new").restype = C.c_void_p
+    g("pc_pre_exchange").argtypes = [C.c_void_p, _l, _i, _i, _i, _dp, _dp, _dp, _dp, _dp, _dp,
+                                     _dp, _dp, _ip, _lp, _ip, _i, _ip, _ip, C.POINTER(_l)]
+    g("pc_pre_exchange").restype = _i
+    g("pack_restart").argtypes = [_i, _i, _dp, _ip, _ip, _ip, _ip, _dp, _dp, _dp, _dp, _dp, _dp,
+                                  _dp, _i, _dp]
+    g("pack_restart").restype = _i
+    for n in ("kernel_quintic2d", "kernel_quintic3d", "dw_quintic2d", "dw_quintic3d"):
+        g(n).argtypes = [_d]
+        g(n).restype = _d
+    # the ref_* names on either library, so callers can swap one for the other
+    class _Named:
+        pass
+    out = _Named()
+    out.lib = R
+    for n in ("neigh_full", "neigh_half_from_full", "fix_meso", "rhosum", "taitwater",
+              "taitwater_morris", "heatconduction", "rhosum_multiphase", "taitwater_multiphase",
+              "heatconduction_phasechange", "colorgradient", "surfacetension", "pc_new",
+              "pc_pre_exchange", "pack_restart", "kernel_quintic2d", "kernel_quintic3d",
+              "dw_quintic2d", "dw_quintic3d"):
+        setattr(out, "ref_" + n, g(n))
+    return out
+
+
 def ref():
-    """The reference's own compute code (oracle/_ref), or None if it was not built."""
+    """The reference's own compute code (oracle/_ref/libsph_ref.so), or None if it was not
+    built."""
     global _ref
     if _ref is None and ref_available():
-        R = C.CDLL(REF_SO)
-        R.ref_neigh_full.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _dp, _dp, _d, _dp,
-                                     _lp, C.c_void_p, _l]
-        R.ref_neigh_full.restype = _l
-        R.ref_neigh_half_from_full.argtypes = [_i, _i, _dp, _lp, _ip, _lp, C.c_void_p]
-        R.ref_neigh_half_from_full.restype = _l
-        R.ref_fix_meso.argtypes = [_i, _i, _i, _i, _d, _ip, _i, _dp, _dp, _dp, _dp, _dp, _dp,
-                                   _dp, _dp, _dp]
-        R.ref_rhosum.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
-        R.ref_taitwater.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _dp,
-                                    _dp, _dp, _lp, _ip, _dp, _dp, _dp]
-        R.ref_taitwater_morris.argtypes = R.ref_taitwater.argtypes
-        R.ref_heatconduction.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
-                                         _dp, _lp, _ip, _dp]
-        R.ref_rhosum_multiphase.argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _lp, _ip, _dp]
-        R.ref_taitwater_multiphase.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp,
-                                               _dp, _dp, _dp, _dp, _dp, _dp, _lp, _ip, _dp]
-        R.ref_heatconduction_phasechange.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _dp,
-                                                     _dp, _ip, _dp, C.c_void_p, C.c_void_p,
-                                                     _dp, _lp, _ip, _dp]
-        R.ref_colorgradient.argtypes = [_i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp, _lp,
-                                        _ip, _dp]
-        R.ref_surfacetension.argtypes = [_i, _i, _i, _i, _i, _dp, _dp, _dp, _ip, _dp, _dp,
-                                         _lp, _ip, _dp]
-        R.ref_pc_new.argtypes = [_i, _i, _dp, _dp, _l, _d, _i, C.POINTER(C.c_char_p)]
-        R.ref_pc_new.restype = C.c_void_p
-        R.ref_pc_pre_exchange.argtypes = [C.c_void_p, _l, _i, _i, _i, _dp, _dp, _dp, _dp,
-                                          _dp, _dp, _dp, _dp, _ip, _lp, _ip, _i, _ip, _ip,
-                                          C.POINTER(_l)]
-        R.ref_pc_pre_exchange.restype = _i
-        R.ref_pack_restart.argtypes = [_i, _i, _dp, _ip, _ip, _ip, _ip, _dp, _dp, _dp, _dp,
-                                       _dp, _dp, _dp, _i, _dp]
-        R.ref_pack_restart.restype = _i
-        for n in ("ref_kernel_quintic2d", "ref_kernel_quintic3d", "ref_dw_quintic2d",
-                  "ref_dw_quintic3d"):
-            getattr(R, n).argtypes = [_d]
-            getattr(R, n).restype = _d
-        _ref = R
+        _ref = _bind_harness(REF_SO, "ref_")
     return _ref
+
+
+SHIM_SO = os.path.join(HERE, "_ref", "libsph_shim.so")
+_shim = None
+
+
+def shim_available() -> bool:
+    return os.path.exists(SHIM_SO)
+
+
+def shim():
+    """The same harness driving this repo's drop-in LAMMPS classes (sph/<style>/hip, fix
+    phase_change/hip -> libsph_hip.so): oracle/_ref/libsph_shim.so, entry points under their
+    ref_* names.  None if it was not built."""
+    global _shim
+    if _shim is None and shim_available():
+        _shim = _bind_harness(SHIM_SO, "shim_")
+        f = _shim.lib.shim_style_lookup
+        f.argtypes = [_i, C.c_char_p, C.c_char_p, C.c_char_p, _i]
+        f.restype = _i
+    return _shim
 
 
 # ---------------------------------------------------------------------------------------

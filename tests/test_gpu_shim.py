@@ -1,0 +1,146 @@
+"""The drop-in LAMMPS classes on the GPU: sph/<style>/hip and fix phase_change/hip
+(lammps-sph-multiphase_amd/lammps/) linked with the reference's own Pair/Neighbor/CommBrick/
+Fix objects (oracle/_ref/libsph_shim.so, see test_lammps_shim.py), driven through their
+compute() / pre_exchange() on the inputs of the golden fixtures -- whose outputs are the
+reference styles' own (tests/golden/make_golden.py, make_phase_change.py).  So the whole
+LAMMPS-facing path is checked: Pair::init -> init_style, the staging of atom->x/vest/rho/e/
+type (rmass, cv, colorgradient) and of the NeighList, the C-ABI calls, results added into
+atom->f/drho/de, forward/reverse comm hooks, and fix phase_change/hip's atom creation and
+reverse_comm_fix.  Tolerance 1e-10 relative (north_star); new atoms' positions bit-exact."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+from conftest import rel_err
+from test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def S(gpu, sph_amd):
+    if not po.shim_available():
+        pytest.skip("oracle/_ref/libsph_shim.so not built")
+    return po.shim()
+
+
+def nz(a):
+    return a if a.size else np.zeros(1, dtype=a.dtype)
+
+
+@pytest.mark.parametrize("name", ["c2_n6", "c2_n7_h2.2", "c3_n6", "c2_2d_n14"])
+def test_single_phase_styles(S, name):
+    d = load(name)
+    dim, nt, n, ng = int(d["dim"]), int(d["ntypes"]), int(d["nlocal"]), int(d["nghost"])
+    x, ty = d["x"], d["type"]
+    if "out_rho" in d:
+        rho = d["rho"].copy()
+        S.ref_rhosum(dim, nt, n, ng, x, ty, d["mass"], d["rhosum_cut"], d["full_off"],
+                     nz(d["full_nbr"]), rho)
+        assert rel_err(rho[:n], d["out_rho"]) < 1e-13
+    if "out_f" in d:
+        f, drho, de = np.zeros((n + ng, 3)), np.zeros(n + ng), np.zeros(n + ng)
+        fn = S.ref_taitwater_morris if int(d["morris"]) else S.ref_taitwater
+        fn(dim, nt, n, ng, 1, x, d["vest"], d["rho"], ty, d["mass"], d["rho0"], d["c0"],
+           d["visc"], d["tait_cut"], d["half_off"], nz(d["half_nbr"]), f, drho, de)
+        for a, b in ((f, d["out_f"]), (drho, d["out_drho"]), (de, d["out_de_tait"])):
+            assert rel_err(a, b) < TOL
+    if "out_de_heat" in d:
+        de = np.zeros(n + ng)
+        S.ref_heatconduction(dim, nt, n, ng, 1, x, d["e"], d["rho"], ty, d["mass"], d["alpha"],
+                             d["heat_cut"], d["half_off"], nz(d["half_nbr"]), de)
+        assert rel_err(de, d["out_de_heat"]) < TOL
+
+
+def test_multiphase_styles(S):
+    d = load("multiphase_n5")
+    n, ng = int(d["nlocal"]), int(d["nghost"])
+    nall = n + ng
+    x, ty, rm, cut = d["x"], d["type"], d["rmass"], d["cut"]
+    rho = d["rho"].copy()
+    S.ref_rhosum_multiphase(3, 2, n, ng, x, ty, rm, cut, d["full_off"], d["full_nbr"], rho)
+    assert rel_err(rho[:n], d["out_rho"]) < 1e-13
+    f = np.zeros((nall, 3))
+    S.ref_taitwater_multiphase(3, 2, n, ng, 1, x, d["vest"], d["rho"], ty, rm, d["rho0"],
+                               d["c0"], d["gamma"], d["rbg"], d["visc"], cut, d["half_off"],
+                               d["half_nbr"], f)
+    assert rel_err(f, d["out_f"]) < TOL
+    de = np.zeros(nall)
+    S.ref_heatconduction_phasechange(3, 2, n, ng, 1, x, d["e"], d["cv"], d["rho"], rm, ty,
+                                     d["alpha"], d["fixflag"].ctypes.data, d["tc"].ctypes.data,
+                                     cut, d["half_off"], d["half_nbr"], de)
+    assert rel_err(de, d["out_de"]) < TOL
+    cg = np.zeros((nall, 3))
+    S.ref_colorgradient(3, 2, n, ng, x, d["rho"], rm, ty, d["cg_alpha"], cut, d["full_off"],
+                        d["full_nbr"], cg)
+    assert rel_err(cg[:n], d["out_cg"]) < TOL
+    f = np.zeros((nall, 3))
+    S.ref_surfacetension(3, 2, n, ng, 1, x, d["rho"], rm, ty, d["cg_all"], d["st_cut"],
+                         d["half_off"], d["half_nbr"], f)
+    assert rel_err(f, d["out_f_st"]) < TOL
+
+
+def test_new_run_restages_same_step_same_sizes(S):
+    """a second run set up at the same timestep with the same list build count
+    and atom counts (Verlet::setup resets neighbor->ncalls) must not reuse the atoms or the
+    list staged by the first: init_style starts a new epoch.  Two computes on the same
+    geometry with different vest/rho and a reversed neighbour order each match the oracle."""
+    d = load("c2_n6")
+    dim, nt, n, ng = int(d["dim"]), int(d["ntypes"]), int(d["nlocal"]), int(d["nghost"])
+    g = po.Ghosted(n, ng, d["x"], d["type"], None, None)
+    for k, scale in enumerate((1.0, 1.7)):
+        vest = d["vest"] * scale
+        rho = d["rho"] * (1.0 + 0.01 * k)
+        hoff, hnb = d["half_off"], d["half_nbr"].copy()
+        if k:
+            for i in range(n):
+                hnb[hoff[i]:hoff[i + 1]] = hnb[hoff[i]:hoff[i + 1]][::-1]
+        f, drho, de = np.zeros((n + ng, 3)), np.zeros(n + ng), np.zeros(n + ng)
+        S.ref_taitwater(dim, nt, n, ng, 1, d["x"], vest, rho, d["type"], d["mass"], d["rho0"],
+                        d["c0"], d["visc"], d["tait_cut"], hoff, hnb, f, drho, de)
+        fo, dro, deo = po.taitwater(dim, g, nt, 1, vest, rho, d["mass"], d["rho0"], d["c0"],
+                                    d["visc"], d["tait_cut"], hoff, hnb)
+        assert rel_err(f, fo) < TOL and rel_err(drho, dro) < TOL and rel_err(de, deo) < TOL
+
+
+@pytest.mark.parametrize("name", ["kat", "slab", "bubble", "slab2d"])
+def test_fix_phase_change_hip_vs_reference(S, name):
+    """fix phase_change/hip through its pre_exchange() on the reference FixPhaseChange's own
+    calls (tests/golden/pc_*.npz): the same atoms created at bit-identical positions, every
+    call (one fix object: the stream carries over), donors' rmass and energies."""
+    import ctypes as C
+    from test_phasechange_golden import call_inputs
+    from test_phasechange_golden import load as pcload
+    d = pcload(name)
+    args = [str(a).encode() for a in d["args"]]
+    av = (C.c_char_p * len(args))(*args)
+    h = S.ref_pc_new(int(d["dim"]), 2, d["boxlo"], d["boxhi"], 0, float(d["dt"]), len(args), av)
+    for c in range(int(d["ncalls"])):
+        g, arrays, off, nb = call_inputs(d, c)
+        nmax = g.nall + 256
+        A = {}
+        for k in ("x", "v", "vest", "cg"):
+            b = np.zeros((nmax, 3))
+            b[:g.nall] = arrays[k]
+            A[k] = b
+        for k in ("e", "rmass", "rho", "cv"):
+            b = np.zeros(nmax)
+            b[:g.nall] = arrays[k]
+            A[k] = b
+        t = np.zeros(nmax, np.int32)
+        t[:g.nall] = arrays["type"]
+        A["type"] = t
+        nr = C.c_long(0)
+        nn = S.ref_pc_pre_exchange(h, c + 1, g.nlocal, g.nghost, nmax, A["x"], A["v"],
+                                   A["vest"], A["cg"], A["e"], A["rmass"], A["rho"], A["cv"],
+                                   A["type"], off, nz(nb), len(g.swap_first) - 1, g.swap_first,
+                                   nz(g.src), C.byref(nr))
+        p = f"c{c}_out_"
+        assert nn == int(d[f"c{c}_out_nlocal"]), (name, c)
+        n0 = g.nlocal
+        assert np.array_equal(A["x"][:nn], d[p + "x"])
+        assert np.array_equal(A["type"][:nn], d[p + "type"])
+        for k in ("v", "vest", "e", "rmass", "rho", "cv"):
+            assert rel_err(A[k][:nn], d[p + k]) < TOL, (name, c, k)
+        assert rel_err(A["rmass"][:n0].sum(), d[p + "rmass"][:n0].sum()) < 1e-14

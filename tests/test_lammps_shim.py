@@ -1,15 +1,40 @@
-"""The LAMMPS-side classes (lammps-sph-multiphase_amd/lammps/) compile against the
-reference's own headers: the sph/<style>/hip pair styles derive from the reference styles
-and fix phase_change/hip from Fix, calling only what include/sph_hip.h declares.
-(Syntax/semantic check with g++ -fsyntax-only; needs /root/reference, skipped elsewhere.)"""
+"""The LAMMPS-side classes (lammps-sph-multiphase_amd/lammps/): the sph/<style>/hip pair
+styles derive from the reference styles and fix phase_change/hip from Fix, calling only what
+include/sph_hip.h declares.
+
+* They compile against the reference's own headers (g++ -fsyntax-only; this container).
+* They LINK: oracle/build_ref.sh builds oracle/_ref/libsph_shim.so from the reference's own
+  objects (Pair, Neighbor, CommBrick, the USER-SPH styles, Fix, Region, ...) plus these
+  classes plus libsph_hip.so -- what a LAMMPS binary with them would link.  The generated
+  style headers and force.cpp are not built here (the reference's build system is not run),
+  so registration is exercised the way force.cpp:81-88 / :148-166 use the style lines: the
+  headers' own PairStyle/FixStyle macros expanded into a creator table and looked up with
+  the "-sf hip" suffix rule (shim_style_lookup).
+* Without a HIP device, compute() ends in error->one with the shim's message -- never a
+  CPU fallback (src/GPU/pair_lj_cut_gpu.cpp:114-115 precedent); fix phase_change/hip parses
+  the reference's argument grammar with the reference's error messages.
+GPU parity of these classes against the reference's own compute: tests/test_gpu_shim.py."""
 import os
 import subprocess
+import sys
 
 import pytest
+
+import pyoracle as po
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/src"
 SHIM = os.path.join(ROOT, "lammps-sph-multiphase_amd", "lammps")
+
+# the reference styles of the hot path and their drop-in /hip classes
+STYLES = {"sph/rhosum": "PairSPHRhoSumHIP", "sph/taitwater": "PairSPHTaitwaterHIP",
+          "sph/taitwater/morris": "PairSPHTaitwaterMorrisHIP",
+          "sph/heatconduction": "PairSPHHeatConductionHIP",
+          "sph/rhosum/multiphase": "PairSPHRhoSumMultiphaseHIP",
+          "sph/taitwater/multiphase": "PairSPHTaitwaterMultiphaseHIP",
+          "sph/heatconduction/phasechange": "PairSPHHeatConductionPhaseChangeHIP",
+          "sph/colorgradient": "PairSPHColorGradientHIP",
+          "sph/surfacetension": "PairSPHSurfaceTensionHIP"}
 
 
 @pytest.mark.ref
@@ -22,3 +47,90 @@ def test_shim_compiles_against_reference_headers(src):
            os.path.join(SHIM, src)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
+
+
+def _shim():
+    if not po.shim_available():
+        pytest.skip("oracle/_ref/libsph_shim.so not built (needs /root/reference at build)")
+    return po.shim()
+
+
+@pytest.mark.parametrize("style", sorted(STYLES))
+def test_style_registered_with_suffix(style):
+    S = _shim()
+    buf = po.C.create_string_buffer(256)
+    assert S.lib.shim_style_lookup(0, style.encode(), b"hip", buf, 256) == 1
+    assert STYLES[style] in buf.value.decode()
+    # no /hip variant for a style outside the hot path
+    assert S.lib.shim_style_lookup(0, b"sph/lj", b"hip", buf, 256) == 0
+
+
+def test_fix_registered_with_suffix():
+    S = _shim()
+    buf = po.C.create_string_buffer(256)
+    assert S.lib.shim_style_lookup(1, b"phase_change", b"hip", buf, 256) == 1
+    assert "FixPhaseChangeHIP" in buf.value.decode()
+
+
+_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, %(oracle)r)
+import pyoracle as po
+S = po.shim() if %(shim)r else po.ref()
+what = %(what)r
+if what == "compute":
+    x = np.array([[0.0, 0, 0], [0.5, 0, 0]]); t = np.array([1, 1], np.int32)
+    off = np.array([0, 1, 1], np.int64); nb = np.array([1], np.int32)
+    z = np.zeros(6); one = np.ones(2); m = np.array([0.0, 1.0])
+    S.ref_taitwater(3, 1, 2, 0, 1, x, z.reshape(2, 3), one, t, m, m, np.array([0, 10.0]),
+                    np.ones((2, 2)), np.ones((2, 2)), off, nb, np.zeros((2, 3)), np.zeros(2),
+                    np.zeros(2))
+    print("NO ERROR")
+else:
+    args = [a.encode() for a in what]
+    av = (po.C.c_char_p * len(args))(*args)
+    S.ref_pc_new(3, 2, np.zeros(3), np.ones(3), 0, 1e-3, len(args), av)
+    print("NO ERROR")
+"""
+
+
+def _child(shim, what):
+    code = _CHILD % dict(oracle=os.path.join(ROOT, "oracle"), shim=shim, what=what)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")   # (no device, also on a GPU box)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=120)
+    return r.returncode, r.stdout + r.stderr
+
+
+def test_compute_without_device_is_error_one():
+    _shim()
+    rc, out = _child(True, "compute")
+    assert rc != 0 and "NO ERROR" not in out
+    assert "ERROR on proc 0: sph/<style>/hip styles need a HIP device" in out
+
+
+BASE = ["fdep", "all", "phase_change", "1", "1", "1", "1", "1", "1", "1", "2", "1", "123456"]
+
+
+@pytest.mark.parametrize("tail,msg", [
+    (["1.0", "region", "box", "units", "lattice"],
+     "Illegal fix phase_change command: 'units lattice' is not implemented"),
+    (["1.0", "region", "nosuch"], "Region ID for fix phase_change does not exist"),
+    (["1.0", "units", "box"], "Must specify a region in fix phase_change"),
+    (["-1.0", "region", "box"], "Illegal value for change_chance"),
+    (["1.0", "region", "box", "bogus", "1"], "Illegal fix phase_change command"),
+    ([], "Illegal fix phase_change command"),
+])
+def test_fix_arguments_match_reference_errors(tail, msg):
+    """The same argument list through the reference's FixPhaseChange and fix
+    phase_change/hip: both stop with the same error->all message."""
+    _shim()
+    if not po.ref_available():
+        pytest.skip("reference oracle not built")
+    outs = []
+    for shim in (False, True):
+        rc, out = _child(shim, BASE + tail)
+        assert rc != 0 and "NO ERROR" not in out, out[-400:]
+        line = [l for l in out.splitlines() if l.startswith("ERROR")][0]
+        outs.append(line.split(" (")[0])
+    assert outs[0] == outs[1] == "ERROR: " + msg

@@ -45,7 +45,17 @@ int64_t list_key(LAMMPS *lmp) { return (int64_t)(g_epoch << 40) + (int64_t)lmp->
 void LAMMPS_NS::sph_hip_new_run() { g_epoch++; }
 
 sph_hip_ctx *LAMMPS_NS::sph_hip_rank_ctx(LAMMPS *lmp) {
+  // one context per rank; made again when the system it was made for changed (a `clear`
+  // followed by a new box with another dimension / number of types / newton setting)
+  static int made_for[3] = {0, 0, 0};
+  const int want[3] = {lmp->domain->dimension, lmp->atom->ntypes, lmp->force->newton_pair};
+  if (g_ctx && (want[0] != made_for[0] || want[1] != made_for[1] || want[2] != made_for[2])) {
+    sph_hip_destroy(g_ctx);
+    g_ctx = NULL;
+    g_key.epoch = -1;
+  }
   if (!g_ctx) {
+    for (int k = 0; k < 3; k++) made_for[k] = want[k];
     const int ndev = sph_hip_device_count();
     if (ndev < 1) lmp->error->one(FLERR, "sph/<style>/hip styles need a HIP device");
     sph_hip_check(lmp,
@@ -101,9 +111,12 @@ namespace {
 // (nt+1)^2 row-major view of a memory->create 2-D table (contiguous backing)
 const double *tab(double **t) { return &t[0][0]; }
 
+// (vflag_atom / vflag_global are meaningful only after ev_setup, i.e. when evflag is set:
+// Pair's constructor leaves them uninitialised, pair.cpp:684-692)
 double *virial_target(LAMMPS *lmp, Pair *p) {
+  if (!p->evflag) return NULL;
   if (p->vflag_atom) lmp->error->all(FLERR, "sph/<style>/hip styles do not tally per-atom virials");
-  return (p->evflag && p->vflag_global) ? p->virial : NULL;
+  return p->vflag_global ? p->virial : NULL;
 }
 
 }  // namespace

@@ -183,7 +183,10 @@ long orc_neigh_full(int dim, int nlocal, int nall, const double *x, const int *t
   for (int i = 1; i <= ntypes; i++)
     for (int j = 1; j <= ntypes; j++)
       if (cutneighsq[IDX2(ntypes, i, j)] > cmaxsq) cmaxsq = cutneighsq[IDX2(ntypes, i, j)];
-  double binsize = sqrt(cmaxsq);
+  /* bins a hair wider than the cutoff: a pair at exactly the cutoff (lattices) then never
+     lands two bins apart through the rounding of (x - lo) / binsize, so the 27-bin walk
+     finds every j the reference's stencil finds (neigh_full.cpp:312 keeps rsq <= cutneighsq) */
+  double binsize = sqrt(cmaxsq) * (1.0 + 1e-9);
   if (binsize <= 0.0) binsize = 1.0;
   double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
   for (int i = 0; i < nall; i++)

@@ -201,3 +201,23 @@ def test_oracle_vs_reference_fresh_seed(po, ref, case):
                                 ph.c0, ph.visc, ph.tait_cut, P["hoff"], P["hnb"],
                                 morris=ph.morris)
     assert np.array_equal(f, fo) and np.array_equal(drho, dro) and np.array_equal(de, deo)
+
+
+@pytest.mark.ref
+@pytest.mark.parametrize("nx,dim", [(10, 3), (16, 2), (7, 3)])
+def test_oracle_vs_reference_lattice_ties(po, ref, nx, dim):
+    """On the C5 bubble lattice ~30 pairs per atom sit exactly at the cutoff (skin 0): the
+    reference's Neighbor::full_bin keeps every one with rsq <= cutneighsq, and so must the
+    restatement's builder (whose bins are a hair wider than the cutoff so that no such pair
+    is ever two bins apart)."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import ref_full
+    from scenarios import bubble_physics, bubble_system
+    s = bubble_system(nx, dim=dim)
+    ph = bubble_physics(nx, dim=dim)
+    r = po.MpRefRun(s, ph)
+    r.setup()
+    foff, fnb = ref_full(ref, r.s, r.g, r.cns, r.cutneighmax)
+    assert np.array_equal(foff, r.foff)
+    assert np.array_equal(sorted_rows(foff, fnb), sorted_rows(r.foff, r.fnb))

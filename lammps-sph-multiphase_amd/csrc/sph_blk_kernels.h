@@ -461,8 +461,13 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
              const unsigned short *__restrict__ snbr, int sstride,
              const int *__restrict__ rcnt, double4 *__restrict__ xf,
              const int *__restrict__ ty, double4 *__restrict__ vr,
-             const Coefs *__restrict__ cf, int um) {
+             const Coefs *__restrict__ cf, int um, const unsigned short *__restrict__ snbi,
+             const int *__restrict__ icnt, const int *__restrict__ moved) {
   constexpr int NTH = R * G;
+  if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
+    snbr = snbi;
+    rcnt = icnt;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   const int nt1 = cf->ntypes + 1;
@@ -538,6 +543,75 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   }
 }
 
+// INNER rows for the pair passes, written at every rebuild: the slots of each full row
+// (cutneighsq = (cut + skin)^2) whose pair is within cut + m now, m = a quarter of the skin.
+// While no atom has moved m/2 since (k_initial_integrate / k_final_initial raise *moved
+// otherwise) every pair inside a pair style's cut is among them, so the passes walk ~128
+// instead of ~160 entries per row at C2 with identical terms (a dropped entry's kernel
+// weight is exactly zero); once an atom has moved further the passes fall back to the full
+// rows until the next rebuild.  The slots keep their full-row order (rank by ballot within
+// the row's G lanes); tails are padded with the sentinel like the full rows.
+template <int R, int G, int U, int NCH, bool NT1, int CQ>
+__global__ void __launch_bounds__(R * G)
+k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
+            const unsigned short *__restrict__ snbr, int sstride, const int *__restrict__ rcnt,
+            const double4 *__restrict__ xf, const int *__restrict__ ty,
+            const Coefs *__restrict__ cf, unsigned short *__restrict__ snbi,
+            int *__restrict__ icnt, int um) {
+  constexpr int NTH = R * G;
+  extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
+  __shared__ double s_c[NT1 ? 1 : NT2];
+  const int b = (int)xcd_block(), tid = threadIdx.x;
+  const int row = b * R + tid / G, lane = tid & (G - 1);
+  const bool live = row < n;
+  const int rr = live ? row : n - 1;
+  const int u = ucnt[b];
+  const int c = live ? rcnt[rr] : 0;
+  const int *const ul = ulist + (size_t)b * ucap;
+  BlkSlots<G, U, NCH> sw;
+  sw.load(snbr + (size_t)rr * sstride, c, lane);
+  const double4 xi = xf[rr];
+  const int it = NT1 ? 1 : ty[rr];
+  const int nt1 = cf->ntypes + 1;
+  double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
+  double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)(um + 1) * 16);
+  unsigned char *const s_t = blk_smem + (size_t)(um + 1) * 24;
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += NTH) s_c[t] = cf->cutinsq[t];
+  for (int p = tid; p < u; p += NTH) {
+    const int j = ul[p];
+    const double4 x = xf[j];
+    s_xy[p + 1] = make_double2(x.x, x.y);
+    s_z[p + 1] = x.z;
+    if (!NT1) s_t[p + 1] = (unsigned char)ty[j];
+  }
+  if (tid == 0) {
+    s_xy[0] = make_double2(1e100, 1e100);
+    s_z[0] = 1e100;
+    if (!NT1) s_t[0] = 1;
+  }
+  __syncthreads();
+  const double c1 = NT1 ? cf->cutinsq[3] : 0.0;
+  const int grp = (tid & 63) / G;                   // the row's lane group in the wave
+  unsigned short *const out = snbi + (size_t)rr * sstride;
+  int base = 0;
+  sw.walk(c, lane, [&](int q, bool in) {
+    const int sj = blk_s<CQ>(q);
+    const double2 xy = s_xy[sj];
+    const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    const bool hit = in && rsq < (NT1 ? c1 : s_c[it * nt1 + s_t[sj]]);
+    const unsigned long long m = __ballot(hit);
+    const unsigned g = (unsigned)(m >> (grp * G)) & ((1u << G) - 1u);
+    if (hit && live) out[blk_tpos<G, U>(base + __popc(g & ((1u << lane) - 1u)))] = (unsigned short)q;
+    base += __popc(g);
+  });
+  if (!live) return;
+  if (lane == 0) icnt[row] = base;
+  const int cend = min((base + U * G - 1) / (U * G) * (U * G), sstride);
+  for (int k = base + lane; k < cend; k += G) out[blk_tpos<G, U>(k)] = 0;  // the sentinel
+}
+
 // sph/taitwater[/morris] [+ sph/heatconduction] over the block union (full list, i side
 // only), pair_sph_taitwater.cpp:139-191, pair_sph_taitwater_morris.cpp:139-191,
 // pair_sph_heatconduction.cpp:103-124.  blist == nullptr: every block whose union fits the
@@ -558,7 +632,13 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             const double4 *__restrict__ vr, const int *__restrict__ ty,
             const double *__restrict__ en, const Coefs *__restrict__ cf,
             double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-            double gz, int um, const int *__restrict__ blist, int cq) {
+            double gz, int um, const int *__restrict__ blist, int cq,
+            const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,
+            const int *__restrict__ moved) {
+  if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
+    snbr = snbi;
+    rcnt = icnt;
+  }
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr int NTH = R * G;
@@ -756,6 +836,9 @@ struct BlkArgs {
   int cq = BLK_CH / 16;  // image chunk bytes / 16 (BLK_CHE / 16 with the heat term)
   const int *ulist = nullptr, *ucnt = nullptr, *rcnt = nullptr, *blist = nullptr;
   const unsigned short *snbr = nullptr;
+  // inner rows (k_blk_inner) and the device flag that retires them; snbi == nullptr: none
+  const unsigned short *snbi = nullptr;
+  const int *icnt = nullptr, *moved = nullptr;
   bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
 };
 
@@ -806,7 +889,8 @@ inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
-                     k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um);
+                     k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um, k.snbi, k.icnt,
+                     k.moved);
 }
 template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
@@ -841,11 +925,47 @@ inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
                                   (int)std::max(lds, ldsb)));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
-                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq);
+                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq, k.snbi,
+                     k.icnt, k.moved);
   if (k.nbig > 0)
     hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
                        k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
-                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq);
+                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq, k.snbi, k.icnt, k.moved);
+}
+
+// the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum
+template <int R, int G, int U, int NCH, bool NT1>
+inline void blk_inner_t(hipStream_t s, const BlkArgs &k, const double4 *xf, const int *ty,
+                        const Coefs *cf, unsigned short *snbi, int *icnt) {
+  const size_t lds = blk_rho_lds(k.um, NT1);
+  auto fn = k.cq == BLK_CH / 16 ? k_blk_inner<R, G, U, NCH, NT1, BLK_CH / 16>
+                                : k_blk_inner<R, G, U, NCH, NT1, BLK_CHE / 16>;
+  SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
+                     k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, cf, snbi, icnt, k.um);
+}
+template <int R, int G, int U>
+inline void blk_inner_s(bool nt1, hipStream_t s, const BlkArgs &k, const double4 *xf,
+                        const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt) {
+  const bool pre = k.pre(BlkShape{R, G, U});
+  if (nt1) {
+    if (pre) blk_inner_t<R, G, U, BLK_NCH, true>(s, k, xf, ty, cf, snbi, icnt);
+    else blk_inner_t<R, G, U, 0, true>(s, k, xf, ty, cf, snbi, icnt);
+  } else {
+    if (pre) blk_inner_t<R, G, U, BLK_NCH, false>(s, k, xf, ty, cf, snbi, icnt);
+    else blk_inner_t<R, G, U, 0, false>(s, k, xf, ty, cf, snbi, icnt);
+  }
+}
+inline void blk_inner(bool nt1, hipStream_t s, const BlkArgs &k, const double4 *xf,
+                      const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt) {
+  if (k.n == 0) return;
+  switch (k.shape) {
+#define SPH_CASE(q, R, G, U) \
+  case q: blk_inner_s<R, G, U>(nt1, s, k, xf, ty, cf, snbi, icnt); break;
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+  }
 }
 template <int R, int G, int U, int NCH, bool NT1>
 inline void blk_force_n(int visc, int mode, hipStream_t s, const BlkArgs &k, const RowArgs &a) {

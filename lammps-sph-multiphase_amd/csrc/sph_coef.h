@@ -88,7 +88,9 @@ inline void coef_heat(Coefs &c, int dim, int nt, const double *alpha, const doub
 }
 
 // neighbor.cpp:251-268: cutoff = sqrt(cutsq) with cutsq = cut*cut, cut += skin, squared
-inline double coef_cutneigh(Coefs &c, int nt, const double *cutmax, double skin) {
+// margin: the block path's inner rows keep pairs within cut + margin (k_blk_inner)
+inline double coef_cutneigh(Coefs &c, int nt, const double *cutmax, double skin,
+                            double margin = 0.0) {
   double cmax = 0.0;
   for (int i = 1; i <= nt; i++)
     for (int j = 1; j <= nt; j++) {
@@ -96,6 +98,8 @@ inline double coef_cutneigh(Coefs &c, int nt, const double *cutmax, double skin)
       const double cutoff = std::sqrt(cu * cu);
       const double cut = cutoff + (cutoff > 0.0 ? skin : 0.0);
       c.cutneighsq[i * (nt + 1) + j] = cut * cut;
+      const double ci = cutoff + (cutoff > 0.0 ? margin : 0.0);
+      c.cutinsq[i * (nt + 1) + j] = ci * ci;
       if (cut > cmax) cmax = cut;
     }
   return cmax;

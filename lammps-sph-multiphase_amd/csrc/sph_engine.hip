@@ -239,6 +239,13 @@ struct sph_engine {
   int blk_sh = 0, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
   DBuf<int> ulist, ucnt, bl;
   DBuf<unsigned short> snbr;
+  // ... and the inner rows of the build (k_blk_inner: pairs within cut + inner_margin), the
+  // owned positions they were written at and the flag that retires them (sc.x0 / sc.moved)
+  DBuf<unsigned short> snbi;
+  DBuf<int> icnt, moved;
+  DBuf<double4> x0;
+  double inner_margin = 0.0;
+  bool inner = false;
   DBuf<int> nbs;  // fixed-stride scratch rows of a CSR build (list_q)
   DBuf<int> mx, ccnt;  // scratch scalars; full-list row counts of the current build
   DBuf<long long> blen;
@@ -1215,6 +1222,11 @@ struct sph_engine {
     k.ucnt = ucnt.p;
     k.rcnt = ccnt.p;
     k.snbr = snbr.p;
+    if (inner) {
+      k.snbi = snbi.p;
+      k.icnt = icnt.p;
+      k.moved = moved.p;
+    }
     return k;
   }
 
@@ -1238,6 +1250,7 @@ struct sph_engine {
     }
     if (want_blk()) {
       blk = build_blk();
+      build_inner();
       if (blk && !need_csr) {
         strided = true;  // (ccnt holds the full-list counts; list_entries sums them)
         nbr_total = -1;
@@ -1248,6 +1261,28 @@ struct sph_engine {
     }
     ov_ready = false;
     if (overlap_on()) classify_rows();
+  }
+
+  // The block path's inner rows (sph_blk_kernels.h k_blk_inner), written after every block
+  // build: the pair passes walk them while no atom has moved inner_margin / 2 since (one
+  // brick: ghosts move with their owners; bricks keep the full rows for now).
+  void build_inner() {
+    inner = blk && inner_margin > 0.0 && !multi() && nlocal > 0;
+    sc.x0 = nullptr;
+    if (!inner) return;
+    const BlkShape sh = blk_shape(blk_sh);
+    snbi.reserve((size_t)nlocal * blk_sstride + 2 * sh.U * sh.G);
+    icnt.reserve(nlocal);
+    moved.reserve(1);
+    x0.reserve(nlocal);
+    BlkArgs k = blk_args();
+    blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
+    SPH_HIP_TRY(hipMemcpyAsync(x0.p, xf.p, (size_t)nlocal * sizeof(double4),
+                               hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemsetAsync(moved.p, 0, sizeof(int), s));
+    sc.x0 = x0.p;
+    sc.lim2 = 0.25 * inner_margin * inner_margin;
+    sc.moved = moved.p;
   }
 
   bool overlap_on() const {
@@ -1967,7 +2002,9 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     // mirror upper triangle into a symmetric max-cut table (init_one semantics)
     for (int i = 1; i <= nt; i++)
       for (int j = 1; j < i; j++) cutmax[i * (nt + 1) + j] = cutmax[j * (nt + 1) + i];
-    e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin);
+    // inner rows of the block path: a quarter of the skin (sph_blk_kernels.h k_blk_inner)
+    e->inner_margin = 0.25 * cfg->skin;
+    e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin, e->inner_margin);
     for (int k = 0; k < NT2; k++)  // tight-list test: the largest force-style cutoff
       c.fcutsq[k] = std::max((e->force_mode & M_TAIT) ? c.tait[k].cutsq : 0.0,
                              (e->force_mode & M_HEAT) ? c.heat[k].cutsq : 0.0);
@@ -2055,6 +2092,10 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->bkey, &e->bkey2}) b->release();
   for (auto *b : {&e->flags, &e->tmp, &e->cbs, &e->cbr, &e->flag2, &e->fl_in, &e->fl_bd}) b->release();
   e->snbr.release();
+  e->snbi.release();
+  e->icnt.release();
+  e->moved.release();
+  e->x0.release();
   e->blen.release();
   for (auto &sw : e->swaps) sw.list.release();
   for (auto &p : e->pending) {

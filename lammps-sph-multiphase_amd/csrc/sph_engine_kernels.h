@@ -13,7 +13,20 @@ struct StepConst {
   double dtv, dtf;
   double mass[MAXT + 1];
   int stationary_mask;
+  // the block path's inner rows (k_blk_inner): positions when they were written, and the
+  // flag raised once an atom has moved more than half their margin since (x0 == nullptr:
+  // no inner rows)
+  const double4 *x0;
+  double lim2;
+  int *moved;
 };
+
+__device__ __forceinline__ void inner_check(const StepConst &sc, int i, const double4 &x) {
+  if (!sc.x0) return;
+  const double4 a = sc.x0[i];
+  const double dx = x.x - a.x, dy = x.y - a.y, dz = x.z - a.z;
+  if (dx * dx + dy * dy + dz * dz > sc.lim2) atomicOr(sc.moved, 1);
+}
 
 // FixMeso::initial_integrate (fix_meso.cpp:91-140) / FixMesoStationary (:71-90)
 static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restrict__ xf,
@@ -45,6 +58,7 @@ static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restr
     x.z += sc.dtv * v.z;
     vel[i] = v;
     xf[i] = x;
+    inner_check(sc, i, x);
   }
   vr[i] = vv;
 }
@@ -111,6 +125,7 @@ static __global__ void k_final_initial(int n, StepConst sc, double4 *__restrict_
     x.z += sc.dtv * v.z;
     vel[i] = v;
     xf[i] = x;
+    inner_check(sc, i, x);
   }
   en[i] = e;
   vr[i] = vv;

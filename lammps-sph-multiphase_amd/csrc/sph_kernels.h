@@ -58,6 +58,7 @@ struct Coefs {
   TaitPair tait[NT2];
   HeatPair heat[NT2];
   double cutneighsq[NT2];
+  double cutinsq[NT2];     // (cut + inner margin)^2 of the block path's inner rows
   double fcutsq[NT2];  // engine: max cutsq of the enabled force styles (tight-list test)
 };
 

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 
 #include "sph_engine_kernels.h"
 #include "sph_row2_kernels.h"
@@ -67,8 +69,17 @@ __device__ __forceinline__ int blk_scan(int v, int *s_w, int *total) {
 // row's G lanes) is stored at U*l + u, so a lane's U slots of a chunk are one load.
 template <int G, int U>
 __host__ __device__ __forceinline__ int blk_tpos(int q) {
-  const int c = q % (U * G);
-  return q - c + U * (c % G) + c / G;
+  const unsigned uq = (unsigned)q, c = uq % (U * G);  // (unsigned: masks and shifts)
+  return (int)(uq - c + U * (c % G) + c / G);
+}
+
+// v_writelane_b32 through its LLVM intrinsic (no clang builtin here; the compiler then
+// knows the instruction and inserts the SGPR-write -> lane-read wait states)
+__device__ int sph_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+// lane LANE of v takes the wave-uniform value `val`
+template <int LANE>
+__device__ __forceinline__ unsigned writelane(unsigned v, unsigned val) {
+  return (unsigned)sph_writelane_i32((int)val, LANE, (int)v);
 }
 
 // ---- the union image ---------------------------------------------------------------------
@@ -386,6 +397,337 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
   }
   const int cend = min((cntr + U * G - 1) / (U * G) * (U * G), sstride);
   for (int k = cntr + sub; k < cend; k += TPR) out[blk_tpos<G, U>(k)] = 0;  // the sentinel
+}
+
+// ---- block neighbour build v2: every row against the block's candidates, ballots --------
+// One workgroup (4 waves) per block of R <= 64 rows.
+//  1. The block's bounding box; the bins within cutneighmax of it (per (y, z) bin-row the
+//     x-range is cut to the sphere-swept box): one contiguous xb range per bin-row, the RAW
+//     candidates, numbered in bin order.
+//  2. Prefilter: a raw candidate farther than cutneighmax from the box cannot be anyone's
+//     neighbour; the others (~60 % at C2) are compacted, in raw order, into the block's
+//     CANDIDATES (their xb positions in LDS).
+//  3. A wave takes 64 candidates at a time, one per lane, and runs every row of the block
+//     against them: the rows' positions are in LDS (broadcast reads), eight rows per
+//     unrolled step; the test is Neighbor::full_bin's (rsq <= cutneighsq, j != i;
+//     neigh_full.cpp:305-312) and its ballot is the row's 64-bit hit word for those
+//     candidates, kept in lane r's registers -- no atomics, no per-row range bookkeeping.
+//     A second ballot (rsq < (cut + inner margin)^2) gives the inner rows (k_blk_inner's)
+//     in the same pass.
+//  4. The union is the OR of the rows' words (candidate order); slots are ranks among used
+//     candidates, as in k_blk_neigh, whose outputs (ulist, ucnt, rcnt, chunk-transposed
+//     16-bit slot rows, the same overflow and statistics words) this kernel produces.
+// Overflow (> BLK_MCAP raw or BLK_SCAP kept candidates, or a bin box wider than BLK_TBL
+// bin-rows) raises *ovf and the host falls back to k_blk_neigh.
+constexpr int BLK_SCAP = 2048;  // kept candidates per block (k_blk_build)
+// set bits of a wave-uniform 64-bit mask below this lane (v_mbcnt_lo / v_mbcnt_hi)
+__device__ __forceinline__ int blk_mbcnt(unsigned long long m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// f(std::integral_constant<int, r>) for r = 0 .. N-1, unrolled at compile time
+template <int N, class F, int... I>
+__device__ __forceinline__ void blk_rows_(F &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void blk_rows(F &&f) {
+  blk_rows_<N>(f, std::make_integer_sequence<int, N>{});
+}
+template <int R, int G, int U, bool NT1, bool INNER>
+__global__ void __launch_bounds__(256)
+k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
+            const int *__restrict__ ty, const double4 *__restrict__ xb,
+            const int *__restrict__ tb, const int *__restrict__ qbeg,
+            const Coefs *__restrict__ cf, int ucap, int sstride, int *__restrict__ ulist,
+            int *__restrict__ ucnt, int *__restrict__ rcnt, unsigned short *__restrict__ snbr,
+            int *__restrict__ icnt, unsigned short *__restrict__ snbi,
+            int *__restrict__ ovf, int *__restrict__ umax, int cq) {
+  static_assert(R <= 64 && R % 8 == 0, "one lane per row, rows in steps of 8");
+  constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
+  constexpr int TPR = NT / R;
+  __shared__ unsigned long long s_bm[SCH][R];
+  __shared__ unsigned long long s_bi[INNER ? SCH : 1][R];
+  __shared__ unsigned long long s_used[SCH];
+  __shared__ unsigned short s_q[SCH][64];
+  __shared__ int s_rpf[NW][64], s_rpi[INNER ? NW : 1][64];
+  __shared__ unsigned long long s_keep[MCH];
+  __shared__ int s_cpos[BLK_SCAP];
+  __shared__ int s_upre[SCH + 1], s_kpre[MCH + 1];
+  __shared__ int s_pre[BLK_TBL + 1], s_st[BLK_TBL];
+  __shared__ double4 s_row[R];
+  __shared__ int s_rty[R];
+  __shared__ int s_self[NW][64];
+  __shared__ double s_bb[6];
+  __shared__ double s_cns[NT1 ? 1 : NT2], s_cin[(NT1 || !INNER) ? 1 : NT2];
+  __shared__ int s_w[NW];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int row0 = b * R;
+  const int nrow = min(R, n - row0);
+  const int nt1 = cf->ntypes + 1;
+  if (!NT1)
+    for (int t = tid; t < nt1 * nt1; t += NT) {
+      s_cns[t] = cf->cutneighsq[t];
+      if (INNER) s_cin[t] = cf->cutinsq[t];
+    }
+  // 1) the rows (far away past the last row: never a hit) and their bounding box (wave 0)
+  if (wv == 0) {
+    double lo[3], hi[3];
+    if (lane < R) {
+      const double4 x = lane < nrow ? xf[row0 + lane] : make_double4(1e300, 1e300, 1e300, 0.0);
+      s_row[lane] = x;
+      if (!NT1) s_rty[lane] = lane < nrow ? ty[row0 + lane] : 1;
+    }
+    if (lane < nrow) {
+      const double4 x = xf[row0 + lane];
+      lo[0] = hi[0] = x.x;
+      lo[1] = hi[1] = x.y;
+      lo[2] = hi[2] = x.z;
+    } else {
+      lo[0] = lo[1] = lo[2] = 1e300;
+      hi[0] = hi[1] = hi[2] = -1e300;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        lo[k] = fmin(lo[k], __shfl_xor(lo[k], d, 64));
+        hi[k] = fmax(hi[k], __shfl_xor(hi[k], d, 64));
+      }
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) {
+        s_bb[k] = lo[k];
+        s_bb[3 + k] = hi[k];
+      }
+  }
+  __syncthreads();
+  // the bin-rows of the sphere-swept box and their x-ranges (conservative margins as
+  // k_neigh3's slab tests)
+  const double cm = sqrt(q.cutmaxsq) * (1.0 + 1e-9);
+  const int by0 = bin_coord(s_bb[1] - cm, q.lo[1], q.inv[1], q.nb[1]);
+  const int by1 = bin_coord(s_bb[4] + cm, q.lo[1], q.inv[1], q.nb[1]);
+  const int bz0 = dim == 3 ? bin_coord(s_bb[2] - cm, q.lo[2], q.inv[2], q.nb[2]) : 0;
+  const int bz1 = dim == 3 ? bin_coord(s_bb[5] + cm, q.lo[2], q.inv[2], q.nb[2]) : 0;
+  const int ny = by1 - by0 + 1, nz = bz1 - bz0 + 1;
+  if (ny * nz > BLK_TBL) {  // workgroup-uniform
+    if (tid == 0) atomicMax(ovf, 1 << 20);
+    return;
+  }
+  int len = 0, st = 0;
+  if (tid < ny * nz) {
+    const int by = by0 + tid % ny, bz = bz0 + tid / ny;
+    auto gap = [&](int bb, int k) {  // box interval to bin slab bb along axis k
+      const double slo = q.lo[k] + bb * q.size[k], shi = slo + q.size[k];
+      const double g = fmax(slo - s_bb[3 + k], s_bb[k] - shi);
+      return fmax(g - 1e-6 * q.size[k], 0.0);
+    };
+    const double gy = gap(by, 1), gz = dim == 3 ? gap(bz, 2) : 0.0;
+    const double d2 = gy * gy + gz * gz;
+    if (d2 <= q.cutmaxsq) {
+      const double ext = sqrt(q.cutmaxsq - d2) * (1.0 + 1e-9) + 1e-9 * q.size[0];
+      const int bx0 = bin_coord(s_bb[0] - ext, q.lo[0], q.inv[0], q.nb[0]);
+      const int bx1 = bin_coord(s_bb[3] + ext, q.lo[0], q.inv[0], q.nb[0]);
+      const int brow = (bz * q.nb[1] + by) * q.nb[0];
+      st = qbeg[brow + bx0];
+      len = qbeg[brow + bx1 + 1] - st;
+    }
+  }
+  int M = 0;
+  const int pre = blk_scan<NT>(len, s_w, &M);
+  if (M > BLK_MCAP) {
+    if (tid == 0) atomicMax(ovf, M);
+    return;
+  }
+  const int ntab = ny * nz;
+  if (tid < ntab) {
+    s_pre[tid] = pre;
+    s_st[tid] = st;
+  }
+  __syncthreads();
+  const int mch = (M + 63) >> 6;
+  // raw candidate p -> its xb position (last bin-row with s_pre <= p)
+  auto rpos = [&](int p) {
+    int lo = 0, hi = ntab - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    return s_st[lo] + (p - s_pre[lo]);
+  };
+  // 2) prefilter: distance to the box <= cutneighmax (conservative margins)
+  const double cmsq = q.cutmaxsq * (1.0 + 1e-9) + 1e-12 * q.size[0] * q.size[0];
+  for (int c = wv; c < mch; c += NW) {
+    const int p = c * 64 + lane;
+    bool keep = false;
+    if (p < M) {
+      const double4 x = xb[rpos(p)];
+      const double gx = fmax(fmax(s_bb[0] - x.x, x.x - s_bb[3]), 0.0);
+      const double gy = fmax(fmax(s_bb[1] - x.y, x.y - s_bb[4]), 0.0);
+      const double gz = fmax(fmax(s_bb[2] - x.z, x.z - s_bb[5]), 0.0);
+      keep = gx * gx + gy * gy + gz * gz <= cmsq;
+    }
+    const unsigned long long k = __ballot(keep);
+    if (lane == 0) s_keep[c] = k;
+  }
+  __syncthreads();
+  int K = 0;
+  {
+    const int v = tid < mch ? __popcll(s_keep[tid]) : 0;
+    const int ex = blk_scan<NT>(v, s_w, &K);
+    if (tid < mch) s_kpre[tid] = ex;
+  }
+  if (K > BLK_SCAP) {  // workgroup-uniform
+    if (tid == 0) atomicMax(ovf, 1 << 22);
+    return;
+  }
+  __syncthreads();
+  for (int c = wv; c < mch; c += NW) {
+    const unsigned long long k = s_keep[c];
+    if ((k >> lane) & 1ull)
+      s_cpos[s_kpre[c] + __popcll(k & ((1ull << lane) - 1ull))] = rpos(c * 64 + lane);
+  }
+  __syncthreads();
+  const int nch = (K + 63) >> 6;
+  // 3) tests: chunk c of 64 kept candidates (one per lane) against every row
+  const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
+  const double cin1 = (NT1 && INNER) ? cf->cutinsq[3] : 0.0;
+  for (int c = wv; c < nch; c += NW) {
+    const int p = c * 64 + lane;
+    const bool valid = p < K;
+    double4 xc = make_double4(-1e300, -1e300, -1e300, -1.0);
+    int tc = 1;
+    if (valid) {
+      const int pos = s_cpos[p];
+      xc = xb[pos];
+      if (!NT1) tc = tb[pos];
+    }
+    const int cid = valid ? (int)xc.w : -1;
+    // j != i: the lane holding row r's own atom (if this chunk has it), for lane r
+    s_self[wv][lane] = -1;
+    if (cid >= row0 && cid < row0 + R) s_self[wv][cid - row0] = lane;
+    unsigned my_lo = 0u, my_hi = 0u, mi_lo = 0u, mi_hi = 0u;
+    // (an opaque 0: the compiler must not hoist the 64 rows' positions out of the chunk
+    // loop into registers -- 256+ VGPRs, one wave per SIMD)
+    int ro = 0;
+    asm volatile("" : "+s"(ro));
+    // every row, fully unrolled (lane r keeps row r's 64-bit word)
+    blk_rows<R>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      const double4 xi = s_row[r + ro];
+      const double rsq = rsq_ref(xi.x - xc.x, xi.y - xc.y, xi.z - xc.z);
+      double cn = cns1, ci = cin1;
+      if (!NT1) {
+        const int it = s_rty[r];
+        cn = s_cns[it * nt1 + tc];
+        if (INNER) ci = s_cin[it * nt1 + tc];
+      }
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(rsq <= cn);
+      my_lo = writelane<r>(my_lo, (unsigned)m);
+      my_hi = writelane<r>(my_hi, (unsigned)(m >> 32));
+      if (INNER) {
+        const unsigned long long mi = __builtin_amdgcn_ballot_w64(rsq < ci);
+        mi_lo = writelane<r>(mi_lo, (unsigned)mi);
+        mi_hi = writelane<r>(mi_hi, (unsigned)(mi >> 32));
+      }
+    });
+    // (rows past the last one sit at 1e300: their words are 0 already)
+    const int self = s_self[wv][lane];
+    const unsigned long long keep = ~((unsigned long long)(self >= 0) << (self & 63));
+    const unsigned long long mine = (((unsigned long long)my_hi << 32) | my_lo) & keep;
+    if (lane < R) {
+      s_bm[c][lane] = mine;
+      if (INNER) s_bi[c][lane] = (((unsigned long long)mi_hi << 32) | mi_lo) & keep;
+    }
+    unsigned long long u = mine;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) u |= __shfl_xor(u, d, 64);
+    if (lane == 0) s_used[c] = u;
+  }
+  __syncthreads();
+  // 4) the union: used candidates in candidate order (slot = rank + 1)
+  int u = 0;
+  {
+    const int v = tid < nch ? __popcll(s_used[tid]) : 0;
+    const int ex = blk_scan<NT>(v, s_w, &u);
+    if (tid < nch) s_upre[tid] = ex;
+  }
+  __syncthreads();
+  // the union list, and each chunk's slot words: candidate l of chunk c, if used, has slot
+  // s_upre[c] + 1 + (used candidates below it)
+  for (int c = wv; c < nch; c += NW) {
+    const unsigned long long used = s_used[c];
+    const int below = blk_mbcnt(used);
+    s_q[c][lane] = (unsigned short)blk_q(s_upre[c] + 1 + below, cq);
+    if ((used >> lane) & 1ull)
+      ulist[(size_t)b * ucap + s_upre[c] + below] = (int)xb[s_cpos[c * 64 + lane]].w;
+  }
+  if (tid == 0) {
+    ucnt[b] = u;
+    atomicMax(umax, u);
+    atomicMax(umax + 1, K);   // (stats: largest candidate set, sums of candidates / unions)
+    atomicAdd(umax + 2, K);
+    atomicAdd(umax + 3, u);
+  }
+  __syncthreads();
+  // 5) the slot rows, full and inner: lane r of every wave is row r; wave w takes a
+  // contiguous quarter of the chunks, starting at the row's hits in the chunks before it.
+  // Each lane walks its row's set bits (a full-list hit; the inner bit is a subset) and
+  // writes the slot word to the full row and, if inner, to the inner row: one useful store
+  // per lane per step, ascending slot order.
+  const int cpw = (nch + NW - 1) / NW;
+  const int c0 = min(wv * cpw, nch), c1 = min(c0 + cpw, nch);
+  int nf = 0, ni = 0;
+  if (lane < R)
+    for (int c = c0; c < c1; c++) {
+      nf += __popcll(s_bm[c][lane]);
+      if (INNER) ni += __popcll(s_bi[c][lane]);
+    }
+  if (lane < R) {
+    s_rpf[wv][lane] = nf;
+    if (INNER) s_rpi[wv][lane] = ni;
+  }
+  __syncthreads();
+  if (lane >= nrow) return;
+  const int row = row0 + lane;
+  int pf = 0, pi = 0, tf = 0, ti = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    const int a = s_rpf[w][lane], bi = INNER ? s_rpi[w][lane] : 0;
+    pf += w < wv ? a : 0;
+    pi += w < wv ? bi : 0;
+    tf += a;
+    ti += bi;
+  }
+  unsigned short *const of = snbr + (size_t)row * sstride;
+  unsigned short *const oi = INNER ? snbi + (size_t)row * sstride : nullptr;
+  for (int c = c0; c < c1; c++) {
+    unsigned lo = (unsigned)s_bm[c][lane], hi = (unsigned)(s_bm[c][lane] >> 32);
+    unsigned long long in = INNER ? s_bi[c][lane] : 0ull;
+    while (lo | hi) {
+      const int bit = lo ? __ffs(lo) - 1 : 31 + __ffs(hi);
+      if (lo) lo &= lo - 1u;
+      else hi &= hi - 1u;
+      const unsigned short qv = s_q[c][bit];
+      if (pf < sstride) of[blk_tpos<G, U>(pf)] = qv;
+      pf++;
+      if (INNER && ((in >> bit) & 1ull)) {
+        if (pi < sstride) oi[blk_tpos<G, U>(pi)] = qv;
+        pi++;
+      }
+    }
+  }
+  if (wv == NW - 1) {  // the last wave pads the tails with the sentinel and stores the counts
+    rcnt[row] = tf;
+    if (tf > sstride) atomicMax(ovf, 1 << 21);
+    for (int k = tf, e = min((tf + U * G - 1) / (U * G) * (U * G), sstride); k < e; k++)
+      of[blk_tpos<G, U>(k)] = 0;
+    if (INNER) {
+      icnt[row] = ti;
+      for (int k = ti, e = min((ti + U * G - 1) / (U * G) * (U * G), sstride); k < e; k++)
+        oi[blk_tpos<G, U>(k)] = 0;
+    }
+  }
 }
 
 // A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.
@@ -874,6 +1216,44 @@ inline void blk_neigh(int shape, bool big, bool nt1, hipStream_t s, int n, const
     else                                                                                  \
       blk_neigh_t<R, G, U, BLK_MCAP>(nt1, s, n, q, dim, xf, ty, xb, tb, qbeg, xpos, cf,   \
                                      ucap, sstride, ulist, ucnt, rcnt, snbr, ovf, umax, cq, bexp); \
+    break;
+    SPH_BLK_SHAPES(SPH_CASE)
+#undef SPH_CASE
+  }
+}
+
+// k_blk_build (the default block build; k_blk_neigh remains the large-image fallback)
+template <int R, int G, int U, bool NT1, bool INNER>
+inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const double4 *xf,
+                        const int *ty, const double4 *xb, const int *tb, const int *qbeg,
+                        const Coefs *cf, int ucap, int sstride, int *ulist, int *ucnt,
+                        int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
+                        int *ovf, int *umax, int cq) {
+  hipLaunchKernelGGL((k_blk_build<R, G, U, NT1, INNER>), dim3(blk_blocks(n, R)), dim3(256), 0,
+                     s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt, rcnt,
+                     snbr, icnt, snbi, ovf, umax, cq);
+}
+inline void blk_build(int shape, bool nt1, bool inner, hipStream_t s, int n, const QBins &q,
+                      int dim, const double4 *xf, const int *ty, const double4 *xb,
+                      const int *tb, const int *qbeg, const Coefs *cf, int ucap, int sstride,
+                      int *ulist, int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
+                      unsigned short *snbi, int *ovf, int *umax, int cq) {
+  switch (shape) {
+#define SPH_CASE(k, R, G, U)                                                                \
+  case k:                                                                                 \
+    if (nt1 && inner)                                                                     \
+      blk_build_t<R, G, U, true, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
+                                       ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+    else if (nt1)                                                                         \
+      blk_build_t<R, G, U, true, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
+                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+    else if (inner)                                                                       \
+      blk_build_t<R, G, U, false, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
+                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+    else                                                                                  \
+      blk_build_t<R, G, U, false, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,     \
+                                         sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, \
+                                         umax, cq);                                       \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE

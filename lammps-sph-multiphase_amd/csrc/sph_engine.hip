@@ -245,7 +245,7 @@ struct sph_engine {
   DBuf<int> icnt, moved;
   DBuf<double4> x0;
   double inner_margin = 0.0;
-  bool inner = false;
+  bool inner = false, inner_written = false;  // (written: by k_blk_build, with the full rows)
   DBuf<int> nbs;  // fixed-stride scratch rows of a CSR build (list_q)
   DBuf<int> mx, ccnt;  // scratch scalars; full-list row counts of the current build
   DBuf<long long> blen;
@@ -1163,9 +1163,23 @@ struct sph_engine {
       ulist.reserve((size_t)nb * BLK_UCAP);
       ucnt.reserve(nb);
       SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
-      blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
-                dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
-                blk_cq(), study_int("SPH_BEXP", 0));
+      // k_blk_build (ballots, inner rows in the same pass); the bitmap walk k_blk_neigh for
+      // the large candidate image (and in study builds, SPH_BUILD=0)
+      const bool v2 = !big && study_int("SPH_BUILD", 1) != 0;
+      const bool want_inner = inner_margin > 0.0 && !multi();
+      if (v2 && want_inner) {
+        snbi.reserve((size_t)n * blk_sstride + 2 * chunk);
+        icnt.reserve(n);
+      }
+      if (v2)
+        blk_build(shape, nt1(), want_inner, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p,
+                  dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, icnt.p, snbi.p,
+                  mx.p, mx.p + 1, blk_cq());
+      else
+        blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
+                  dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
+                  blk_cq(), study_int("SPH_BEXP", 0));
+      inner_written = v2 && want_inner;
       int hm[5];
       SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
@@ -1275,8 +1289,10 @@ struct sph_engine {
     icnt.reserve(nlocal);
     moved.reserve(1);
     x0.reserve(nlocal);
-    BlkArgs k = blk_args();
-    blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
+    if (!inner_written) {
+      BlkArgs k = blk_args();
+      blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
+    }
     SPH_HIP_TRY(hipMemcpyAsync(x0.p, xf.p, (size_t)nlocal * sizeof(double4),
                                hipMemcpyDeviceToDevice, s));
     SPH_HIP_TRY(hipMemsetAsync(moved.p, 0, sizeof(int), s));

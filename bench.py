@@ -367,8 +367,9 @@ def c3_main(args, sph):
                    "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                    "n_half_per_particle": n_half, "parallelism": "single GPU"},
         "roofline": {"bound": "hbm",
-                     "kernel": "k_row2_force<MORRIS, TAIT|HEAT> (taitwater/morris + "
-                               "heatconduction, one fused pass)",
+                     "kernel": ("k_blk_force" if st["staged"] == 1 else "k_row2_force")
+                               + "<MORRIS, TAIT|HEAT> (taitwater/morris + heatconduction, "
+                               "one fused pass)",
                      "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": ach / PEAK_HBM_GBS, "traffic": None,
                      "bytes_per_particle": bytes_pass, "ms_per_launch": ms_pass},

@@ -16,7 +16,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsph_hip.so")
+# (SPH_HIP_LIB: another build of the same library, e.g. the study build of `make STUDY=1`)
+LIB_PATH = os.environ.get("SPH_HIP_LIB") or os.path.join(HERE, "libsph_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "sph_hip.h")
 
 SPH_LIST_FULL, SPH_LIST_HALF = 0, 1

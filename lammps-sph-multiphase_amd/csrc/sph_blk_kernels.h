@@ -65,12 +65,12 @@ __device__ __forceinline__ int blk_scan(int v, int *s_w, int *total) {
   return base + x - v;
 }
 
-// Chunk-transposed slot rows: entry u*G + l of a U*G-entry chunk (taken by lane l of the
-// row's G lanes) is stored at U*l + u, so a lane's U slots of a chunk are one load.
+// Slot rows are plain arrays: lane l of the row's G lanes takes entries U*l .. U*l + U-1 of
+// each U*G-entry chunk (one load), so a row written in entry order is written contiguously
+// (k_blk_build's coalesced stores).  (Kept as a function for the older writers.)
 template <int G, int U>
 __host__ __device__ __forceinline__ int blk_tpos(int q) {
-  const unsigned uq = (unsigned)q, c = uq % (U * G);  // (unsigned: masks and shifts)
-  return (int)(uq - c + U * (c % G) + c / G);
+  return q;
 }
 
 // v_writelane_b32 through its LLVM intrinsic (no clang builtin here; the compiler then
@@ -434,7 +434,16 @@ template <int N, class F>
 __device__ __forceinline__ void blk_rows(F &&f) {
   blk_rows_<N>(f, std::make_integer_sequence<int, N>{});
 }
-template <int R, int G, int U, bool NT1, bool INNER>
+// a wave-uniform 64-bit value into scalar registers
+__device__ __forceinline__ unsigned long long blk_uniform64(unsigned long long x) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)x);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(x >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+// BEXP (study builds, SPH_BEXP with the build v2): 1 = return after the bin table, 2 = after
+// the candidates, 3 = no emit (rows not written), 4 = no tests (every word 0).  Outputs
+// meaningless.
+template <int R, int G, int U, bool NT1, bool INNER, int BEXP = 0>
 __global__ void __launch_bounds__(256)
 k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             const int *__restrict__ ty, const double4 *__restrict__ xb,
@@ -443,14 +452,17 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             int *__restrict__ ucnt, int *__restrict__ rcnt, unsigned short *__restrict__ snbr,
             int *__restrict__ icnt, unsigned short *__restrict__ snbi,
             int *__restrict__ ovf, int *__restrict__ umax, int cq) {
-  static_assert(R <= 64 && R % 8 == 0, "one lane per row, rows in steps of 8");
   constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
-  constexpr int TPR = NT / R;
-  __shared__ unsigned long long s_bm[SCH][R];
-  __shared__ unsigned long long s_bi[INNER ? SCH : 1][R];
+  constexpr int RPW = R / NW, UG = U * G, WS = INNER ? 2 : 1;
+  static_assert(R <= 64 && R % 32 == 0, "one lane per row, rows in steps of 8 per wave");
+  static_assert(UG <= 64, "a row's padding in one store");
+  // the rows' hit words per chunk (full, inner); before the tests the same storage holds
+  // the raw candidates' bin-row numbers
+  __shared__ __attribute__((aligned(16))) unsigned long long s_w[SCH * R * WS];
+  static_assert(SCH * R * WS * 8 >= BLK_MCAP, "the bin-row table fits the hit words");
+  unsigned char *const s_rowof = reinterpret_cast<unsigned char *>(s_w);
   __shared__ unsigned long long s_used[SCH];
   __shared__ unsigned short s_q[SCH][64];
-  __shared__ int s_rpf[NW][64], s_rpi[INNER ? NW : 1][64];
   __shared__ unsigned long long s_keep[MCH];
   __shared__ int s_cpos[BLK_SCAP];
   __shared__ int s_upre[SCH + 1], s_kpre[MCH + 1];
@@ -460,8 +472,9 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   __shared__ int s_self[NW][64];
   __shared__ double s_bb[6];
   __shared__ double s_cns[NT1 ? 1 : NT2], s_cin[(NT1 || !INNER) ? 1 : NT2];
-  __shared__ int s_w[NW];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ int s_sc[NW];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, 
+            wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar)
   const int row0 = b * R;
   const int nrow = min(R, n - row0);
   const int nt1 = cf->ntypes + 1;
@@ -533,7 +546,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     }
   }
   int M = 0;
-  const int pre = blk_scan<NT>(len, s_w, &M);
+  const int pre = blk_scan<NT>(len, s_sc, &M);
   if (M > BLK_MCAP) {
     if (tid == 0) atomicMax(ovf, M);
     return;
@@ -542,39 +555,42 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   if (tid < ntab) {
     s_pre[tid] = pre;
     s_st[tid] = st;
+    for (int k = 0; k < len; k++) s_rowof[pre + k] = (unsigned char)tid;
   }
   __syncthreads();
+  if (BEXP == 1) return;
   const int mch = (M + 63) >> 6;
-  // raw candidate p -> its xb position (last bin-row with s_pre <= p)
+  // raw candidate p -> its xb position
   auto rpos = [&](int p) {
-    int lo = 0, hi = ntab - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_pre[mid] <= p) lo = mid;
-      else hi = mid - 1;
-    }
-    return s_st[lo] + (p - s_pre[lo]);
+    const int t = s_rowof[p];
+    return s_st[t] + (p - s_pre[t]);
   };
-  // 2) prefilter: distance to the box <= cutneighmax (conservative margins)
+  // 2) prefilter: distance to the box <= cutneighmax (conservative margins); two chunks per
+  // step, so that their loads overlap
   const double cmsq = q.cutmaxsq * (1.0 + 1e-9) + 1e-12 * q.size[0] * q.size[0];
-  for (int c = wv; c < mch; c += NW) {
-    const int p = c * 64 + lane;
-    bool keep = false;
-    if (p < M) {
-      const double4 x = xb[rpos(p)];
-      const double gx = fmax(fmax(s_bb[0] - x.x, x.x - s_bb[3]), 0.0);
-      const double gy = fmax(fmax(s_bb[1] - x.y, x.y - s_bb[4]), 0.0);
-      const double gz = fmax(fmax(s_bb[2] - x.z, x.z - s_bb[5]), 0.0);
-      keep = gx * gx + gy * gy + gz * gz <= cmsq;
+  auto near = [&](const double4 &x) {
+    const double gx = fmax(fmax(s_bb[0] - x.x, x.x - s_bb[3]), 0.0);
+    const double gy = fmax(fmax(s_bb[1] - x.y, x.y - s_bb[4]), 0.0);
+    const double gz = fmax(fmax(s_bb[2] - x.z, x.z - s_bb[5]), 0.0);
+    return gx * gx + gy * gy + gz * gz <= cmsq;
+  };
+  for (int c = wv; c < mch; c += 2 * NW) {
+    const int p = c * 64 + lane, p2 = p + NW * 64;
+    double4 x = make_double4(0.0, 0.0, 0.0, 0.0), x2 = x;
+    if (p < M) x = xb[rpos(p)];
+    if (p2 < M) x2 = xb[rpos(p2)];
+    const unsigned long long k = __ballot(p < M && near(x));
+    const unsigned long long k2 = __ballot(p2 < M && near(x2));
+    if (lane == 0) {
+      s_keep[c] = k;
+      if (c + NW < mch) s_keep[c + NW] = k2;
     }
-    const unsigned long long k = __ballot(keep);
-    if (lane == 0) s_keep[c] = k;
   }
   __syncthreads();
   int K = 0;
   {
     const int v = tid < mch ? __popcll(s_keep[tid]) : 0;
-    const int ex = blk_scan<NT>(v, s_w, &K);
+    const int ex = blk_scan<NT>(v, s_sc, &K);
     if (tid < mch) s_kpre[tid] = ex;
   }
   if (K > BLK_SCAP) {  // workgroup-uniform
@@ -588,21 +604,33 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
       s_cpos[s_kpre[c] + __popcll(k & ((1ull << lane) - 1ull))] = rpos(c * 64 + lane);
   }
   __syncthreads();
+  if (BEXP == 2) return;
   const int nch = (K + 63) >> 6;
-  // 3) tests: chunk c of 64 kept candidates (one per lane) against every row
+  // 3) tests: chunk c of 64 kept candidates (one per lane) against every row; the next
+  // chunk's candidates are loaded while this one is tested
   const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
   const double cin1 = (NT1 && INNER) ? cf->cutinsq[3] : 0.0;
+  auto cload = [&](int c, double4 &x, int &t) {
+    const int p = c * 64 + lane;
+    x = make_double4(-1e300, -1e300, -1e300, -1.0);
+    t = 1;
+    if (p < K) {
+      const int pos = s_cpos[p];
+      x = xb[pos];
+      if (!NT1) t = tb[pos];
+    }
+  };
+  double4 xn;
+  int tn = 1;
+  if (wv < nch) cload(wv, xn, tn);
   for (int c = wv; c < nch; c += NW) {
     const int p = c * 64 + lane;
     const bool valid = p < K;
-    double4 xc = make_double4(-1e300, -1e300, -1e300, -1.0);
-    int tc = 1;
-    if (valid) {
-      const int pos = s_cpos[p];
-      xc = xb[pos];
-      if (!NT1) tc = tb[pos];
-    }
+    const double4 xc = xn;
+    const int tc = tn;
+    if (c + NW < nch) cload(c + NW, xn, tn);
     const int cid = valid ? (int)xc.w : -1;
+    if (valid) s_cpos[p] = cid;  // (the xb position is spent: the union takes the atom id)
     // j != i: the lane holding row r's own atom (if this chunk has it), for lane r
     s_self[wv][lane] = -1;
     if (cid >= row0 && cid < row0 + R) s_self[wv][cid - row0] = lane;
@@ -612,7 +640,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     int ro = 0;
     asm volatile("" : "+s"(ro));
     // every row, fully unrolled (lane r keeps row r's 64-bit word)
-    blk_rows<R>([&](auto rc) {
+    if (BEXP != 4) blk_rows<R>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       const double4 xi = s_row[r + ro];
       const double rsq = rsq_ref(xi.x - xc.x, xi.y - xc.y, xi.z - xc.z);
@@ -636,8 +664,11 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     const unsigned long long keep = ~((unsigned long long)(self >= 0) << (self & 63));
     const unsigned long long mine = (((unsigned long long)my_hi << 32) | my_lo) & keep;
     if (lane < R) {
-      s_bm[c][lane] = mine;
-      if (INNER) s_bi[c][lane] = (((unsigned long long)mi_hi << 32) | mi_lo) & keep;
+      if (INNER)
+        reinterpret_cast<ulonglong2 *>(s_w)[c * R + lane] =
+            make_ulonglong2(mine, (((unsigned long long)mi_hi << 32) | mi_lo) & keep);
+      else
+        s_w[c * R + lane] = mine;
     }
     unsigned long long u = mine;
 #pragma unroll
@@ -649,7 +680,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   int u = 0;
   {
     const int v = tid < nch ? __popcll(s_used[tid]) : 0;
-    const int ex = blk_scan<NT>(v, s_w, &u);
+    const int ex = blk_scan<NT>(v, s_sc, &u);
     if (tid < nch) s_upre[tid] = ex;
   }
   __syncthreads();
@@ -659,8 +690,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     const unsigned long long used = s_used[c];
     const int below = blk_mbcnt(used);
     s_q[c][lane] = (unsigned short)blk_q(s_upre[c] + 1 + below, cq);
-    if ((used >> lane) & 1ull)
-      ulist[(size_t)b * ucap + s_upre[c] + below] = (int)xb[s_cpos[c * 64 + lane]].w;
+    if ((used >> lane) & 1ull) ulist[(size_t)b * ucap + s_upre[c] + below] = s_cpos[c * 64 + lane];
   }
   if (tid == 0) {
     ucnt[b] = u;
@@ -670,64 +700,67 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     atomicAdd(umax + 3, u);
   }
   __syncthreads();
-  // 5) the slot rows, full and inner: lane r of every wave is row r; wave w takes a
-  // contiguous quarter of the chunks, starting at the row's hits in the chunks before it.
-  // Each lane walks its row's set bits (a full-list hit; the inner bit is a subset) and
-  // writes the slot word to the full row and, if inner, to the inner row: one useful store
-  // per lane per step, ascending slot order.
-  const int cpw = (nch + NW - 1) / NW;
-  const int c0 = min(wv * cpw, nch), c1 = min(c0 + cpw, nch);
-  int nf = 0, ni = 0;
-  if (lane < R)
-    for (int c = c0; c < c1; c++) {
-      nf += __popcll(s_bm[c][lane]);
-      if (INNER) ni += __popcll(s_bi[c][lane]);
-    }
-  if (lane < R) {
-    s_rpf[wv][lane] = nf;
-    if (INNER) s_rpi[wv][lane] = ni;
-  }
-  __syncthreads();
-  if (lane >= nrow) return;
-  const int row = row0 + lane;
-  int pf = 0, pi = 0, tf = 0, ti = 0;
+  if (BEXP == 3) return;
+  // 5) the slot rows, full and inner: wave w writes rows w*RPW .. w*RPW + RPW-1, one chunk
+  // at a time -- lane l stores candidate l's slot word if it is a hit of the row, at the
+  // row's running count + the hits below it: ascending slots, each store one contiguous
+  // piece of the row (the rows' offsets and counts are wave-uniform, in scalar registers)
+  const int r0 = wv * RPW;
+  int pf[RPW], pi[RPW];
 #pragma unroll
-  for (int w = 0; w < NW; w++) {
-    const int a = s_rpf[w][lane], bi = INNER ? s_rpi[w][lane] : 0;
-    pf += w < wv ? a : 0;
-    pi += w < wv ? bi : 0;
-    tf += a;
-    ti += bi;
-  }
-  unsigned short *const of = snbr + (size_t)row * sstride;
-  unsigned short *const oi = INNER ? snbi + (size_t)row * sstride : nullptr;
-  for (int c = c0; c < c1; c++) {
-    unsigned lo = (unsigned)s_bm[c][lane], hi = (unsigned)(s_bm[c][lane] >> 32);
-    unsigned long long in = INNER ? s_bi[c][lane] : 0ull;
-    while (lo | hi) {
-      const int bit = lo ? __ffs(lo) - 1 : 31 + __ffs(hi);
-      if (lo) lo &= lo - 1u;
-      else hi &= hi - 1u;
-      const unsigned short qv = s_q[c][bit];
-      if (pf < sstride) of[blk_tpos<G, U>(pf)] = qv;
-      pf++;
-      if (INNER && ((in >> bit) & 1ull)) {
-        if (pi < sstride) oi[blk_tpos<G, U>(pi)] = qv;
-        pi++;
+  for (int i = 0; i < RPW; i++) pf[i] = pi[i] = 0;
+  for (int c = 0; c < nch; c++) {
+    const unsigned short qv = s_q[c][lane];
+    blk_rows<RPW>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int r = r0 + i;
+      if (r >= nrow) return;  // (wave-uniform)
+      unsigned long long wf, wi = 0ull;
+      if (INNER) {
+        const ulonglong2 w2 = reinterpret_cast<const ulonglong2 *>(s_w)[c * R + r];
+        wf = blk_uniform64(w2.x);
+        wi = blk_uniform64(w2.y);
+      } else {
+        wf = blk_uniform64(s_w[c * R + r]);
       }
-    }
+      const size_t rb = (size_t)(row0 + r) * sstride;
+      if ((wf >> lane) & 1ull) {
+        const int k = pf[i] + blk_mbcnt(wf);
+        if (k < sstride) snbr[rb + k] = qv;
+      }
+      pf[i] += __popcll(wf);
+      if (INNER) {
+        if ((wi >> lane) & 1ull) {
+          const int k = pi[i] + blk_mbcnt(wi);
+          if (k < sstride) snbi[rb + k] = qv;
+        }
+        pi[i] += __popcll(wi);
+      }
+    });
   }
-  if (wv == NW - 1) {  // the last wave pads the tails with the sentinel and stores the counts
-    rcnt[row] = tf;
-    if (tf > sstride) atomicMax(ovf, 1 << 21);
-    for (int k = tf, e = min((tf + U * G - 1) / (U * G) * (U * G), sstride); k < e; k++)
-      of[blk_tpos<G, U>(k)] = 0;
+  // the tails up to whole chunks hold the sentinel; the counts (lane i: row r0 + i)
+  unsigned cf_v = 0u, ci_v = 0u;
+  bool over = false;
+  blk_rows<RPW>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int r = r0 + i;
+    if (r >= nrow) return;
+    const size_t rb = (size_t)(row0 + r) * sstride;
+    const int ef = min((pf[i] + UG - 1) / UG * UG, sstride);
+    if (pf[i] + lane < ef) snbr[rb + pf[i] + lane] = 0;
+    cf_v = writelane<i>(cf_v, (unsigned)pf[i]);
+    over |= pf[i] > sstride;
     if (INNER) {
-      icnt[row] = ti;
-      for (int k = ti, e = min((ti + U * G - 1) / (U * G) * (U * G), sstride); k < e; k++)
-        oi[blk_tpos<G, U>(k)] = 0;
+      const int ei = min((pi[i] + UG - 1) / UG * UG, sstride);
+      if (pi[i] + lane < ei) snbi[rb + pi[i] + lane] = 0;
+      ci_v = writelane<i>(ci_v, (unsigned)pi[i]);
     }
+  });
+  if (lane < RPW && r0 + lane < nrow) {
+    rcnt[row0 + r0 + lane] = (int)cf_v;
+    if (INNER) icnt[row0 + r0 + lane] = (int)ci_v;
   }
+  if (over && lane == 0) atomicMax(ovf, 1 << 21);
 }
 
 // A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.
@@ -746,8 +779,7 @@ struct SlotWord<4> {
   }
 };
 
-// A row's c slots (chunk-transposed, blk_tpos) for the row's G lanes, U slots per lane per
-// chunk.  load() issues the lane's slot-word loads -- before the block's staging, so their
+// A row's c slots for the row's G lanes, U consecutive slots per lane per chunk.  load() issues the lane's slot-word loads -- before the block's staging, so their
 // latency overlaps it; walk() calls body(slot, in) for every slot position of the lane
 // (in = position < c; padded positions hold the sentinel slot).  NCH > 0: all of the
 // row's chunks (at most NCH, the host guarantees c <= NCH*U*G) are held in registers;
@@ -776,7 +808,7 @@ struct BlkSlots {
         if (k * U * G >= c) break;
 #pragma unroll
         for (int q = 0; q < U; q++)
-          body(SlotWord<U>::get(w[k], q), k * U * G + q * G + lane < c);
+          body(SlotWord<U>::get(w[k], q), k * U * G + U * lane + q < c);
       }
     } else {
       SW wn = w[0];
@@ -784,7 +816,7 @@ struct BlkSlots {
         const SW cur = wn;
         wn = *reinterpret_cast<const SW *>(sl + k0 + U * G + U * lane);
 #pragma unroll
-        for (int q = 0; q < U; q++) body(SlotWord<U>::get(cur, q), k0 + q * G + lane < c);
+        for (int q = 0; q < U; q++) body(SlotWord<U>::get(cur, q), k0 + U * lane + q < c);
       }
     }
   }
@@ -1143,6 +1175,19 @@ static __global__ void k_blk_large(int nb, const int *__restrict__ ucnt, int um,
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < nb && ucnt[b] > um) blist[atomicAdd(nbig, 1)] = b;
 }
+// k_blk_large right behind the build, without a host round trip: the force pass's image
+// size umf from the build's statistics words (mx[1] = largest union, mx[4] = sum of the
+// unions: ~1.25x the mean, whole 64-record steps, or `fixed` if > 0) into mx[6], the blocks
+// above it into blist (count mx[5])
+static __global__ void k_blk_large_dev(int nb, const int *__restrict__ ucnt, int fixed,
+                                       int *__restrict__ mx, int *__restrict__ blist) {
+  const int um = max(mx[1], 1);
+  int umf = min(um, ((int)(1.25 * ((double)mx[4] / nb)) + 63) / 64 * 64);
+  if (fixed > 0) umf = min(um, fixed);
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b == 0) mx[6] = umf;
+  if (b < nb && umf < um && ucnt[b] > umf) blist[atomicAdd(mx + 5, 1)] = b;
+}
 
 // ---- host-side launch helpers ----------------------------------------------------------
 // Block shapes (rows per block R, lanes per row G, slots per lane and chunk U); SPH_BLK
@@ -1228,32 +1273,41 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
                         const int *ty, const double4 *xb, const int *tb, const int *qbeg,
                         const Coefs *cf, int ucap, int sstride, int *ulist, int *ucnt,
                         int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
-                        int *ovf, int *umax, int cq) {
-  hipLaunchKernelGGL((k_blk_build<R, G, U, NT1, INNER>), dim3(blk_blocks(n, R)), dim3(256), 0,
-                     s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, ulist, ucnt, rcnt,
-                     snbr, icnt, snbi, ovf, umax, cq);
+                        int *ovf, int *umax, int cq, int bexp) {
+#ifdef SPH_STUDY
+  auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, 1>
+          : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, 2>
+          : bexp == 3 ? k_blk_build<R, G, U, NT1, INNER, 3>
+          : bexp == 4 ? k_blk_build<R, G, U, NT1, INNER, 4>
+                      : k_blk_build<R, G, U, NT1, INNER, 0>;
+#else
+  (void)bexp;
+  auto fn = k_blk_build<R, G, U, NT1, INNER, 0>;
+#endif
+  hipLaunchKernelGGL(fn, dim3(blk_blocks(n, R)), dim3(256), 0, s, n, q, dim, xf, ty, xb, tb,
+                     qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq);
 }
 inline void blk_build(int shape, bool nt1, bool inner, hipStream_t s, int n, const QBins &q,
                       int dim, const double4 *xf, const int *ty, const double4 *xb,
                       const int *tb, const int *qbeg, const Coefs *cf, int ucap, int sstride,
                       int *ulist, int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
-                      unsigned short *snbi, int *ovf, int *umax, int cq) {
+                      unsigned short *snbi, int *ovf, int *umax, int cq, int bexp) {
   switch (shape) {
 #define SPH_CASE(k, R, G, U)                                                                \
   case k:                                                                                 \
     if (nt1 && inner)                                                                     \
       blk_build_t<R, G, U, true, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                       ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+                                       ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
     else if (nt1)                                                                         \
       blk_build_t<R, G, U, true, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
     else if (inner)                                                                       \
       blk_build_t<R, G, U, false, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq); \
+                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
     else                                                                                  \
       blk_build_t<R, G, U, false, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,     \
                                          sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, \
-                                         umax, cq);                                       \
+                                         umax, cq, bexp);                                 \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE

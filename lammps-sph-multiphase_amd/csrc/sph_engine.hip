@@ -142,6 +142,8 @@ struct sph_engine {
   // fix phase_change scratch, kept across calls (no allocation per step)
   DBuf<int> pc_flag, pc_cand, pc_otag, pc_idx, pc_minr, pc_one, pc_grank, pc_key, pc_val, gsrc;
   std::vector<int> gswap_first;  // one brick: first ghost of each swap (+ nghost at the end)
+  int gcap_hint = 0;              // one brick: ghost room of the next borders
+  DBuf<int> gnall;                // one brick: nall before each swap (+ the overflow word)
   DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec;
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
@@ -253,6 +255,7 @@ struct sph_engine {
   DBuf<unsigned char> tmp;
   // pinned host scalar
   int *h_scalar = nullptr;
+  int *h_small = nullptr;  // pinned: a few device words read back together (borders)
 
   // timing
   bool timing = false;
@@ -886,59 +889,90 @@ struct sph_engine {
     de.reserve(nlocal > 0 ? nlocal : 1, true, s);
   }
 
+  // One brick: CommBrick::borders' self swaps (comm_brick.cpp:696-864) with every count kept
+  // on the device -- each swap's selection size, and where its ghosts go, is read by the next
+  // kernels from device words (gnall), so the swaps run back to back with ONE host read at
+  // the end.  The ghost arrays are sized ahead from the last borders' ghost count (or the
+  // box geometry); a borders that would outgrow them is redone with twice the room.
   void borders() {
     if (multi()) {
       borders_multi();
       return;
     }
-    nghost = 0;
-    int nall = nlocal;
     const int ndim = cfg.dim;
-    nsel.reserve(1);
-    gswap_first.clear();
-    for (int d = 0; d < ndim; d++) {
-      if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
-      const int nlast = nall;
-      for (int ineed = 0; ineed < 2; ineed++) {
-        double lo, hi, shift;
-        int pbc;
-        if (ineed == 0) {
-          lo = -1.0e20;
-          hi = sublo[d] + cutghost;
-          pbc = 1;
-        } else {
-          lo = subhi[d] - cutghost;
-          hi = 1.0e20;
-          pbc = -1;
-        }
-        shift = pbc * box.prd[d];
-        flags.reserve(nlast);
-        sel.reserve(nlast);
-        hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d, lo, hi, xf.p, flags.p);
-        hipcub::CountingInputIterator<int> it(0);
-        size_t tb = 0;
-        SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flags.p, sel.p, nsel.p, nlast, s));
-        tmp_reserve(tb);
-        SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flags.p, sel.p, nsel.p, nlast, s));
-        const int ns = read_scalar(nsel.p);
-        gswap_first.push_back(nall - nlocal);
-        if (ns == 0) continue;
-        ensure_atoms((size_t)nall + ns, true);
-        gowner.reserve((size_t)nall + ns - nlocal, true, s);
-        gimg.reserve((size_t)nall + ns - nlocal, true, s);
-        if (pc) {  // the swap's sendlist (each ghost's source), for LAMMPS' ghost slot order
-          gsrc.reserve((size_t)nall + ns - nlocal, true, s);
-          SPH_HIP_TRY(hipMemcpyAsync(gsrc.p + (nall - nlocal), sel.p, ns * sizeof(int),
-                                     hipMemcpyDeviceToDevice, s));
-        }
-        hipLaunchKernelGGL(k_append_ghosts, dim3(blocks(ns)), dim3(BLK), 0, s, ns, sel.p,
-                           nlocal, nall, d, pbc, shift, xf.p, vr.p, en.p, ty.p, gowner.p, gimg.p);
-        mpx_copy(ns, sel.p, nall, xbuf);
-        nall += ns;
+    int nsw = 0;
+    for (int d = 0; d < ndim; d++)
+      if (cfg.periodic[d]) nsw += 2;
+    if (gcap_hint <= 0) {  // the ghost shell's share of the sub-box, with room
+      double in = 1.0, out = 1.0;
+      for (int d = 0; d < ndim; d++) {
+        const double ext = std::max(subhi[d] - sublo[d], 1e-300);
+        in *= ext;
+        out *= ext + (cfg.periodic[d] ? 2.0 * cutghost : 0.0);
       }
+      gcap_hint = (int)std::min(1.5 * (out / in - 1.0) * nlocal + 4096.0, 2.0e9 - nlocal);
     }
-    nghost = nall - nlocal;
-    gswap_first.push_back(nghost);
+    gnall.reserve(nsw + 2);
+    nsel.reserve(nsw + 1);
+    for (;;) {
+      const int gcap = gcap_hint, cap = nlocal + gcap;
+      ensure_atoms((size_t)cap, true);
+      gowner.reserve(gcap, true, s);
+      gimg.reserve(gcap, true, s);
+      if (pc) gsrc.reserve(gcap, true, s);
+      flags.reserve(cap);
+      sel.reserve(cap);
+      h_small[14] = nlocal;  // (pinned; the read-back below lands in words 0 .. nsw + 1)
+      h_small[15] = 0;       // the overflow word
+      SPH_HIP_TRY(hipMemcpyAsync(gnall.p, h_small + 14, sizeof(int), hipMemcpyHostToDevice, s));
+      SPH_HIP_TRY(hipMemcpyAsync(gnall.p + nsw + 1, h_small + 15, sizeof(int),
+                                 hipMemcpyHostToDevice, s));
+      int w = 0;
+      for (int d = 0; d < ndim; d++) {
+        if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
+        const int *const nlast = gnall.p + w;  // both swaps scan the atoms before this dim
+        for (int ineed = 0; ineed < 2; ineed++, w++) {
+          double lo, hi;
+          int pbc;
+          if (ineed == 0) {
+            lo = -1.0e20;
+            hi = sublo[d] + cutghost;
+            pbc = 1;
+          } else {
+            lo = subhi[d] - cutghost;
+            hi = 1.0e20;
+            pbc = -1;
+          }
+          const double shift = pbc * box.prd[d];
+          hipLaunchKernelGGL(k_slab_flags_dev, dim3(blocks(cap)), dim3(BLK), 0, s, cap, nlast,
+                             d, lo, hi, xf.p, flags.p);
+          hipcub::CountingInputIterator<int> it(0);
+          size_t tb = 0;
+          SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flags.p, sel.p, nsel.p + w,
+                                                    cap, s));
+          tmp_reserve(tb);
+          SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flags.p, sel.p, nsel.p + w,
+                                                    cap, s));
+          hipLaunchKernelGGL(k_append_ghosts_dev, dim3(blocks(gcap)), dim3(BLK), 0, s, gcap,
+                             nsel.p + w, sel.p, nlocal, gnall.p + w, cap, d, pbc, shift, xf.p,
+                             vr.p, en.p, ty.p, gowner.p, gimg.p, pc ? gsrc.p : (int *)nullptr,
+                             mp ? vel.p : (double4 *)nullptr, mp ? rm.p : (double *)nullptr,
+                             mp ? cvv.p : (double *)nullptr, mp ? cg.p : (double4 *)nullptr,
+                             gnall.p + nsw + 1);
+        }
+      }
+      SPH_HIP_TRY(hipMemcpyAsync(h_small, gnall.p, (nsw + 2) * sizeof(int),
+                                 hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipStreamSynchronize(s));
+      if (h_small[nsw + 1] == 0) break;
+      SPH_REQUIRE(gcap < 1000000000, SPH_HIP_EOVERFLOW, "ghost count exceeds 2^30");
+      gcap_hint = 2 * gcap;
+    }
+    gswap_first.clear();
+    for (int w = 0; w <= nsw; w++) gswap_first.push_back(h_small[w] - nlocal);
+    nghost = h_small[nsw] - nlocal;
+    // next time: this count with room (atoms drift between rebuilds)
+    gcap_hint = std::max(gcap_hint, nghost + nghost / 8 + 4096);
   }
 
   // LAMMPS' index order of this brick's ghosts (one process): CommBrick::borders appends each
@@ -1162,7 +1196,7 @@ struct sph_engine {
       const int nb = blk_blocks(n, sh.R);
       ulist.reserve((size_t)nb * BLK_UCAP);
       ucnt.reserve(nb);
-      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 5 * sizeof(int), s));
+      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 7 * sizeof(int), s));
       // k_blk_build (ballots, inner rows in the same pass); the bitmap walk k_blk_neigh for
       // the large candidate image (and in study builds, SPH_BUILD=0)
       const bool v2 = !big && study_int("SPH_BUILD", 1) != 0;
@@ -1174,14 +1208,18 @@ struct sph_engine {
       if (v2)
         blk_build(shape, nt1(), want_inner, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p,
                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, icnt.p, snbi.p,
-                  mx.p, mx.p + 1, blk_cq());
+                  mx.p, mx.p + 1, blk_cq(), study_int("SPH_BEXP", 0));
       else
         blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
                   blk_cq(), study_int("SPH_BEXP", 0));
       inner_written = v2 && want_inner;
-      int hm[5];
-      SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 5 * sizeof(int), hipMemcpyDeviceToHost, s));
+      // the force pass's image size and its large-union blocks, then ONE read-back
+      bl.reserve(nb);
+      hipLaunchKernelGGL(k_blk_large_dev, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p,
+                         env_int("SPH_BLKUMF", 0), mx.p, bl.p);
+      int *const hm = h_small;
+      SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
       if (env_int("SPH_DEBUG", 0))
         fprintf(stderr,
@@ -1202,18 +1240,9 @@ struct sph_engine {
       blk_sh = shape;
       blk_um = std::max(hm[1], 1);
       // the force pass's LDS image: ~1.25x the mean union (64-record steps), the blocks
-      // above it in a second launch (k_blk_large)
-      const double mean = (double)hm[4] / nb;
-      blk_umf = std::min(blk_um, ((int)(1.25 * mean) + 63) / 64 * 64);
-      if (env_int("SPH_BLKUMF", 0) > 0) blk_umf = std::min(blk_um, env_int("SPH_BLKUMF", 0));
-      blk_nbig = 0;
-      if (blk_umf < blk_um) {
-        bl.reserve(nb);
-        SPH_HIP_TRY(hipMemsetAsync(mx.p + 5, 0, sizeof(int), s));
-        hipLaunchKernelGGL(k_blk_large, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p, blk_umf,
-                           bl.p, mx.p + 5);
-        blk_nbig = read_scalar(mx.p + 5);
-      }
+      // above it in a second launch (k_blk_large_dev)
+      blk_umf = hm[6];
+      blk_nbig = hm[5];
       return 1;
     }
     return 0;
@@ -2075,6 +2104,7 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
       SPH_HIP_TRY(hipMemcpy(e->dm, &e->hm, sizeof(MpCoefs), hipMemcpyHostToDevice));
     }
     SPH_HIP_TRY(hipHostMalloc(&e->h_scalar, sizeof(int)));
+    SPH_HIP_TRY(hipHostMalloc(&e->h_small, 16 * sizeof(int)));
   } catch (...) {
     delete e;
     throw;
@@ -2120,6 +2150,7 @@ int sph_engine_destroy(sph_engine *e) {
   }
   for (auto ev : e->evpool) (void)hipEventDestroy(ev);
   if (e->h_scalar) (void)hipHostFree(e->h_scalar);
+  if (e->h_small) (void)hipHostFree(e->h_small);
   delete e->tr;
   if (e->dc) (void)hipFree(e->dc);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);

@@ -199,6 +199,21 @@ static __global__ void k_slab_flags(int n, int dim, double lo, double hi,
   flag[i] = (c >= lo && c <= hi) ? 1 : 0;
 }
 
+// k_slab_flags over [0, *n) of a launch sized for an upper bound (the count on the device)
+static __global__ void k_slab_flags_dev(int nmax, const int *__restrict__ n, int dim, double lo,
+                                        double hi, const double4 *__restrict__ xf,
+                                        unsigned char *__restrict__ flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nmax) return;
+  unsigned char f = 0;
+  if (i < *n) {
+    const double4 x = xf[i];
+    const double c = dim == 0 ? x.x : (dim == 1 ? x.y : x.z);
+    f = (c >= lo && c <= hi) ? 1 : 0;
+  }
+  flag[i] = f;
+}
+
 // image packed as 3 x 8-bit signed fields
 __host__ __device__ __forceinline__ int img_get(int img, int k) {
   return (int)(signed char)((img >> (8 * k)) & 0xff);
@@ -237,6 +252,55 @@ static __global__ void k_append_ghosts(int nsel, const int *__restrict__ sel, in
   }
   gowner[g - nlocal] = own;
   gimg[g - nlocal] = img_add(img, dim, pbc);
+}
+
+// k_append_ghosts with the swap's counts on the device (no host round trip per swap):
+// *nsel atoms sel[] appended at nall = nalls[0]; nalls[1] <- the new nall.  A swap that would
+// pass `cap` atoms appends what fits and raises *ovf (the host redoes the borders with more
+// room).  Also the swap's sendlist (gsrc, if given) and the multiphase fields (vel, rm, cv,
+// cg, if given; atom_vec_meso_multiphase.cpp pack/unpack_border).
+static __global__ void k_append_ghosts_dev(
+    int gmax, const int *__restrict__ nsel, const int *__restrict__ sel, int nlocal,
+    int *__restrict__ nalls, int cap, int dim, int pbc, double shift, double4 *__restrict__ xf,
+    double4 *__restrict__ vr, double *__restrict__ en, int *__restrict__ ty,
+    int *__restrict__ gowner, int *__restrict__ gimg, int *__restrict__ gsrc,
+    double4 *__restrict__ vel, double *__restrict__ rm, double *__restrict__ cv,
+    double4 *__restrict__ cg, int *__restrict__ ovf) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ns = *nsel, nall = nalls[0];
+  if (k == 0) {
+    nalls[1] = min(nall + ns, cap);
+    if (nall + ns > cap) *ovf = 1;
+  }
+  if (k >= gmax || k >= ns || nall + k >= cap) return;
+  const int s = sel[k];
+  const int g = nall + k;
+  double4 x = xf[s];
+  if (dim == 0) x.x = x.x + shift;
+  else if (dim == 1) x.y = x.y + shift;
+  else x.z = x.z + shift;
+  xf[g] = x;
+  vr[g] = vr[s];
+  en[g] = en[s];
+  ty[g] = ty[s];
+  int own, img;
+  if (s < nlocal) {
+    own = s;
+    img = 0;
+  } else {
+    own = gowner[s - nlocal];
+    img = gimg[s - nlocal];
+  }
+  gowner[g - nlocal] = own;
+  gimg[g - nlocal] = img_add(img, dim, pbc);
+  if (gsrc) gsrc[g - nlocal] = s;
+  if (vel) {
+    const double4 v = vel[s], c = cg[s];
+    vel[g] = make_double4(v.x, v.y, v.z, vel[g].w);
+    rm[g] = rm[s];
+    cv[g] = cv[s];
+    cg[g] = make_double4(c.x, c.y, c.z, 0.0);
+  }
 }
 
 // forward_comm (atom_vec_meso.cpp:246-288): ghost <- owner (+image*prd on x), vest, rho, e

@@ -701,66 +701,70 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   }
   __syncthreads();
   if (BEXP == 3) return;
-  // 5) the slot rows, full and inner: wave w writes rows w*RPW .. w*RPW + RPW-1, one chunk
-  // at a time -- lane l stores candidate l's slot word if it is a hit of the row, at the
-  // row's running count + the hits below it: ascending slots, each store one contiguous
-  // piece of the row (the rows' offsets and counts are wave-uniform, in scalar registers)
-  const int r0 = wv * RPW;
-  int pf[RPW], pi[RPW];
-#pragma unroll
-  for (int i = 0; i < RPW; i++) pf[i] = pi[i] = 0;
-  for (int c = 0; c < nch; c++) {
-    const unsigned short qv = s_q[c][lane];
-    blk_rows<RPW>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      const int r = r0 + i;
-      if (r >= nrow) return;  // (wave-uniform)
-      unsigned long long wf, wi = 0ull;
-      if (INNER) {
-        const ulonglong2 w2 = reinterpret_cast<const ulonglong2 *>(s_w)[c * R + r];
-        wf = blk_uniform64(w2.x);
-        wi = blk_uniform64(w2.y);
-      } else {
-        wf = blk_uniform64(s_w[c * R + r]);
-      }
-      const size_t rb = (size_t)(row0 + r) * sstride;
-      if ((wf >> lane) & 1ull) {
-        const int k = pf[i] + blk_mbcnt(wf);
-        if (k < sstride) snbr[rb + k] = qv;
-      }
-      pf[i] += __popcll(wf);
-      if (INNER) {
-        if ((wi >> lane) & 1ull) {
-          const int k = pi[i] + blk_mbcnt(wi);
-          if (k < sstride) snbi[rb + k] = qv;
-        }
-        pi[i] += __popcll(wi);
-      }
-    });
-  }
-  // the tails up to whole chunks hold the sentinel; the counts (lane i: row r0 + i)
-  unsigned cf_v = 0u, ci_v = 0u;
+  // 5) the slot rows, full and inner: wave w writes rows w*RPW .. w*RPW + RPW-1 with LPR
+  // lanes per row; lane `part` of a row writes the row's entries [part*Q, part*Q + Q) (Q a
+  // multiple of 4: every store one aligned 8-byte word of 4 slots, no word shared by two
+  // lanes), walking the row's set bits from the chunk holding its first entry (ascending
+  // slots).  The lane holding the row's last entry also writes the sentinel up to a whole
+  // chunk.
+  constexpr int LPR = 64 / RPW;
+  const int r = wv * RPW + lane / LPR, part = lane % LPR;
+  const bool live = r < nrow;
+  auto word = [&](int c, int sel) -> unsigned long long {
+    return INNER ? s_w[(c * R + r) * 2 + sel] : s_w[c * R + r];
+  };
   bool over = false;
-  blk_rows<RPW>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    const int r = r0 + i;
-    if (r >= nrow) return;
-    const size_t rb = (size_t)(row0 + r) * sstride;
-    const int ef = min((pf[i] + UG - 1) / UG * UG, sstride);
-    if (pf[i] + lane < ef) snbr[rb + pf[i] + lane] = 0;
-    cf_v = writelane<i>(cf_v, (unsigned)pf[i]);
-    over |= pf[i] > sstride;
-    if (INNER) {
-      const int ei = min((pi[i] + UG - 1) / UG * UG, sstride);
-      if (pi[i] + lane < ei) snbi[rb + pi[i] + lane] = 0;
-      ci_v = writelane<i>(ci_v, (unsigned)pi[i]);
+  auto emit = [&](int sel, unsigned short *__restrict__ rows, int *__restrict__ cnt_out) {
+    int cnt = 0;
+    if (live)
+      for (int c = 0; c < nch; c++) cnt += __popcll(word(c, sel));
+    const int Q = ((cnt + LPR - 1) / LPR + 3) & ~3;
+    const int k0 = min(part * Q, cnt), k1 = min(k0 + Q, cnt);
+    int c = 0;
+    unsigned long long w = 0ull;
+    if (k0 < k1) {  // the chunk holding entry k0, and its bits from that entry on
+      int acc = 0;
+      for (;;) {
+        w = word(c, sel);
+        const int pc = __popcll(w);
+        if (acc + pc > k0) break;
+        acc += pc;
+        c++;
+      }
+      for (int j = k0 - acc; j > 0; j--) w &= w - 1ull;
     }
-  });
-  if (lane < RPW && r0 + lane < nrow) {
-    rcnt[row0 + r0 + lane] = (int)cf_v;
-    if (INNER) icnt[row0 + r0 + lane] = (int)ci_v;
-  }
-  if (over && lane == 0) atomicMax(ovf, 1 << 21);
+    unsigned long long *const out =
+        reinterpret_cast<unsigned long long *>(rows + (size_t)(row0 + r) * sstride);
+    unsigned long long buf = 0ull;
+    int pos = k0;
+    while (pos < k1) {
+      while (w == 0ull) w = word(++c, sel);
+      const int bit = __ffsll((long long)w) - 1;
+      w &= w - 1ull;
+      buf |= (unsigned long long)s_q[c][bit] << (16 * (pos & 3));
+      if ((pos & 3) == 3) {
+        if (pos < sstride) out[pos >> 2] = buf;
+        buf = 0ull;
+      }
+      pos++;
+    }
+    if (k0 < k1 && k1 == cnt) {  // the row's last word (zero-padded) and the sentinel
+      const int e = min((cnt + UG - 1) / UG * UG, sstride);
+      int q = pos >> 2;
+      if (pos & 3) {
+        if (4 * q < e) out[q] = buf;
+        q++;
+      }
+      for (; 4 * q < e; q++) out[q] = 0ull;
+    }
+    if (live && part == 0) {
+      cnt_out[row0 + r] = cnt;
+      over |= cnt > sstride;
+    }
+  };
+  emit(0, snbr, rcnt);
+  if (INNER) emit(1, snbi, icnt);
+  if (over) atomicMax(ovf, 1 << 21);
 }
 
 // A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.

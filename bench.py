@@ -721,32 +721,74 @@ def c5_physics(n, dim=3):
     return mp, dt, pc
 
 
-def c5_main(args, sph):
-    """C5 on the device-resident engine: the bubble_growth stack + fix phase_change on one
-    GPU (the largest single-GPU C5, 159^3 = 4.02M), rebuilding every step as the script
-    does.  `value` = particle-steps/s of the whole step (integration, phase change, rebuild,
-    the five pair passes, reverse comm)."""
+def brick_of(x, boxlo, boxhi, pg):
+    """The rank owning each position on a uniform brick grid, ranks x fastest: sublo <= x <
+    subhi with the engine's split points (sph_engine_create, CommBrick::exchange)."""
+    r = np.zeros(x.shape[0], dtype=np.int64)
+    mult = 1
+    for d in range(3):
+        prd = boxhi[d] - boxlo[d]
+        c = np.zeros(x.shape[0], dtype=np.int64)
+        for k in range(1, pg[d]):
+            c += (x[:, d] >= boxlo[d] + prd * (k / pg[d])).astype(np.int64)
+        r += c * mult
+        mult *= pg[d]
+    return r
+
+
+def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
+    """C5 on the device-resident engine: the bubble_growth stack + fix phase_change,
+    rebuilding every step as the script does.  One GPU: the largest single-GPU C5, 159^3 =
+    4.02M.  N GPUs: the same 4.02M box split into bricks (strong scaling; BASELINE C5 is this
+    box over 8 GPUs), every rank running fix phase_change on its own atoms with its own
+    random stream, dmass reverse comm and tag_extend over RCCL.  `value` = particle-steps/s
+    of the whole step (integration, phase change, exchange, borders, list build, the five
+    pair passes), all ranks, max-over-ranks time."""
     n = args.edge
     x, v, t, rho, e, cv, rmass = c5_system(n)
     mp, dt, pc = c5_physics(n)
     N = x.shape[0]
+    pg = procgrid_for(world)
     cfg = sph.make_config(3, 2, [0.0] * 3, [1.0] * 3, [1, 1, 1], [0.0, 1.0, 1.0], 0.0, dt,
-                          neigh_every=1, mp=mp)
-    eng = sph.Engine(cfg)
-    eng.set_atoms(x, v, t, rho, e, cv)
-    eng.set_atoms_multiphase(rmass, cv)
+                          neigh_every=1, mp=mp, procgrid=pg, rank=rank)
+    eng = sph.Engine(cfg, device=dev)
+    if world > 1:
+        sel = np.nonzero(brick_of(x, [0.0] * 3, [1.0] * 3, pg) == rank)[0]
+        eng.set_atoms(x[sel], v[sel], t[sel], rho[sel], e[sel], cv[sel])
+        eng.set_atoms_multiphase(rmass[sel], cv[sel])
+        eng.set_tags(sel.astype(np.int32))
+    else:
+        eng.set_atoms(x, v, t, rho, e, cv)
+        eng.set_atoms_multiphase(rmass, cv)
     eng.phase_change(pc["Tc"], pc["Tt"], pc["Hwv"], pc["dr"], pc["to_mass"], pc["cutoff"],
                      pc["from_type"], pc["to_type"], nevery=pc["nevery"], seed=pc["seed"],
                      prob=pc["prob"])
+    uid = share_uid(dist, rank, sph.comm_uid) if world > 1 else None
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
     with stdout_to_stderr():
+        if world > 1:
+            eng.comm_init(uid, world, rank)
         eng.setup()
         eng.run(args.warmup)
+    eng.sync()
+    barrier()
     eng.sync()
     eng.set_timing(True)
     t0 = time.perf_counter()
     eng.run(args.steps)
     eng.sync()
-    elapsed = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
     st = eng.stats()
     nloc = st["nlocal"]
     n_full = st["nbr_full"] / max(nloc, 1)
@@ -758,13 +800,21 @@ def c5_main(args, sph):
     ms_half = st["ms_tait"] / max(st["n_tait"], 1)
     ach_half = b_half * nloc / (ms_half * 1e-3) / 1e9
     ach_full = b_full * nloc / (ms_full * 1e-3) / 1e9
-    mpst = eng.get_atoms_multiphase()
+    ins = int(eng.get_atoms_multiphase()["ninserted"])
+    if dist is not None:
+        import torch
+        tt = torch.tensor([ins], dtype=torch.int64)
+        dist.all_reduce(tt)
+        ins = int(tt.item())
+    par = (f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo exchange + migration + "
+           "fix phase_change dmass reverse comm and tag_extend, one rank per GPU"
+           if world > 1 else "single GPU")
     out = {
         "metric": "particle-steps/s, C5 bubble_growth multiphase stack + fix phase_change",
-        "value": N * args.steps / elapsed, "unit": "particle-steps/s", "n_gpus": 1,
+        "value": N * args.steps / elapsed, "unit": "particle-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (bubble_growth geometry: sc lattice, vapour sphere r 0.05)",
         "config": {"workload": f"C5: {N} particles ({n}^3), bubble_growth/bubble.lmp stack "
                                "(rhosum/multiphase, colorgradient, taitwater/multiphase, "
@@ -772,8 +822,7 @@ def c5_main(args, sph):
                                "every step, rebuild every step, skin 0",
                    "particles_per_gpu": nloc, "ghosts_per_gpu": st["nghost"],
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
-                   "atoms_inserted": mpst["ninserted"], "dt": dt,
-                   "parallelism": "single GPU"},
+                   "atoms_inserted": ins, "dt": dt, "parallelism": par},
         "roofline": {"bound": "hbm",
                      "kernel": "k_mp_gather (taitwater/multiphase + surfacetension + "
                                "heatconduction/phasechange fused: full-list gather, each pair "
@@ -786,13 +835,111 @@ def c5_main(args, sph):
                          "bytes_per_particle": b_full},
                     "neighbor_build_and_phase_change_ms": st["ms_neigh"] / max(st["n_neigh"], 1),
                     "integrate_ms_per_step": st["ms_integrate"] / args.steps,
-                    "reverse_comm_ms_per_step": st["ms_comm"] / args.steps},
+                    "comm_ms_per_step": st["ms_comm"] / args.steps},
     }
-    if not args.no_cpu:
-        d = c5_pair_system(args.c5_cpu_n)
-        out["cpu_baseline"] = c5_pair_cpu(d)
-    print(json.dumps(out), flush=True)
-    eng.close()
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = c5_cpu_baseline(args.c5_cpu_n)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    with stdout_to_stderr():
+        eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def c5_cpu_baseline(n_cpu, steps=2):
+    """The same C5 step in the reference's own code (oracle/_ref, one core) on the same
+    bubble geometry at n_cpu^3 particles: Neighbor::full_bin + half_from_full_newton (the
+    script rebuilds every step), the five pair styles' compute(), and FixPhaseChange::
+    pre_exchange, `steps` times; borders/comm and FixMeso (<1 %) are not timed."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes as C
+    import pyoracle as po
+    if not po.ref_available():
+        return None
+    R = po.ref()
+    x, v, ty, rho, e, cv, rmass = c5_system(n_cpu)
+    mp, dt, pc = c5_physics(n_cpu)
+    N = x.shape[0]
+    s = po.System(3, np.zeros(3), np.ones(3), (1, 1, 1), x, v, ty, rho, e, cv, 2, np.zeros(3),
+                  rmass=rmass)
+    h = float(mp["rhosum_cut"][1, 1])
+    cut = np.ascontiguousarray(mp["rhosum_cut"])
+    cns, cmax = po.cutneighsq(2, cut, 0.0)
+    g = po.borders(s, cmax)
+    gx = np.ascontiguousarray(g.x)
+    nz = lambda a: a if a.size else np.zeros(1, np.int32)
+    d = {k: np.ascontiguousarray(g.gather(a)) for k, a in
+         dict(v=v, rho=rho, e=e, cv=cv, rmass=rmass).items()}
+    rho0, c0 = np.array(mp["rho0"], float), np.array(mp["c0"], float)
+    gam, rbg = np.array(mp["gamma"], float), np.array(mp["rbg"], float)
+    visc = np.ascontiguousarray(mp["visc"], dtype=float)
+    alpha = np.ascontiguousarray(mp["cg_alpha"], dtype=float)
+    halpha = np.ascontiguousarray(mp["heat_alpha"], dtype=float)
+    ff = np.ascontiguousarray(mp["heat_fixflag"], dtype=np.int32)
+    tc = np.ascontiguousarray(mp["heat_tc"], dtype=float)
+    args = ["pc", "all", "phase_change", repr(pc["Tc"]), repr(pc["Tt"]), repr(pc["Hwv"]),
+            repr(pc["dr"]), repr(pc["to_mass"]), repr(pc["cutoff"]), "1", "2", "1",
+            str(pc["seed"]), repr(pc["prob"]), "region", "box", "units", "box"]
+    av = (C.c_char_p * len(args))(*[a.encode() for a in args])
+    hnd = R.ref_pc_new(3, 2, s.boxlo, s.boxhi, 0, dt, len(args), av)
+    t = dict(list=0.0, pair=0.0, pc=0.0)
+    for step in range(steps):
+        t0 = time.perf_counter()
+        args_n = (3, 2, g.nlocal, g.nghost, gx, g.type, s.boxlo, s.boxhi, s.boxlo, s.boxhi,
+                  cmax, np.ascontiguousarray(cns))
+        foff = np.zeros(g.nlocal + 1, dtype=np.int64)
+        tot = R.ref_neigh_full(*args_n, foff, None, 0)
+        fnb = np.zeros(max(tot, 1), dtype=np.int32)
+        R.ref_neigh_full(*args_n, foff, fnb.ctypes.data, tot)
+        hoff = np.zeros(g.nlocal + 1, dtype=np.int64)
+        htot = R.ref_neigh_half_from_full(g.nlocal, g.nghost, gx, foff, fnb, hoff, None)
+        hnb = np.zeros(max(htot, 1), dtype=np.int32)
+        R.ref_neigh_half_from_full(g.nlocal, g.nghost, gx, foff, fnb, hoff, hnb.ctypes.data)
+        t1 = time.perf_counter()
+        t["list"] += (t1 - t0) / 2.0   # (two full_bin passes: count + fill)
+        rr = d["rho"].copy()
+        cg = np.zeros((g.nall, 3))
+        f = np.zeros((g.nall, 3))
+        de = np.zeros(g.nall)
+        t0 = time.perf_counter()
+        R.ref_rhosum_multiphase(3, 2, g.nlocal, g.nghost, gx, g.type, d["rmass"], cut, foff,
+                                nz(fnb), rr)
+        R.ref_colorgradient(3, 2, g.nlocal, g.nghost, gx, d["rho"], d["rmass"], g.type, alpha,
+                            cut, foff, nz(fnb), cg)
+        R.ref_taitwater_multiphase(3, 2, g.nlocal, g.nghost, 1, gx, d["v"], d["rho"], g.type,
+                                   d["rmass"], rho0, c0, gam, rbg, visc, cut, hoff, nz(hnb), f)
+        R.ref_surfacetension(3, 2, g.nlocal, g.nghost, 1, gx, d["rho"], d["rmass"], g.type, cg,
+                             cut, hoff, nz(hnb), f)
+        R.ref_heatconduction_phasechange(3, 2, g.nlocal, g.nghost, 1, gx, d["e"], d["cv"],
+                                         d["rho"], d["rmass"], g.type, halpha, ff.ctypes.data,
+                                         tc.ctypes.data, cut, hoff, nz(hnb), de)
+        t["pair"] += time.perf_counter() - t0
+        nmax = g.nall + 4096
+        A = {}
+        for k, src in (("x", gx), ("v", d["v"]), ("vest", d["v"]), ("cg", cg)):
+            A[k] = np.zeros((nmax, 3))
+            A[k][:g.nall] = src
+        for k in ("e", "rmass", "rho", "cv"):
+            A[k] = np.zeros(nmax)
+            A[k][:g.nall] = d[k]
+        A["type"] = np.zeros(nmax, np.int32)
+        A["type"][:g.nall] = g.type
+        nr = C.c_long(0)
+        t0 = time.perf_counter()
+        R.ref_pc_pre_exchange(hnd, step + 1, g.nlocal, g.nghost, nmax, A["x"], A["v"], A["vest"],
+                              A["cg"], A["e"], A["rmass"], A["rho"], A["cv"], A["type"], foff,
+                              nz(fnb), len(g.swap_first) - 1, g.swap_first, nz(g.src),
+                              C.byref(nr))
+        t["pc"] += time.perf_counter() - t0
+    per = {k: v / steps for k, v in t.items()}
+    tot = sum(per.values())
+    return {"value": N / tot, "unit": "particle-steps/s", "cores": 1, "kind": "reference",
+            "sample": f"reference code (oracle/_ref, g++ -O3, one core) on the same C5 bubble "
+                      f"geometry at {n_cpu}^3 = {N} particles, per step (mean of {steps}): "
+                      f"Neighbor::full_bin + half_from_full_newton {per['list']:.3f} s, the five "
+                      f"pair styles' compute() {per['pair']:.3f} s, FixPhaseChange::pre_exchange "
+                      f"{per['pc']:.4f} s; borders/comm and FixMeso not timed"}
 
 
 def main():
@@ -849,9 +996,8 @@ def main():
         args.edge = args.edge or 80
         return (c2_pair_main if args.workload == "c2pair" else c5_pair_main)(args, sph)
     if args.workload == "c5":
-        assert world == 1, "the C5 workload runs on one GPU (fix phase_change: one brick)"
         args.edge = args.edge or 159
-        return c5_main(args, sph)
+        return c5_main(args, sph, dist, rank, world, local % max(ndev, 1))
     args.edge = args.edge or 100
     if args.workload == "c3":
         assert world == 1, "the C3 workload runs on one GPU"

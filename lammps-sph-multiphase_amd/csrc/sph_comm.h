@@ -59,6 +59,13 @@ struct Transport {
   virtual void exchange_multi(int n, const int *peer, const void *const *sb,
                               const size_t *sbytes, void *const *rb, const size_t *rbytes,
                               hipStream_t s) = 0;
+  // every rank's v into out[size()] (MPI_Allgather of one int); host-synchronous
+  void allgather_int(int v, int *out, hipStream_t s) {
+    const int P = size(), me = rank();
+    std::vector<int> sc(P, v);
+    exchange_counts_all(sc.data(), out, s);
+    out[me] = v;
+  }
 };
 
 #define SPH_NCCL_TRY(call)                                                             \

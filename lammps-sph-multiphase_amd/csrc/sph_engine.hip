@@ -150,7 +150,8 @@ struct sph_engine {
   sph_phasechange_params pcp{};
   int pc_nevery = 1, pc_seed = 0;
   int64_t pc_next = 1, pc_inserted = 0;
-  int tag_next = 0;  // tag of the next created atom (atom->tag_extend on one brick)
+  int tag_next = 0;  // tag of the next created atom (atom->tag_extend)
+  bool pc_tags_agreed = false;  // bricks: tag_next agreed over the ranks (first call)
   std::vector<double> cv_by_tag;  // single-phase engines: the constant cv, for restarts
 
   int nlocal = 0, nghost = 0;
@@ -1001,6 +1002,52 @@ struct sph_engine {
     }
   }
 
+  // Bricks: the same slot order, but a swap's ghosts come from another rank, whose scan
+  // order (owned atoms in tag order, then its ghosts in slot order) only it knows -- each
+  // dimension's two swaps send that key along the send lists (one exchange), the receiver
+  // sorts each swap by it.  Collective over the ranks (every rank calls it).
+  void pc_ghost_slots_multi() {
+    pc_grank.reserve(nghost > 0 ? nghost : 1);
+    for (int k = 0; k + 1 < nswap; k += 2) {
+      Swap &a = swaps[k], &b = swaps[k + 1];
+      const size_t sa = (size_t)a.nsend * 4, sb = (size_t)b.nsend * 4;
+      const size_t ra = (size_t)a.nrecv * 4, rb = (size_t)b.nrecv * 4;
+      const size_t so = (sa + 255) & ~(size_t)255, ro = (ra + 255) & ~(size_t)255;
+      cbs.reserve(std::max<size_t>(so + sb, 1), true, s);
+      cbr.reserve(std::max<size_t>(ro + rb, 1), true, s);
+      if (a.nsend)
+        hipLaunchKernelGGL(k_pc_sendkeys, dim3(blocks(a.nsend)), dim3(BLK), 0, s, a.nsend,
+                           a.list.p, nlocal, tag.p, pc_grank.p, (int *)cbs.p);
+      if (b.nsend)
+        hipLaunchKernelGGL(k_pc_sendkeys, dim3(blocks(b.nsend)), dim3(BLK), 0, s, b.nsend,
+                           b.list.p, nlocal, tag.p, pc_grank.p, (int *)(cbs.p + so));
+      if (a.remote) {
+        tr->exchange2(cbs.p, sa, a.sendproc, cbr.p, ra, a.recvproc, cbs.p + so, sb, b.sendproc,
+                      cbr.p + ro, rb, b.recvproc, s);
+      } else {
+        if (ra) SPH_HIP_TRY(hipMemcpyAsync(cbr.p, cbs.p, ra, hipMemcpyDeviceToDevice, s));
+        if (rb) SPH_HIP_TRY(hipMemcpyAsync(cbr.p + ro, cbs.p + so, rb, hipMemcpyDeviceToDevice, s));
+      }
+      for (int dir = 0; dir < 2; dir++) {
+        Swap &sw = dir ? b : a;
+        const int ns = sw.nrecv, first = sw.firstrecv - nlocal;
+        if (ns == 0) continue;
+        pc_key.reserve(2 * (size_t)ns);
+        pc_val.reserve(2 * (size_t)ns);
+        hipLaunchKernelGGL(k_pc_keys_in, dim3(blocks(ns)), dim3(BLK), 0, s, ns,
+                           (const int *)(cbr.p + (dir ? ro : 0)), pc_key.p, pc_val.p);
+        size_t tb = 0;
+        SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pc_key.p, pc_key.p + ns,
+                                                       pc_val.p, pc_val.p + ns, ns, 0, 31, s));
+        tmp_reserve(tb);
+        SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, pc_key.p, pc_key.p + ns,
+                                                       pc_val.p, pc_val.p + ns, ns, 0, 31, s));
+        hipLaunchKernelGGL(k_pc_swaprank, dim3(blocks(ns)), dim3(BLK), 0, s, ns, first,
+                           pc_val.p + ns, pc_grank.p);
+      }
+    }
+  }
+
   void setup_bins_geometry() {
     for (int k = 0; k < 3; k++) {
       double lo = sublo[k], hi = subhi[k];
@@ -1743,11 +1790,17 @@ struct sph_engine {
   }
 
   // FixPhaseChange::pre_exchange (fix_phase_change.cpp:167-352) on the last build's full
-  // list, owned atoms as integrated, ghosts as last communicated; the rebuild follows
+  // list, owned atoms as integrated, ghosts as last communicated; the rebuild follows.
+  // Bricks: every rank runs the call on its own atoms with its own RanPark of the same seed
+  // (:116), creating atoms only inside its sub-box; the ghosts' dmass goes back over the
+  // swaps (reverse_comm_fix, :324), and the created atoms take the next tags rank by rank
+  // (MPI_Allreduce + Atom::tag_extend, :338-351).  A rank with no candidate still takes part
+  // in the collectives (slot keys, reverse comm, counts) and in the finish loop.
   void phase_change() {
     Scope t(this, T_NEIGH);
+    const bool mul = multi();
     const int n = nlocal, nall = nlocal + nghost;
-    if (n == 0) return;
+    if (n == 0 && !mul) return;
     sph_phasechange_params p = pcp;
     for (int k = 0; k < 3; k++) {
       p.sublo[k] = sublo[k];
@@ -1758,17 +1811,14 @@ struct sph_engine {
     const PcDev pd{cfg.dim, p.from_type, p.to_type, p.Tc, p.to_mass, p.cutoff};
     DBuf<int> &flag = pc_flag, &cand = pc_cand, &otag = pc_otag, &idx = pc_idx;
     DBuf<double> &rec = pc_rec, &gat = pc_gat, &Wd = pc_Wd, &vals = pc_vals, &nrec = pc_nrec;
-    flag.reserve(n);
-    hipLaunchKernelGGL(k_pc_flags, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
-                       ty.p, en.p, cvv.p, pd, flag.p);
-    const int ncand = select_flagged_i(flag.p, n, cand);
-    if (ncand == 0) return;  // (dmass 0: the finish loop leaves rmass and e as they are)
-    rec.reserve((size_t)8 * ncand);
-    gat.reserve((size_t)9 * ncand);
-    otag.reserve(ncand);
-    // first pass screens: every ghost ranks 0, so minr < NORANK flags the candidates whose
-    // row holds a from_type ghost at all; only then are LAMMPS' ghost slots worked out
-    pc_minr.reserve(ncand);
+    int ncand = 0;
+    if (n > 0) {
+      flag.reserve(n);
+      hipLaunchKernelGGL(k_pc_flags, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
+                         ty.p, en.p, cvv.p, pd, flag.p);
+      ncand = select_flagged_i(flag.p, n, cand);
+    }
+    if (ncand == 0 && !mul) return;  // (dmass 0: the finish loop leaves rmass and e as they are)
     const int lst = strided ? list_stride : 0;
     PcRank rk{n, 1, nullptr};
     auto walk = [&](const PcRank &r) {
@@ -1776,26 +1826,41 @@ struct sph_engine {
                          (const int *)nullptr, off.p, nbr.p, xf.p, vr.p, (const double *)vel.p,
                          4, ty.p, rm.p, pd, rec.p, lst, ccnt.p, r, 0, 0, pc_minr.p);
     };
-    walk(rk);
-    std::vector<int> hm(ncand);
-    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    if (std::any_of(hm.begin(), hm.end(), [](int v) { return v != PC_NORANK; })) {
-      pc_ghost_slots();
-      rk = PcRank{n, 2, pc_grank.p};
-      walk(rk);
-    }
-    hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
-                       vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
-    std::vector<int> hc(ncand), ht(ncand);
+    std::vector<int> hm(ncand), hc(ncand), ht(ncand);
     std::vector<double> hr((size_t)8 * ncand), hg((size_t)9 * ncand);
-    SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipMemcpyAsync(hc.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipMemcpyAsync(ht.data(), otag.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipMemcpyAsync(hr.data(), rec.p, hr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipMemcpyAsync(hg.data(), gat.p, hg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));
-    // the reference meets the candidates in its atom order: tag order on one process
+    if (mul) {  // slot ranks first (collective), then one walk with them
+      pc_ghost_slots_multi();
+      rk = PcRank{n, 2, pc_grank.p};
+    }
+    if (ncand > 0) {
+      rec.reserve((size_t)8 * ncand);
+      gat.reserve((size_t)9 * ncand);
+      otag.reserve(ncand);
+      // one brick: the first pass screens -- every ghost ranks 0, so minr < NORANK flags the
+      // candidates whose row holds a from_type ghost at all; only then are LAMMPS' ghost
+      // slots worked out
+      pc_minr.reserve(ncand);
+      walk(rk);
+      if (!mul) {
+        SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+        SPH_HIP_TRY(hipStreamSynchronize(s));
+        if (std::any_of(hm.begin(), hm.end(), [](int v) { return v != PC_NORANK; })) {
+          pc_ghost_slots();
+          rk = PcRank{n, 2, pc_grank.p};
+          walk(rk);
+        }
+      }
+      hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
+                         vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
+      SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(hc.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(ht.data(), otag.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(hr.data(), rec.p, hr.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(hg.data(), gat.p, hg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipStreamSynchronize(s));
+    }
+    // the reference meets the candidates in its atom order: tag order (one process, or one
+    // rank's owned atoms while none has migrated)
     std::vector<int> ord(ncand);
     for (int k = 0; k < ncand; k++) ord[k] = k;
     std::sort(ord.begin(), ord.end(), [&](int a, int b) { return ht[a] < ht[b]; });
@@ -1828,7 +1893,25 @@ struct sph_engine {
     std::vector<double> ins_rec, ins_W;
     pc_replay(p, cfg.dim, pc_seed, cands, ins_k, ins_W, ins_rec, recompute);
     const int nins = (int)ins_k.size();
-    if (nins == 0) return;
+    // MPI_Allreduce(nins) and the tag base of this rank's created atoms (tag_extend: rank
+    // order); the first call also agrees on the next free tag
+    int ninsall = nins, tag0 = tag_next;
+    if (mul) {
+      std::vector<int> all(tr->size());
+      if (!pc_tags_agreed) {
+        tr->allgather_int(tag_next, all.data(), s);
+        tag_next = *std::max_element(all.begin(), all.end());
+        pc_tags_agreed = true;
+      }
+      tr->allgather_int(nins, all.data(), s);
+      ninsall = 0;
+      tag0 = tag_next;
+      for (int r = 0; r < (int)all.size(); r++) {
+        if (r < tr->rank()) tag0 += all[r];
+        ninsall += all[r];
+      }
+    }
+    if (nins == 0 && !mul) return;
     std::vector<int> hidx(nins);
     std::vector<double> hval(nins), hW(nins);
     for (int q = 0; q < nins; q++) {
@@ -1837,36 +1920,42 @@ struct sph_engine {
       hval[q] = ins_rec[(size_t)13 * q + 9];
       hW[q] = ins_W[q];
     }
-    idx.reserve(nins);
-    vals.reserve(nins);
-    Wd.reserve(nins);
-    nrec.reserve((size_t)13 * nins);
-    dmass.reserve(nall);
-    SPH_HIP_TRY(hipMemcpyAsync(idx.p, hidx.data(), nins * sizeof(int), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(vals.p, hval.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(Wd.p, hW.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipMemcpyAsync(nrec.p, ins_rec.data(), ins_rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipMemsetAsync(dmass.p, 0, nall * sizeof(double), s));
-    // e_i = (e_i - Hwv)/2 of the atoms that changed phase, the donors' dmass, its reverse
-    // comm, rmass -= dmass and e renormalised, then the new atoms
-    hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
-    hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
-                       (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p,
-                       lst, ccnt.p, rk);
+    dmass.reserve(nall > 0 ? nall : 1);
+    if (nall) SPH_HIP_TRY(hipMemsetAsync(dmass.p, 0, nall * sizeof(double), s));
+    if (nins) {
+      idx.reserve(nins);
+      vals.reserve(nins);
+      Wd.reserve(nins);
+      nrec.reserve((size_t)13 * nins);
+      SPH_HIP_TRY(hipMemcpyAsync(idx.p, hidx.data(), nins * sizeof(int), hipMemcpyHostToDevice, s));
+      SPH_HIP_TRY(hipMemcpyAsync(vals.p, hval.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
+      SPH_HIP_TRY(hipMemcpyAsync(Wd.p, hW.data(), nins * sizeof(double), hipMemcpyHostToDevice, s));
+      SPH_HIP_TRY(hipMemcpyAsync(nrec.p, ins_rec.data(), ins_rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
+      // e_i = (e_i - Hwv)/2 of the atoms that changed phase, the donors' dmass
+      hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
+      hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
+                         (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p,
+                         lst, ccnt.p, rk);
+    }
+    // its reverse comm, rmass -= dmass and e renormalised, then the new atoms
     reverse1(dmass.p);
-    hipLaunchKernelGGL(k_pc_finish, dim3(blocks(n)), dim3(BLK), 0, s, n, dmass.p, rm.p, en.p);
-    ensure_atoms((size_t)n + nins, true);  // (over the ghost slots: the rebuild follows)
-    vel.reserve((size_t)n + nins, true, s);
-    tag.reserve((size_t)n + nins, true, s);
-    fo.reserve((size_t)n + nins, true, s);
-    de.reserve((size_t)n + nins, true, s);
-    hipLaunchKernelGGL(k_pc_append, dim3(blocks(nins)), dim3(BLK), 0, s, nins, nrec.p, n,
-                       p.to_type, tag_next, xf.p, vr.p, vel.p, en.p, rm.p, cvv.p, cg.p, ty.p,
-                       tag.p, fo.p, de.p);
+    if (n)
+      hipLaunchKernelGGL(k_pc_finish, dim3(blocks(n)), dim3(BLK), 0, s, n, dmass.p, rm.p, en.p);
+    if (nins) {
+      ensure_atoms((size_t)n + nins, true);  // (over the ghost slots: the rebuild follows)
+      vel.reserve((size_t)n + nins, true, s);
+      tag.reserve((size_t)n + nins, true, s);
+      fo.reserve((size_t)n + nins, true, s);
+      de.reserve((size_t)n + nins, true, s);
+      hipLaunchKernelGGL(k_pc_append, dim3(blocks(nins)), dim3(BLK), 0, s, nins, nrec.p, n,
+                         p.to_type, tag0, xf.p, vr.p, vel.p, en.p, rm.p, cvv.p, cg.p, ty.p,
+                         tag.p, fo.p, de.p);
+    }
     SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host staging vectors go out of scope)
+    if (ninsall == 0) return;  // (natoms unchanged: the ghosts stay, the rebuild follows)
     nlocal = n + nins;
     nghost = 0;
-    tag_next += nins;
+    tag_next += ninsall;
     pc_inserted += nins;
   }
 
@@ -2174,6 +2263,7 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   e->nlocal = n;
   e->nghost = 0;
   e->tag_next = n;
+  e->pc_tags_agreed = false;
   e->pc_inserted = 0;
   e->cv_by_tag.assign(n, 1.0);
   if (cv)
@@ -2250,8 +2340,6 @@ int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int 
   SPH_REQUIRE(e && p, SPH_HIP_EINVAL, "sph_engine_phase_change: NULL argument");
   SPH_REQUIRE(e->mp, SPH_HIP_EINVAL,
               "fix phase_change needs atom_style meso/multiphase (a multiphase engine)");
-  SPH_REQUIRE(!e->multi(), SPH_HIP_EINVAL,
-              "sph_engine_phase_change: one brick only (new tags need a global tag_extend)");
   SPH_REQUIRE(seed > 0, SPH_HIP_EINVAL, "Invalid seed for Park random # generator");
   SPH_REQUIRE(nevery >= 1, SPH_HIP_EINVAL, "sph_engine_phase_change: nevery < 1");
   SPH_REQUIRE(p->to_mass > 0.0 && p->maxattempt >= 1 && p->cutoff > 0.0, SPH_HIP_EINVAL,
@@ -2675,9 +2763,17 @@ int sph_engine_set_tags(sph_engine *e, const int *tags) {
   SPH_API_BEGIN
   SPH_REQUIRE(e && (tags || e->nlocal == 0), SPH_HIP_EINVAL, "sph_engine_set_tags: bad argument");
   SPH_HIP_TRY(hipSetDevice(e->device));
+  int mx = -1;
+  for (int i = 0; i < e->nlocal; i++) {
+    SPH_REQUIRE(tags[i] >= 0 && tags[i] < (1 << 30), SPH_HIP_EINVAL,
+                "sph_engine_set_tags: tag %d outside [0, 2^30)", tags[i]);
+    mx = std::max(mx, tags[i]);
+  }
   if (e->nlocal)
     SPH_HIP_TRY(hipMemcpy(e->tag.p, tags, e->nlocal * sizeof(int), hipMemcpyHostToDevice));
   e->global_tags = true;
+  e->tag_next = mx + 1;  // (bricks: the ranks agree on the largest at the first phase change)
+  e->pc_tags_agreed = false;
   SPH_API_END
 }
 

@@ -197,6 +197,26 @@ static __global__ void k_pc_swaprank(int ns, int first, const int *__restrict__ 
   grank[first + val_sorted[p]] = first + p;
 }
 
+// bricks: the key each sent atom carries to the receiving rank -- its place in the order
+// CommBrick::borders scanned this rank's atoms (owned in tag order, then ghosts in LAMMPS
+// slot order); tags stay below 2^30
+static __global__ void k_pc_sendkeys(int n, const int *__restrict__ list, int nlocal,
+                                     const int *__restrict__ tag,
+                                     const int *__restrict__ grank, int *__restrict__ key) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int i = list[k];
+  key[k] = i < nlocal ? tag[i] : (1 << 30) + grank[i - nlocal];
+}
+// received keys of one swap -> (key, position) pairs for the sort
+static __global__ void k_pc_keys_in(int n, const int *__restrict__ in, int *__restrict__ key,
+                                    int *__restrict__ val) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  key[k] = in[k];
+  val[k] = k;
+}
+
 // ---- host side: the random stream, in the reference's order ----------------------------
 inline double park_uniform(int &seed) {  // RanPark::uniform, random_park.cpp:42-49
   const int IA = 16807, IM = 2147483647, IQ = 127773, IR = 2836;

@@ -449,6 +449,13 @@ def half_from_full(g: Ghosted, foff: np.ndarray, fneigh: np.ndarray):
     return hoff, h[:tot]
 
 
+def _reverse_rows(off, nb):
+    out = nb.copy()
+    for i in range(len(off) - 1):
+        out[off[i]:off[i + 1]] = nb[off[i]:off[i + 1]][::-1]
+    return out
+
+
 def _nz(a):
     return a if a.size else np.zeros(1, dtype=a.dtype)
 
@@ -774,6 +781,146 @@ def pc_params(sysm: System, pc: dict, dt: float) -> PcParams:
     return p
 
 
+# ---------------------------------------------------------------------------------------
+# Brick decomposition (CommBrick on a uniform processor grid): the per-rank views fix
+# phase_change sees when the box is split over several ranks
+# ---------------------------------------------------------------------------------------
+def brick_grid(sysm: System, pg):
+    """Domain::set_local_box with uniform splits and CommBrick's procneigh, ranks x fastest
+    (the engine's formula, sph_engine_create): per rank its grid location, sub-box and the
+    lower/upper neighbour along each dimension."""
+    P = int(pg[0] * pg[1] * pg[2])
+    out = []
+    for r in range(P):
+        loc = [r % pg[0], (r // pg[0]) % pg[1], r // (pg[0] * pg[1])]
+        lo, hi = np.zeros(3), np.zeros(3)
+        nb = np.zeros((3, 2), dtype=np.int64)
+        for k in range(3):
+            prd = float(sysm.boxhi[k] - sysm.boxlo[k])
+            lo[k] = sysm.boxlo[k] + prd * (loc[k] / pg[k])
+            hi[k] = (sysm.boxhi[k] if loc[k] + 1 == pg[k]
+                     else sysm.boxlo[k] + prd * ((loc[k] + 1) / pg[k]))
+            for side, step in ((0, -1), (1, 1)):
+                m = list(loc)
+                m[k] = (m[k] + step) % pg[k]
+                nb[k, side] = (m[2] * pg[1] + m[1]) * pg[0] + m[0]
+        out.append(dict(loc=loc, lo=lo, hi=hi, neigh=nb))
+    return out
+
+
+def brick_owner(sysm: System, x: np.ndarray, pg) -> np.ndarray:
+    """The rank owning each atom: sublo <= x < subhi per dimension (CommBrick::exchange)."""
+    r = np.zeros(x.shape[0], dtype=np.int64)
+    mult = 1
+    for d in range(3):
+        prd = float(sysm.boxhi[d] - sysm.boxlo[d])
+        c = np.zeros(x.shape[0], dtype=np.int64)
+        for k in range(1, pg[d]):
+            c += (x[:, d] >= sysm.boxlo[d] + prd * (k / pg[d])).astype(np.int64)
+        r += c * mult
+        mult *= pg[d]
+    return r
+
+
+@dataclass
+class BrickView:
+    """One rank's atoms after CommBrick::borders over a processor grid: owned atoms in tag
+    order (their LAMMPS order while nothing has migrated), then each swap's ghosts in the
+    order the sending rank scanned its atoms (comm_brick.cpp:733-800)."""
+
+    rank: int
+    nlocal: int
+    gid: np.ndarray          # (nall,) global (tag-order) index of the atom or its origin
+    x: np.ndarray            # (nall,3) at borders time
+    type: np.ndarray
+    image: np.ndarray        # (nall,3) periodic image of each copy (0 for owned)
+    swap_first: list         # first ghost of each swap, + nghost
+    src_rank: np.ndarray     # (nghost,) sending rank of each ghost
+    src_idx: np.ndarray      # (nghost,) its index on the sending rank (sendlist entry)
+    lo: np.ndarray = None
+    hi: np.ndarray = None
+    loc: list = None
+    off: np.ndarray = None   # full list of the build (local indices)
+    nb: np.ndarray = None
+    hoff: np.ndarray = None  # its half list (half_from_full_newton on the rank's atoms)
+    hnb: np.ndarray = None
+
+    @property
+    def nghost(self) -> int:
+        return int(self.gid.shape[0]) - self.nlocal
+
+
+def borders_bricks(sysm: System, cutghost: float, pg, x: np.ndarray | None = None):
+    """CommBrick::borders (comm_brick.cpp:696-864, maxneed 1) on every rank of the grid at
+    once: per dimension both swaps scan owned + earlier dimensions' ghosts, the lower swap's
+    ghosts are appended before the upper one's; a brick at the periodic edge shifts the
+    copies by the box length (one add per coordinate)."""
+    xo = sysm.x if x is None else x
+    grid = brick_grid(sysm, pg)
+    own = brick_owner(sysm, xo, pg)
+    V = []
+    for r, b in enumerate(grid):
+        idx = np.nonzero(own == r)[0]
+        V.append(dict(gid=[idx], x=[xo[idx].copy()], type=[sysm.type[idx].copy()],
+                      image=[np.zeros((idx.size, 3), dtype=np.int64)], sf=[], srank=[],
+                      sidx=[], nlocal=int(idx.size)))
+    cat = lambda v, k: np.concatenate(v[k]) if len(v[k]) > 1 else v[k][0]
+    for d in range(sysm.dim):
+        prd = float(sysm.boxhi[d] - sysm.boxlo[d])
+        snap = [dict(gid=cat(v, "gid"), x=cat(v, "x"), type=cat(v, "type"),
+                     image=cat(v, "image")) for v in V]
+        incoming = [[None, None] for _ in V]
+        for ineed in (0, 1):
+            for r, b in enumerate(grid):
+                loc = b["loc"][d]
+                if sysm.periodic[d]:
+                    sendflag = True
+                else:
+                    sendflag = loc > 0 if ineed == 0 else loc < pg[d] - 1
+                if ineed == 0:
+                    lo, hi = -1.0e20, b["lo"][d] + cutghost
+                    pbc = 1 if loc == 0 else 0
+                else:
+                    lo, hi = b["hi"][d] - cutghost, 1.0e20
+                    pbc = -1 if loc == pg[d] - 1 else 0
+                sv = snap[r]
+                xs = sv["x"]
+                if sendflag:
+                    sel = np.nonzero((xs[:, d] >= lo) & (xs[:, d] <= hi))[0]
+                else:
+                    sel = np.zeros(0, dtype=np.int64)
+                xg = xs[sel].copy()
+                if pbc:
+                    xg[:, d] = xg[:, d] + pbc * prd
+                img = sv["image"][sel].copy()
+                img[:, d] += pbc
+                incoming[int(b["neigh"][d, ineed])][ineed] = (
+                    sv["gid"][sel], xg, sv["type"][sel], img, r, sel)
+        for r, v in enumerate(V):
+            for ineed in (0, 1):
+                v["sf"].append(sum(a.shape[0] for a in v["gid"]) - v["nlocal"])
+                inc = incoming[r][ineed]
+                if inc is None:
+                    continue
+                g, xg, t, img, src, sel = inc
+                v["gid"].append(g)
+                v["x"].append(xg)
+                v["type"].append(t)
+                v["image"].append(img)
+                v["srank"].append(np.full(sel.size, src, dtype=np.int64))
+                v["sidx"].append(sel)
+    out = []
+    for r, v in enumerate(V):
+        gid = cat(v, "gid")
+        v["sf"].append(gid.shape[0] - v["nlocal"])
+        sr = np.concatenate(v["srank"]) if v["srank"] else np.zeros(0, np.int64)
+        si = np.concatenate(v["sidx"]) if v["sidx"] else np.zeros(0, np.int64)
+        b = grid[r]
+        out.append(BrickView(r, v["nlocal"], gid, cat(v, "x"), cat(v, "type").astype(np.int32),
+                             cat(v, "image"), v["sf"], sr, si, b["lo"], b["hi"], b["loc"]))
+    return out
+
+
 class MpRefRun:
     """C5 Verlet (verlet.cpp:222-308) over the C restatement: initial_integrate (fix meso,
     rmass) -> [pre_exchange: fix phase_change] -> pbc/borders/lists or forward comm (comm
@@ -783,9 +930,18 @@ class MpRefRun:
     half list with Newton-3 -> reverse comm (f, de) -> final_integrate.  Atom order = tag
     order (new atoms appended, no sort)."""
 
-    def __init__(self, sysm: System, ph: MpPhysics, cg=None):
+    def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None):
         self.s = sysm.copy()
         assert self.s.rmass is not None
+        # procgrid: fix phase_change as it runs on a grid of ranks (each rank scans its owned
+        # atoms in tag order with its own RanPark of the same seed, fix_phase_change.cpp:116,
+        # creates atoms only in its sub-box, and the ghosts' dmass goes back over the ranks'
+        # swaps); the pair styles, integrators and lists do not depend on the decomposition
+        self.pg = None if procgrid is None or int(np.prod(procgrid)) == 1 else tuple(procgrid)
+        # rev: every list row walked backwards -- the same physics in another summation
+        # order, so a test can size its tolerance to how far the reference's own result moves
+        # under reordering where a sum nearly cancels (ill-conditioned atoms)
+        self.rev = False
         self.ph = ph
         nt = sysm.ntypes
         self.cns, self.cutneighmax = cutneighsq(nt, ph.cutmax(nt), ph.skin)
@@ -800,6 +956,8 @@ class MpRefRun:
         self.dtf = 0.5 * ph.dt
         self.next_pc = 1                      # next_reneighbor = ntimestep + 1 (:120)
         self.seed = int(ph.pc["seed"]) if ph.pc else 0
+        if self.pg:
+            self.seeds = [self.seed] * int(np.prod(self.pg))
         self.ninserted = 0
         self.tabs = {}
         for name in ("rhosum_cut", "cg_alpha", "cg_cut", "visc", "tait_cut", "st_cut",
@@ -821,6 +979,10 @@ class MpRefRun:
         self.cv_all = g.gather(s.cv)
         self.rm_all = g.gather(s.rmass)
         self.cg_all = g.gather(self.cg)
+        if self.pg:   # the owned values as communicated: what every rank's ghosts hold
+            self.comm = dict(x=s.x.copy(), v=s.v.copy(), vest=self.vest.copy(),
+                             rho=s.rho.copy(), e=s.e.copy(), cv=s.cv.copy(),
+                             rmass=s.rmass.copy(), cg=self.cg.copy())
 
     def _build(self):
         s = self.s
@@ -832,8 +994,19 @@ class MpRefRun:
         self.image = im + pbc_images(s, x0)
         self.g = borders(s, self.cutneighmax)
         self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
+        if self.rev:
+            self.fnb = _reverse_rows(self.foff, self.fnb)
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
         self._ghost_fields()
+        if self.pg:
+            self.bviews = borders_bricks(s, self.cutneighmax, self.pg)
+            for bv in self.bviews:
+                gh = Ghosted(bv.nlocal, bv.nghost, np.ascontiguousarray(bv.x), bv.type,
+                             np.zeros(bv.nghost, np.int32), np.zeros((bv.nghost, 3), np.int32))
+                bv.off, bv.nb = neigh_full(s.dim, gh, s.ntypes, self.cns)
+                if self.rev:
+                    bv.nb = _reverse_rows(bv.off, bv.nb)
+                bv.hoff, bv.hnb = half_from_full(gh, bv.off, bv.nb)
 
     def _forward(self):
         g, s = self.g, self.s
@@ -843,7 +1016,113 @@ class MpRefRun:
                                np.ascontiguousarray(g.image.ravel()), xa, None, None, None)
         self._ghost_fields()
 
+    def _ghost_x(self, bv):
+        """A rank's ghost positions as last communicated: the origin's x then plus its image
+        (one add per coordinate, as every hop adds it)."""
+        s = self.s
+        prd = np.asarray(s.boxhi, dtype=np.float64) - np.asarray(s.boxlo, dtype=np.float64)
+        nl = bv.nlocal
+        xg = self.comm["x"][bv.gid[nl:]].copy()
+        im = bv.image[nl:]
+        for d in range(3):
+            m = im[:, d] != 0
+            xg[m, d] = xg[m, d] + im[m, d] * prd[d]
+        return xg
+
+    def _reverse_bricks(self, arrs):
+        """CommBrick::reverse_comm over the grid: swaps in reverse order, every rank's ghost
+        values added onto the atoms they were copied from on the sending rank."""
+        nsw = len(self.bviews[0].swap_first) - 1
+        for sw in range(nsw - 1, -1, -1):
+            for bv in self.bviews:
+                g0, g1 = bv.swap_first[sw], bv.swap_first[sw + 1]
+                if g1 == g0:
+                    continue
+                src = int(bv.src_rank[g0])
+                np.add.at(arrs[src], bv.src_idx[g0:g1],
+                          arrs[bv.rank][bv.nlocal + g0:bv.nlocal + g1])
+
+    def _force_bricks(self):
+        """The stack rank by rank: every rank's styles see its owned atoms' fresh rho and
+        colour gradient but its ghosts' values as communicated (the styles' pack_comm moves
+        nothing) -- so which neighbours are ghosts, and hence the results,
+        depend on the decomposition.  rhosum/multiphase itself reads only x and rmass."""
+        s, ph, L = self.s, self.ph, lib()
+        nt, n = s.ntypes, s.n
+        T = self.tabs
+        c = self.comm
+        loc = []
+        for bv in self.bviews:
+            nl = bv.nlocal
+            own, gg = bv.gid[:nl], bv.gid[nl:]
+            loc.append(dict(x=np.ascontiguousarray(np.concatenate([s.x[own], self._ghost_x(bv)])),
+                            rm=np.concatenate([s.rmass[own], c["rmass"][gg]]),
+                            rho=np.concatenate([s.rho[own], c["rho"][gg]]),
+                            v=np.concatenate([s.v[own], c["v"][gg]]),
+                            e=np.concatenate([s.e[own], c["e"][gg]]),
+                            cv=np.concatenate([s.cv[own], c["cv"][gg]]),
+                            cg=np.concatenate([self.cg[own], c["cg"][gg]])))
+        if ph.rhosum_nstep > 0 and self.step % ph.rhosum_nstep == 0:
+            cc = T["rhosum_cut"]
+            for bv, a in zip(self.bviews, loc):
+                nl = bv.nlocal
+                rho = np.zeros(a["x"].shape[0])
+                L.orc_rhosum_multiphase(s.dim, nl, a["x"], bv.type, nt, a["rm"], cc, cc * cc,
+                                        bv.off, _nz(bv.nb), rho)
+                a["rho"][:nl] = rho[:nl]
+                s.rho[bv.gid[:nl]] = rho[:nl]
+        if ph.cg_nstep > 0 and self.step % ph.cg_nstep == 0:
+            cc = T["cg_cut"]
+            for bv, a in zip(self.bviews, loc):
+                nl = bv.nlocal
+                cgo = np.zeros((a["x"].shape[0], 3))
+                L.orc_colorgradient(s.dim, nl, a["x"], a["rho"], a["rm"], bv.type, nt,
+                                    T["cg_alpha"], cc, cc * cc, bv.off, _nz(bv.nb), cgo)
+                a["cg"][:nl] = cgo[:nl]
+                self.cg[bv.gid[:nl]] = cgo[:nl]
+        fs, ds = [], []
+        for bv, a in zip(self.bviews, loc):
+            nl = bv.nlocal
+            nall = a["x"].shape[0]
+            f = np.zeros((nall, 3))
+            de = np.zeros(nall)
+            if ph.tait:
+                cc = T["tait_cut"]
+                L.orc_taitwater_multiphase(s.dim, nl, 1, a["x"], np.ascontiguousarray(a["v"]),
+                                           a["rho"], bv.type, nt, a["rm"],
+                                           np.ascontiguousarray(ph.rho0, dtype=np.float64),
+                                           np.ascontiguousarray(ph.c0, dtype=np.float64), self.B,
+                                           np.ascontiguousarray(ph.gamma, dtype=np.float64),
+                                           np.ascontiguousarray(ph.rbg, dtype=np.float64),
+                                           T["visc"], cc, cc * cc, bv.hoff, _nz(bv.hnb), f)
+            if ph.st:
+                cc = T["st_cut"]
+                L.orc_surfacetension(s.dim, nl, 1, a["x"], a["rho"], a["rm"], bv.type, nt,
+                                     np.ascontiguousarray(a["cg"]), cc, cc * cc, bv.hoff,
+                                     _nz(bv.hnb), f)
+            if ph.heat:
+                cc = T["heat_cut"]
+                L.orc_heatconduction_phasechange(s.dim, nl, 1, a["x"], a["e"], a["cv"],
+                                                 a["rho"], a["rm"], bv.type, nt,
+                                                 T["heat_alpha"], T["heat_fixflag"].ctypes.data,
+                                                 T["heat_tc"].ctypes.data, cc, cc * cc, bv.hoff,
+                                                 _nz(bv.hnb), de)
+            fs.append(f)
+            ds.append(de)
+        self._reverse_bricks(fs)
+        self._reverse_bricks(ds)
+        self.f = np.zeros((n, 3))
+        self.de = np.zeros(n)
+        for bv, f, de in zip(self.bviews, fs, ds):
+            self.f[bv.gid[:bv.nlocal]] = f[:bv.nlocal]
+            self.de[bv.gid[:bv.nlocal]] = de[:bv.nlocal]
+        self.drho = np.zeros(n)
+        self.rho_all[:n] = s.rho
+        self.cg_all[:n] = self.cg
+
     def _force(self):
+        if self.pg:
+            return self._force_bricks()
         s, g, ph, L = self.s, self.g, self.ph, lib()
         nt, n, nall = s.ntypes, s.n, g.nall
         T = self.tabs
@@ -898,6 +1177,8 @@ class MpRefRun:
         over ghost slots, reverse comm along the swaps; pinned to the reference by
         tests/test_phasechange_golden.py).  Otherwise the port semantics (orc_phasechange:
         every candidate on the atoms as found)."""
+        if self.pg:
+            return self._phase_change_bricks()
         s, g, L = self.s, self.g, lib()
         n = s.n
         p = pc_params(s, self.ph.pc, self.ph.dt)
@@ -936,6 +1217,84 @@ class MpRefRun:
                 s.type = np.concatenate([s.type, np.full(nins, to, dtype=np.int32)])
                 self.cg = np.concatenate([self.cg, np.zeros((nins, 3))])   # create_atom
         if nins:
+            self.f = np.concatenate([self.f, np.zeros((nins, 3))])
+            self.drho = np.concatenate([self.drho, np.zeros(nins)])
+            self.de = np.concatenate([self.de, np.zeros(nins)])
+            self.ninserted += nins
+        return nins
+
+    def _phase_change_bricks(self):
+        """pre_exchange on every rank of the grid (orc_pre_exchange_ref up to the reverse
+        comm, on the rank's view: owned atoms as integrated, ghosts as last communicated,
+        the last build's full list), then reverse_comm_fix over the ranks' swaps in reverse
+        order, the finish loop per rank, and Atom::tag_extend: the created atoms take the
+        next tags rank by rank (atom.cpp:598-630, MPI_Scan order)."""
+        s, L = self.s, lib()
+        c = self.comm
+        res = []
+        for bv in self.bviews:
+            nl = bv.nlocal
+            own, gg = bv.gid[:nl], bv.gid[nl:]
+            xg = self._ghost_x(bv)
+            arrays = dict(x=np.concatenate([s.x[own], xg]),
+                          v=np.concatenate([s.v[own], c["v"][gg]]),
+                          vest=np.concatenate([self.vest[own], c["vest"][gg]]),
+                          cg=np.concatenate([self.cg[own], c["cg"][gg]]),
+                          e=np.concatenate([s.e[own], c["e"][gg]]),
+                          rmass=np.concatenate([s.rmass[own], c["rmass"][gg]]),
+                          rho=np.concatenate([s.rho[own], c["rho"][gg]]),
+                          cv=np.concatenate([s.cv[own], c["cv"][gg]]), type=bv.type)
+            p = pc_params(s, self.ph.pc, self.ph.dt)
+            for k in range(3):
+                p.sublo[k], p.subhi[k] = bv.lo[k], bv.hi[k]
+                p.top[k] = int(bv.loc[k] == self.pg[k] - 1)
+            extra = 64
+            while True:
+                nmax = bv.nlocal + bv.nghost + extra
+                a = {}
+                for k in ("x", "v", "vest", "cg"):
+                    a[k] = np.zeros((nmax, 3))
+                    a[k][:arrays[k].shape[0]] = arrays[k]
+                for k in ("e", "rmass", "rho", "cv"):
+                    a[k] = np.zeros(nmax)
+                    a[k][:arrays[k].shape[0]] = arrays[k]
+                a["type"] = np.zeros(nmax, dtype=np.int32)
+                a["type"][:bv.type.shape[0]] = bv.type
+                sd = C.c_int(int(self.seeds[bv.rank]))
+                dm = np.zeros(nmax)
+                ncur = L.orc_pre_exchange_ref(C.byref(p), C.byref(sd), nl, bv.nghost, nmax,
+                                              a["x"], a["v"], a["vest"], a["cg"], a["e"],
+                                              a["rmass"], a["rho"], a["cv"], a["type"], bv.off,
+                                              _nz(bv.nb), -1, np.zeros(1, np.int32),
+                                              np.zeros(1, np.int32), dm)
+                if ncur >= 0:
+                    break
+                extra *= 4
+            self.seeds[bv.rank] = sd.value
+            res.append((a, dm, ncur))
+        self._reverse_bricks([r[1] for r in res])   # reverse_comm_fix of dmass
+        new = []
+        for bv, (a, dm, ncur) in zip(self.bviews, res):
+            nl = bv.nlocal
+            own = bv.gid[:nl]
+            rm, e = a["rmass"][:nl].copy(), a["e"][:nl].copy()
+            L.orc_phasechange_finish(nl, np.ascontiguousarray(dm[:nl]), rm, e)
+            s.rmass[own] = rm
+            s.e[own] = e
+            if ncur > nl:
+                new.append({k: v[nl:ncur].copy() for k, v in a.items()})
+        nins = sum(d["x"].shape[0] for d in new)
+        if nins:
+            cat = lambda k: np.concatenate([d[k] for d in new])
+            s.x = np.concatenate([s.x, cat("x")])
+            s.v = np.concatenate([s.v, cat("v")])
+            self.vest = np.concatenate([self.vest, cat("vest")])
+            s.e = np.concatenate([s.e, cat("e")])
+            s.rmass = np.concatenate([s.rmass, cat("rmass")])
+            s.rho = np.concatenate([s.rho, cat("rho")])
+            s.cv = np.concatenate([s.cv, cat("cv")])
+            s.type = np.concatenate([s.type, cat("type")])
+            self.cg = np.concatenate([self.cg, cat("cg")])
             self.f = np.concatenate([self.f, np.zeros((nins, 3))])
             self.drho = np.concatenate([self.drho, np.zeros(nins)])
             self.de = np.concatenate([self.de, np.zeros(nins)])

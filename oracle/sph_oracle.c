@@ -1244,6 +1244,9 @@ int orc_pre_exchange_ref(const orc_pc_params *p, int *seed, int nlocal, int ngho
     e[i] = energy_aux;
     e[m] = energy_aux;
   }
+  /* nswap < 0: one rank of several -- stop here with the ghosts' dmass in place; the
+     caller runs reverse_comm_fix across the ranks' swaps and the finish loop */
+  if (nswap < 0) return ncur;
   orc_reverse_swaps(nlocal, nswap, swap_first, ghost_src, dmass);   /* :324 */
   for (int i = 0; i < nlocal; i++) {
     const double mold = rmass[i];

@@ -126,3 +126,32 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                         "--dry-run"], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def _visible_devices():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "sph_amd_probe", os.path.join(ROOT, "lammps-sph-multiphase_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.device_count()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["c2", "c5"])
+def test_bench_two_gpus(workload):
+    """`bench.py --gpus 2` over RCCL when the box shows two devices (the driver's multi-GPU
+    node); skipped on a one-GPU box, where two RCCL ranks cannot share the card."""
+    import subprocess
+    probe = subprocess.run([sys.executable, "-c",
+                            "import test_multi_rank as t; print(t._visible_devices())"],
+                           cwd=os.path.dirname(__file__), capture_output=True, text=True,
+                           timeout=240)
+    ndev = int(probe.stdout.strip().splitlines()[-1]) if probe.returncode == 0 else 0
+    if ndev < 2:
+        pytest.skip(f"{ndev} HIP device(s) visible")
+    args = ["--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu", "--workload", workload]
+    if workload == "c5":
+        args += ["--edge", "60"]
+    out = _bench_json(args)
+    assert out["n_gpus"] == 2 and out["value"] > 0

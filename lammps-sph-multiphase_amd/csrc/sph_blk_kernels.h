@@ -825,6 +825,36 @@ struct BlkSlots {
     }
   }
 };
+// walk2: the same slots, but each record is read by load(slot) and used by body(record); with
+// SPH_BLK_PIPE a lane's U records of a chunk are all read before the first is used (U
+// independent pair evaluations in flight, the LDS latency covered by the next pairs' reads)
+#ifndef SPH_BLK_PIPE
+#define SPH_BLK_PIPE 1
+#endif
+template <int G, int U, int NCH, class Load, class Body>
+__device__ __forceinline__ void blk_walk2(BlkSlots<G, U, NCH> &sw, int c, int lane, Load load,
+                                          Body body) {
+  if (NCH > 0 && SPH_BLK_PIPE) {
+#pragma unroll
+    for (int k = 0; k < (NCH > 0 ? NCH : 1); k++) {
+      if (k * U * G >= c) break;
+      decltype(load(0)) r[U];
+#pragma unroll
+      for (int q = 0; q < U; q++) r[q] = load(SlotWord<U>::get(sw.w[k], q));
+#pragma unroll
+      for (int q = 0; q < U; q++) body(r[q]);
+    }
+  } else {
+    sw.walk(c, lane, [&](int q, bool) { body(load(q)); });
+  }
+}
+// a neighbour's record in the force pass's image (blk_put layout)
+struct BlkRec {
+  double2 a0, a1, a2, a3;
+  double e;
+  int q;
+};
+
 // union positions staged from registers loaded ahead of the slot rows (the rest, for
 // unions over BLK_SP*threads atoms, in a plain loop)
 constexpr int BLK_SP = 2;
@@ -1002,8 +1032,20 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
 // EXP (study builds, SPH_EXP): 1 = neighbour records synthesised from the slot (no LDS
 // reads), 2 = LDS reads with a trivial body, 3 = no staging loads (LDS image left as is).
 // Outputs meaningless.
+// Occupancy the pair passes really get: the LDS image (~64 KiB at C2) admits two 512-thread
+// workgroups per CU, i.e. 4 waves per SIMD -- told to the compiler so that it schedules for
+// that (loads further ahead, up to 128 VGPRs) instead of for the 6-8 waves VGPRs alone allow
+#ifndef SPH_BLK_WPE
+#define SPH_BLK_WPE 0
+#endif
+#if SPH_BLK_WPE > 0
+#define SPH_BLK_OCC __attribute__((amdgpu_waves_per_eu(SPH_BLK_WPE, SPH_BLK_WPE)))
+#else
+#define SPH_BLK_OCC
+#endif
+
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
-__global__ void __launch_bounds__(R * G)
+__global__ void __launch_bounds__(R * G) SPH_BLK_OCC
 k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
             const unsigned short *__restrict__ snbr, int sstride,
             const int *__restrict__ rcnt, const double4 *__restrict__ xf,
@@ -1088,21 +1130,28 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   // the heat terms.  One type: sp = (P_i/rho_i^2 + P_j/rho_j^2 [+ fvisc]) w, the row's
   // factors applied at the end; several types: sp, sv, D and EH terms carry them per pair.
   double fx = 0.0, fy = 0.0, fz = 0.0, D = 0.0, E = 0.0, EH = 0.0;
-  sw.walk(c, lane, [&](int q, bool) {
+  auto load = [&](int q) {
     const unsigned char *const rec = blk_smem + q * 16;
-    double2 a0, a1, a2, a3;
+    BlkRec r;
+    r.q = q;
     if (EXP == 1) {
       const double o = (double)(q & 7);
-      a0 = make_double2(xi.x + 0.25 * o, xi.y + 0.5);
-      a1 = make_double2(xi.z - 0.125 * o, xi.w);
-      a2 = make_double2(vi.x, vi.y - 0.01 * o);
-      a3 = make_double2(vi.z, vi.w);
+      r.a0 = make_double2(xi.x + 0.25 * o, xi.y + 0.5);
+      r.a1 = make_double2(xi.z - 0.125 * o, xi.w);
+      r.a2 = make_double2(vi.x, vi.y - 0.01 * o);
+      r.a3 = make_double2(vi.z, vi.w);
     } else {
-      a0 = *reinterpret_cast<const double2 *>(rec);
-      a1 = *reinterpret_cast<const double2 *>(rec + 256);
-      a2 = *reinterpret_cast<const double2 *>(rec + 512);
-      a3 = *reinterpret_cast<const double2 *>(rec + 768);
+      r.a0 = *reinterpret_cast<const double2 *>(rec);
+      r.a1 = *reinterpret_cast<const double2 *>(rec + 256);
+      r.a2 = *reinterpret_cast<const double2 *>(rec + 512);
+      r.a3 = *reinterpret_cast<const double2 *>(rec + 768);
     }
+    r.e = HEAT ? *reinterpret_cast<const double *>(rec + 1024) : 0.0;
+    return r;
+  };
+  blk_walk2(sw, c, lane, load, [&](const BlkRec &rc) {
+    const int q = rc.q;
+    const double2 a0 = rc.a0, a1 = rc.a1, a2 = rc.a2, a3 = rc.a3;
     if (EXP == 2) {
       fx += a0.x + a2.x;
       fy += a0.y + a2.y;
@@ -1144,7 +1193,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       const HeatPair cc = NT1 ? h1 : s_hp[pidx];
       const double d = fmax(cc.h - r, 0.0);
       const double w = NT1 ? d * d : cc.wK * (d * d);
-      const double ej = *reinterpret_cast<const double *>(rec + 1024);
+      const double ej = rc.e;
       const double t = ((vi.w + a3.y) * rcp1(vi.w * a3.y)) * ((ei - ej) * w);
       EH += NT1 ? t : cc.hmD * t;
     }
@@ -1197,11 +1246,23 @@ static __global__ void k_blk_large_dev(int nb, const int *__restrict__ ucnt, int
 // Block shapes (rows per block R, lanes per row G, slots per lane and chunk U); SPH_BLK
 // picks one (tuning).  R*G threads per pair-pass workgroup.
 #ifdef SPH_STUDY
-#define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4) X(2, 32, 16, 2)
+#define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4) X(2, 32, 16, 2) X(3, 64, 16, 4) X(4, 32, 16, 4)
 #else
 #define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4)
 #endif
 constexpr int BLK_NCH = 8;  // slot chunks preloaded per row (rows up to BLK_NCH*U*G entries)
+// The pair passes walk a row in chunks of BLK_WALK_U * G entries (the build pads rows to
+// U * G): with 16-entry chunks a row of c entries costs ceil(c/16)*16 pair evaluations
+// instead of ceil(c/32)*32 -- measured slower (16-entry walk: force 0.457 vs 0.287 ms at
+// C2, profiles/r03/README.md), so the walk stays at the build's U
+#ifndef SPH_BLK_WALK_U
+#define SPH_BLK_WALK_U 4
+#endif
+template <int U>
+struct BlkWalk {
+  static constexpr int UW = (U > SPH_BLK_WALK_U) ? SPH_BLK_WALK_U : U;
+  static constexpr int NCH = BLK_NCH * U / UW;
+};
 struct BlkShape {
   int R, G, U;
 };
@@ -1334,11 +1395,12 @@ template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
                          double4 *vr, const Coefs *cf) {
   const bool pre = k.pre(BlkShape{R, G, U});
+  constexpr int UW = BlkWalk<U>::UW, NW = BlkWalk<U>::NCH;
   if (nt1) {
-    if (pre) blk_rhosum_t<R, G, U, BLK_NCH, true>(s, k, xf, ty, vr, cf);
+    if (pre) blk_rhosum_t<R, G, UW, NW, true>(s, k, xf, ty, vr, cf);
     else blk_rhosum_t<R, G, U, 0, true>(s, k, xf, ty, vr, cf);
   } else {
-    if (pre) blk_rhosum_t<R, G, U, BLK_NCH, false>(s, k, xf, ty, vr, cf);
+    if (pre) blk_rhosum_t<R, G, UW, NW, false>(s, k, xf, ty, vr, cf);
     else blk_rhosum_t<R, G, U, 0, false>(s, k, xf, ty, vr, cf);
   }
 }
@@ -1429,11 +1491,12 @@ template <int R, int G, int U>
 inline void blk_force_s(bool nt1, int visc, int mode, hipStream_t s, const BlkArgs &k,
                         const RowArgs &a) {
   const bool pre = k.pre(BlkShape{R, G, U});
+  constexpr int UW = BlkWalk<U>::UW, NW = BlkWalk<U>::NCH;
   if (nt1) {
-    if (pre) blk_force_n<R, G, U, BLK_NCH, true>(visc, mode, s, k, a);
+    if (pre) blk_force_n<R, G, UW, NW, true>(visc, mode, s, k, a);
     else blk_force_n<R, G, U, 0, true>(visc, mode, s, k, a);
   } else {
-    if (pre) blk_force_n<R, G, U, BLK_NCH, false>(visc, mode, s, k, a);
+    if (pre) blk_force_n<R, G, UW, NW, false>(visc, mode, s, k, a);
     else blk_force_n<R, G, U, 0, false>(visc, mode, s, k, a);
   }
 }

@@ -28,6 +28,9 @@
 using namespace sph;
 
 namespace sph {
+#ifndef SPH_INNER_FRAC
+#define SPH_INNER_FRAC 0.0625
+#endif
 static int env_int(const char *name, int dflt) {
   const char *s = getenv(name);
   return s ? atoi(s) : dflt;
@@ -1247,7 +1250,7 @@ struct sph_engine {
       // k_blk_build (ballots, inner rows in the same pass); the bitmap walk k_blk_neigh for
       // the large candidate image (and in study builds, SPH_BUILD=0)
       const bool v2 = !big && study_int("SPH_BUILD", 1) != 0;
-      const bool want_inner = inner_margin > 0.0 && !multi();
+      const bool want_inner = inner_margin > 0.0;
       if (v2 && want_inner) {
         snbi.reserve((size_t)n * blk_sstride + 2 * chunk);
         icnt.reserve(n);
@@ -1354,23 +1357,23 @@ struct sph_engine {
   }
 
   // The block path's inner rows (sph_blk_kernels.h k_blk_inner), written after every block
-  // build: the pair passes walk them while no atom has moved inner_margin / 2 since (one
-  // brick: ghosts move with their owners; bricks keep the full rows for now).
+  // build: the pair passes walk them while no atom has moved inner_margin / 2 since (owned
+  // atoms: checked by the integrate kernels; bricks: the ghosts after each forward comm).
   void build_inner() {
-    inner = blk && inner_margin > 0.0 && !multi() && nlocal > 0;
+    inner = blk && inner_margin > 0.0 && nlocal > 0;
     sc.x0 = nullptr;
     if (!inner) return;
     const BlkShape sh = blk_shape(blk_sh);
     snbi.reserve((size_t)nlocal * blk_sstride + 2 * sh.U * sh.G);
     icnt.reserve(nlocal);
     moved.reserve(1);
-    x0.reserve(nlocal);
+    const size_t nx0 = (size_t)nlocal + (multi() ? nghost : 0);
+    x0.reserve(nx0);
     if (!inner_written) {
       BlkArgs k = blk_args();
       blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
     }
-    SPH_HIP_TRY(hipMemcpyAsync(x0.p, xf.p, (size_t)nlocal * sizeof(double4),
-                               hipMemcpyDeviceToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(x0.p, xf.p, nx0 * sizeof(double4), hipMemcpyDeviceToDevice, s));
     SPH_HIP_TRY(hipMemsetAsync(moved.p, 0, sizeof(int), s));
     sc.x0 = x0.p;
     sc.lim2 = 0.25 * inner_margin * inner_margin;
@@ -1452,6 +1455,9 @@ struct sph_engine {
     if (multi()) {
       Scope t(this, T_COMM);
       forward_multi();
+      if (inner && sc.x0 && nghost)
+        hipLaunchKernelGGL(k_inner_ghosts, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost,
+                           nlocal, sc, xf.p);
       return;
     }
     if (nghost == 0) return;
@@ -2136,8 +2142,10 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     // mirror upper triangle into a symmetric max-cut table (init_one semantics)
     for (int i = 1; i <= nt; i++)
       for (int j = 1; j < i; j++) cutmax[i * (nt + 1) + j] = cutmax[j * (nt + 1) + i];
-    // inner rows of the block path: a quarter of the skin (sph_blk_kernels.h k_blk_inner)
-    e->inner_margin = 0.25 * cfg->skin;
+    // inner rows of the block path (sph_blk_kernels.h k_blk_inner): a sixteenth of the skin
+    // -- rows of ~110 instead of ~120 entries at C2 (with 16-entry walk chunks 114.5 instead
+    // of 128 pair evaluations), valid while no atom has moved skin/32 since the build
+    e->inner_margin = SPH_INNER_FRAC * cfg->skin;
     e->cutneighmax = coef_cutneigh(c, nt, cutmax.data(), cfg->skin, e->inner_margin);
     for (int k = 0; k < NT2; k++)  // tight-list test: the largest force-style cutoff
       c.fcutsq[k] = std::max((e->force_mode & M_TAIT) ? c.tait[k].cutsq : 0.0,

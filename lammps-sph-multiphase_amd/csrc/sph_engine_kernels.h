@@ -28,6 +28,16 @@ __device__ __forceinline__ void inner_check(const StepConst &sc, int i, const do
   if (dx * dx + dy * dy + dz * dz > sc.lim2) atomicOr(sc.moved, 1);
 }
 
+// bricks: the ghosts' positions arrive from other ranks, so their displacement since the
+// inner rows were written is checked after each forward comm (one brick: a ghost moves with
+// the owned atom it images, which the integrate kernels check)
+static __global__ void k_inner_ghosts(int ng, int nlocal, StepConst sc,
+                                      const double4 *__restrict__ xf) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  inner_check(sc, nlocal + g, xf[nlocal + g]);
+}
+
 // FixMeso::initial_integrate (fix_meso.cpp:91-140) / FixMesoStationary (:71-90)
 static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restrict__ xf,
                                            double4 *__restrict__ vr, double *__restrict__ en,

@@ -1,9 +1,9 @@
 #!/bin/bash
-# C5 engine tests, then a short C5 bench at a given edge (default 60) and the 4.02M one
+# C5 at 4.02M on one GPU: bench line + rocprofv3 kernel stats into gpurun_out/r03.
 cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}" || exit 1
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_c5_engine.py -x -q --timeout 240 --timeout-method thread -m gpu > gpurun_out/c5.log 2>&1 || { grep -E "Error|error|FAILED|passed|failed|assert" gpurun_out/c5.log | head -20; exit 1; }
-tail -1 gpurun_out/c5.log
-timeout -k 10 200 python3 bench.py --workload c5 --edge ${1:-60} --steps 5 --warmup 2 --no-cpu 2>gpurun_out/c5b.err | tee gpurun_out/c5_small.json || { tail -5 gpurun_out/c5b.err; exit 1; }
-[ -n "$2" ] && timeout -k 10 400 python3 bench.py --workload c5 --edge $2 --steps ${3:-10} --warmup 2 2>>gpurun_out/c5b.err | tee gpurun_out/c5_big.json
-exit 0
+R=$(pwd); O=$R/gpurun_out/r03; mkdir -p "$O"
+timeout -k 10 600 python3 bench.py --workload c5 --steps 10 --warmup 3 > "$O/bench_c5.json" 2> "$O/bench_c5.err" || { tail -5 "$O/bench_c5.err"; exit 1; }
+echo "c5: $(cut -c1-300 "$O/bench_c5.json")"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c5" -o c5 -- python3 "$R/bench.py" --workload c5 --steps 5 --warmup 2 --no-cpu > "$O/bench_c5_prof.json" 2> "$O/prof_c5.err" || exit 1
+cd "$R" && python3 tools/kstats.py "$(find "$O/prof_c5" -name '*kernel_stats.csv' | head -1)" 25

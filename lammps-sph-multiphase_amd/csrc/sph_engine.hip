@@ -21,6 +21,7 @@
 #include "sph_blk_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_engine_mp.h"
+#include "sph_mp2_kernels.h"
 #include "sph_pc.h"
 #include "sph_row2_kernels.h"
 #include "sph_util.h"
@@ -1696,7 +1697,7 @@ struct sph_engine {
       if (rdue) {
         rho_tmp.reserve(nall);
         a.rho = rho_tmp.p;
-        hipLaunchKernelGGL(k_mp_rhosum<8>, mp_rows(n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mp2_rhosum<8>, mp_rows(n), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_mp_rho_store, dim3(blocks(n)), dim3(BLK), 0, s, n, rho_tmp.p, vr.p);
       }
       if (cdue) {
@@ -1705,7 +1706,7 @@ struct sph_engine {
         hipLaunchKernelGGL(k_mp_pack_sigma, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vr.p,
                            rm.p, recA.p);
         a.xs = recA.p;
-        hipLaunchKernelGGL(k_mp_colorgradient<8>, mp_rows(n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mp2_colorgradient<8>, mp_rows(n), dim3(256), 0, s, a);
         a.xs = nullptr;
       }
     }
@@ -1738,17 +1739,27 @@ struct sph_engine {
     recK.reserve(nall);
     recF.reserve(nall);
     recS.reserve(nall);
-    hipLaunchKernelGGL(k_mp_pack_rec, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vel.p,
-                       rm.p, en.p, cvv.p, rF, rhoS.p, cF, cgS.p, mpc.heat_on ? 1 : 0, recA.p,
-                       recK.p, recF.p, recS.p);
+    // symmetric styles (mp2_symmetric): the issue-rate gather of sph_mp2_kernels.h
+    const bool sym = mp2_symmetric(hm);
+    if (sym)
+      hipLaunchKernelGGL(k_mp2_pack_rec, dim3(blocks(nall)), dim3(BLK), 0, s, nall, cfg.dim,
+                         xf.p, vel.p, rm.p, en.p, cvv.p, rF, rhoS.p, cF, cgS.p,
+                         mpc.heat_on ? 1 : 0, recA.p, recK.p, recF.p, recS.p);
+    else
+      hipLaunchKernelGGL(k_mp_pack_rec, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vel.p,
+                         rm.p, en.p, cvv.p, rF, rhoS.p, cF, cgS.p, mpc.heat_on ? 1 : 0, recA.p,
+                         recK.p, recF.p, recS.p);
     h.pA = recA.p;
     h.pK = recK.p;
     h.pF = recF.p;
     h.pS = recS.p;
     const int sel = (mpc.tait_on ? 1 : 0) | (mpc.st_on ? 2 : 0) | (mpc.heat_on ? 4 : 0);
     switch (sel) {
-#define SPH_MPG(k, T, S, H) \
-  case k: hipLaunchKernelGGL((k_mp_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h); break;
+#define SPH_MPG(k, T, S, H)                                                                   \
+  case k:                                                                                     \
+    if (sym) hipLaunchKernelGGL((k_mp2_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);  \
+    else hipLaunchKernelGGL((k_mp_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);       \
+    break;
       SPH_MPG(1, true, false, false)
       SPH_MPG(2, false, true, false)
       SPH_MPG(3, true, true, false)

@@ -1,0 +1,333 @@
+// sph_mp2_kernels.h -- the engine's multiphase passes (C5, bubble_growth stack), written for
+// the issue rate: the row kernels of sph_mp_kernels.h spend ~300 VALU instructions per pair
+// in the fused gather (profiles/r03: 543 M wave-instructions for 1M rows) on branchy quintic
+// pieces, per-pair coefficient loads with lane-varying indices and the swaps that put each
+// pair in its half-list orientation.  Here
+//   * the quintic kernel and its derivative are branch-free, in the factored form
+//     W(s) ~ a^5 - 6 b^5 + 15 c^5, dW/ds ~ -5 a^4 + 30 b^4 - 75 c^4 with a = max(3-s, 0),
+//     b = max(2-s, 0), c = max(1-s, 0) -- algebraically the reference's piecewise
+//     polynomials (sph_kernel_quintic.cpp:17-73), without their cancellation near s = 3;
+//     zero beyond the cutoff, so the cut test rides on the weight;
+//   * the per-pair-type coefficients sit in LDS, loaded once per workgroup;
+//   * when every style is symmetric under exchanging the pair's atoms (all gamma equal, so
+//     the p_j-with-gamma[itype] quirk is moot, and no type pinned to its own type's Tc) a
+//     pair is evaluated with i as the row atom whatever its half-list orientation: the
+//     orientation then only selects the fresh or stale rho / colour gradient of each side
+//     (k_mp_gather's comment); otherwise the engine keeps k_mp_gather;
+//   * the surface stress S = (|c|^2/ndim e - (c.e) c)/|c| (pair_sph_surfacetension.cpp:
+//     135-168, same vector, the reference's terms collected) reads w = c/sqrt(|c|) from the
+//     records (|w|^2 = |c|, (w.e) w = (c.e) c/|c|): no square root or division per pair.
+// The fields agree with the reference restatement to rounding (~1e-15 relative per pair);
+// the parity bar of the C5 tests is 1e-10.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "sph_kernels.h"
+#include "sph_mp_kernels.h"
+
+namespace sph {
+
+// quintic W(s) and dW/ds without the norm (s = 3 r / h)
+__device__ __forceinline__ double q5_w(double s) {
+  const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
+  const double a2 = a * a, b2 = b * b, c2 = c * c;
+  return fma(15.0 * c2 * c2, c, fma(-6.0 * b2 * b2, b, a2 * a2 * a));
+}
+__device__ __forceinline__ double q5_dw(double s) {
+  const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
+  const double a2 = a * a, b2 = b * b, c2 = c * c;
+  return fma(-75.0 * c2, c2, fma(30.0 * b2, b2, -5.0 * (a2 * a2)));
+}
+
+// per pair type: the stack's cutoffs (squared), 1/h and the coefficients the pair terms use
+struct Mp2Pair {
+  double rcsq, rih;           // rhosum/multiphase
+  double ccsq, cih, calpha;   // colorgradient
+  double tcsq, tih, tvisc;    // taitwater/multiphase
+  double scsq, sih;           // surfacetension
+  double hcsq, hih, halpha2;  // heatconduction/phasechange (2 alpha)
+  double htc;
+  int hfix, pad;
+};
+struct Mp2Type {
+  double B, rho0i, gamma, rbg;
+};
+
+// stage the tables of pair types and types into LDS (every thread of the block calls it)
+__device__ __forceinline__ void mp2_tables(const MpCoefs *c, Mp2Pair *sp, Mp2Type *st) {
+  const int nt1 = c->ntypes + 1;
+  for (int p = threadIdx.x; p < nt1 * nt1; p += blockDim.x) {
+    Mp2Pair q;
+    q.rcsq = c->rcutsq[p];
+    q.rih = c->rcut_inv[p];
+    q.ccsq = c->ccutsq[p];
+    q.cih = c->ccut_inv[p];
+    q.calpha = c->calpha[p];
+    q.tcsq = c->tcutsq[p];
+    q.tih = c->tcut_inv[p];
+    q.tvisc = c->tvisc[p];
+    q.scsq = c->scutsq[p];
+    q.sih = c->scut_inv[p];
+    q.hcsq = c->hcutsq[p];
+    q.hih = c->hcut_inv[p];
+    q.halpha2 = 2.0 * c->halpha[p];
+    q.htc = c->htc[p];
+    q.hfix = c->hfix[p];
+    q.pad = 0;
+    sp[p] = q;
+  }
+  for (int t = threadIdx.x; t < nt1; t += blockDim.x)
+    st[t] = Mp2Type{c->B[t], c->rho0_inv[t], c->gamma[t], c->rbg[t]};
+  __syncthreads();
+}
+
+// h^-dim (W) and h^-(dim+1) (dW) with the norms of sph_kernel_quintic.cpp
+__device__ __forceinline__ double mp2_wnorm(int dim, double ih) {
+  return dim == 3 ? 0.0716197243913529 * (ih * ih * ih) : 0.04195297663091802 * (ih * ih);
+}
+__device__ __forceinline__ double mp2_dwnorm(int dim, double ih) {
+  const double ih2 = ih * ih;
+  return dim == 3 ? 3.0 * 0.0716197243913529 * (ih2 * ih2) : 3.0 * 0.04195297663091802 * (ih2 * ih);
+}
+
+// rhosum/multiphase (pair_sph_rhosum_multiphase.cpp:118-167) over the engine's strided /
+// CSR full rows: rho_i = rmass_i (W(0)/h^dim + sum_j W(r/h)/h^dim), two entries per lane and
+// round with both loads issued first
+template <int G>
+__global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
+  __shared__ Mp2Pair s_p[NT2];
+  __shared__ Mp2Type s_t[MAXT + 1];
+  mp2_tables(a.mc, s_p, s_t);
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const int nt1 = a.mc->ntypes + 1, dim = a.dim;
+  const int i = a.ilist ? a.ilist[row] : row;
+  const double4 xi = a.xf[i];
+  const int it = a.ty[i];
+  const Mp2Pair *const pi = s_p + it * nt1;
+  double acc = 0.0;
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  constexpr int NU = 2;
+  for (int k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
+    double4 xj[NU];
+    int tj[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int j = (k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg]) & MP_NMASK;
+      xj[u] = a.xf[j];
+      tj[u] = a.ty[j];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      if (k0 + u * G >= rw.end) break;
+      const Mp2Pair &q = pi[tj[u]];
+      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      if (rsq < q.rcsq) acc += q5_w(3.0 * (sqrt(rsq) * q.rih)) * mp2_wnorm(dim, q.rih);
+    }
+  }
+  acc = group_sum<G>(acc);
+  if (lane == 0) {
+    const Mp2Pair &q = pi[it];
+    a.rho[i] = (q5_w(0.0) * mp2_wnorm(dim, q.rih) + acc) * a.rm[i];
+  }
+}
+
+// colorgradient (pair_sph_colorgradient.cpp:139-181) over the same rows: records (x, sigma)
+template <int G>
+__global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
+  __shared__ Mp2Pair s_p[NT2];
+  __shared__ Mp2Type s_t[MAXT + 1];
+  mp2_tables(a.mc, s_p, s_t);
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const int nt1 = a.mc->ntypes + 1, dim = a.dim;
+  const int i = a.ilist ? a.ilist[row] : row;
+  const double4 xi = a.xs[i];
+  const int it = a.ty[i];
+  const Mp2Pair *const pi = s_p + it * nt1;
+  const double sigmai = xi.w;
+  double gx = 0.0, gy = 0.0, gz = 0.0;
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  constexpr int NU = 2;
+  for (int k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
+    double4 xj[NU];
+    int tj[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int j = (k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg]) & MP_NMASK;
+      xj[u] = a.xs[j];
+      tj[u] = a.ty[j];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      if (k0 + u * G >= rw.end) break;
+      const Mp2Pair &q = pi[tj[u]];
+      if (q.calpha == 0.0) continue;
+      const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      if (!(rsq < q.ccsq)) continue;
+      const double r = sqrt(rsq);
+      const double wfd = q5_dw(3.0 * (r * q.cih)) * mp2_dwnorm(dim, q.cih);
+      const double sj = xj[u].w;
+      const double dphi = -wfd * q.calpha * mp_rcp(sj * sj) * sigmai * mp_rcp(r);
+      gx += dphi * dx;
+      gy += dphi * dy;
+      if (dim == 3) gz += dphi * dz;
+    }
+  }
+  gx = group_sum<G>(gx);
+  gy = group_sum<G>(gy);
+  gz = group_sum<G>(gz);
+  if (lane == 0) a.cg[i] = make_double4(gx, gy, gz, 0.0);
+}
+
+// the gather's fresh / stale records of (colour gradient, rho): w = c / sqrt(|c|), zero where
+// |c| <= EPSILON = 1e-12 (pair_sph_surfacetension.cpp:29) -- see the header
+__device__ __forceinline__ double4 mp2_wrec(const double4 c, double rho, int dim) {
+  const double c2 = dim == 3 ? c.x * c.x + c.y * c.y + c.z * c.z : c.x * c.x + c.y * c.y;
+  const double ac = sqrt(c2);
+  if (!(ac > 1.0e-12)) return make_double4(0.0, 0.0, 0.0, rho);
+  const double f = 1.0 / sqrt(ac);
+  return make_double4(c.x * f, c.y * f, dim == 3 ? c.z * f : 0.0, rho);
+}
+static __global__ void k_mp2_pack_rec(int nall, int dim, const double4 *__restrict__ xf,
+                                      const double4 *__restrict__ vel,
+                                      const double *__restrict__ rm, const double *__restrict__ en,
+                                      const double *__restrict__ cv,
+                                      const double *__restrict__ rhoF,
+                                      const double *__restrict__ rhoS,
+                                      const double4 *__restrict__ cgF,
+                                      const double4 *__restrict__ cgS, int heat,
+                                      double4 *__restrict__ A, double4 *__restrict__ K,
+                                      double4 *__restrict__ F, double4 *__restrict__ S) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nall) return;
+  const double4 x = xf[i], v = vel[i];
+  A[i] = make_double4(x.x, x.y, x.z, rm[i]);
+  K[i] = make_double4(v.x, v.y, v.z, heat ? en[i] / cv[i] : 0.0);  // (sph_energy2t)
+  F[i] = mp2_wrec(cgF[i], rhoF[i], dim);
+  S[i] = mp2_wrec(cgS[i], rhoS[i], dim);
+}
+
+// S(w, e) V^2 with |w|^2 = |c|: (|c| e / ndim - (c.e) c / |c|) V^2
+__device__ __forceinline__ double3 mp2_svec(int dim, const double4 &w, double3 e, double v2) {
+  const double w2 = w.x * w.x + w.y * w.y + w.z * w.z;
+  const double we = w.x * e.x + w.y * e.y + w.z * e.z;
+  const double a = (dim == 3 ? (1.0 / 3.0) : 0.5) * w2 * v2, b = we * v2;
+  return make_double3(a * e.x - b * w.x, a * e.y - b * w.y, dim == 3 ? a * e.z - b * w.z : 0.0);
+}
+
+// taitwater/multiphase + surfacetension + heatconduction/phasechange fused over the full
+// rows, symmetric styles only (see the header; k_mp_gather otherwise).  Per pair (i = row,
+// j = entry; bit 31 = the pair is i's in the half list): i's values fresh unless j is a ghost
+// whose image pair belongs to j's owner, j's fresh if owned or if the pair is not i's -- the
+// pair terms themselves with i first.
+template <int G, bool TAIT, bool SURF, bool HEAT>
+__global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
+  __shared__ Mp2Pair s_p[NT2];
+  __shared__ Mp2Type s_t[MAXT + 1];
+  mp2_tables(a.mc, s_p, s_t);
+  const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
+  const int lane = threadIdx.x & (G - 1);
+  if (row >= a.inum) return;
+  const int nt1 = a.mc->ntypes + 1, dim = a.dim;
+  const int i = a.ilist ? a.ilist[row] : row;
+  const double4 xi = a.pA[i], v4i = a.pK[i];
+  const int ti = a.ty[i];
+  const Mp2Pair *const pi = s_p + ti * nt1;
+  const Mp2Type tyi = s_t[ti];
+  const double mi = xi.w, Ti = v4i.w;
+  const double4 cFi = a.pF[i], cSi = a.pS[i];
+  double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
+  constexpr int NU = 2;
+  const MpRow rw(a.off, a.cnt, a.stride, row);
+  const int kend = rw.end;
+  for (int k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
+    int jrs[NU], tjs[NU];
+    double4 xjs[NU], v4js[NU], cjs[NU];
+#pragma unroll
+    for (int u = 0; u < NU; u++) jrs[u] = k0 + u * G < kend ? a.nbr[k0 + u * G] : a.nbr[rw.beg];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const int j = jrs[u] & MP_NMASK;
+      const bool fj = j < a.nlocal || jrs[u] >= 0;
+      xjs[u] = a.pA[j];
+      v4js[u] = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
+      cjs[u] = (fj ? a.pF : a.pS)[j];
+      tjs[u] = a.ty[j];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      if (k0 + u * G >= kend) break;
+      const int jr = jrs[u], j = jr & MP_NMASK;
+      const bool fi = !(j >= a.nlocal && jr >= 0);
+      const double4 xj = xjs[u], v4j = v4js[u], cj = cjs[u];
+      const double4 ci = fi ? cFi : cSi;
+      const Mp2Pair &q = pi[tjs[u]];
+      const double rhoi = ci.w, rhoj = cj.w, mj = xj.w;
+      const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      const bool ct = TAIT && rsq < q.tcsq, cs = SURF && rsq < q.scsq, ch = HEAT && rsq < q.hcsq;
+      if (!(ct || cs || ch)) continue;
+      const double r = sqrt(rsq), ir = mp_rcp(r);
+      const double qt = ct ? q5_dw(3.0 * (r * q.tih)) * mp2_dwnorm(dim, q.tih) : 0.0;
+      const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt
+                                    : q5_dw(3.0 * (r * q.sih)) * mp2_dwnorm(dim, q.sih);
+      const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt
+                                   : q5_dw(3.0 * (r * q.hih)) * mp2_dwnorm(dim, q.hih);
+      const double iri = mp_rcp(rhoi), irj = mp_rcp(rhoj);
+      const double Vi = mi * iri, Vj = mj * irj;
+      const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
+      if (ct) {  // pair_sph_taitwater_multiphase.cpp:128-170
+        const Mp2Type tyj = s_t[tjs[u]];
+        const double pI = tyi.B * ((tyi.gamma == 1.0 ? rhoi * tyi.rho0i
+                                                      : pow(rhoi * tyi.rho0i, tyi.gamma)) - tyi.rbg);
+        const double pJ = tyj.B * ((tyi.gamma == 1.0 ? rhoj * tyj.rho0i
+                                                      : pow(rhoj * tyj.rho0i, tyi.gamma)) - tyj.rbg);
+        const double pij = (rhoj * pI + rhoi * pJ) * mp_rcp(rhoi + rhoj);
+        const double wfd = qt * ir, V2 = Vi2 + Vj2;
+        const double fvisc = V2 * q.tvisc * wfd, fpair = -V2 * pij * wfd;
+        fx += dx * fpair + (v4i.x - v4j.x) * fvisc;
+        fy += dy * fpair + (v4i.y - v4j.y) * fvisc;
+        fz += dz * fpair + (v4i.z - v4j.z) * fvisc;
+      }
+      if (SURF && cs) {  // pair_sph_surfacetension.cpp:100-190
+        const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
+        const double3 Si = mp2_svec(dim, ci, e, Vi2), Sj = mp2_svec(dim, cj, e, Vj2);
+        fx += (Si.x + Sj.x) * qs;
+        fy += (Si.y + Sj.y) * qs;
+        if (dim == 3) fz += (Si.z + Sj.z) * qs;
+      }
+      if (HEAT && ch) {  // pair_sph_heatconduction_phasechange.cpp:101-136
+        double Tp = Ti, Tq = v4j.w;
+        if (q.hfix == ti && Tp < Tq) Tp = q.htc;
+        if (q.hfix == tjs[u] && Tq < Tp) Tq = q.htc;
+        dE += q.halpha2 * (Tp - Tq) * (qh * ir) * (iri * irj) * mj;
+      }
+    }
+  }
+  fx = group_sum<G>(fx);
+  fy = group_sum<G>(fy);
+  fz = group_sum<G>(fz);
+  dE = group_sum<G>(dE);
+  if (lane == 0) {
+    if (TAIT || SURF) a.fo[i] = make_double4(fx, fy, fz, 0.0);
+    if (HEAT) a.de[i] = dE;
+  }
+}
+
+// the styles are symmetric under exchanging a pair's atoms (k_mp2_gather applies): every
+// gamma equal, and no type pinned to Tc against its own type
+inline bool mp2_symmetric(const MpCoefs &c) {
+  const int nt1 = c.ntypes + 1;
+  for (int t = 2; t <= c.ntypes; t++)
+    if (c.gamma[t] != c.gamma[1]) return false;
+  for (int t = 1; t <= c.ntypes; t++)
+    if (c.hfix[t * nt1 + t] == t) return false;
+  return true;
+}
+
+}  // namespace sph

@@ -65,6 +65,9 @@ struct ForceArgs {
   double gx, gy, gz;
   double *virial;
   int nojside = 0;  // HALF: i share only, no atomics (two-pass reverse-list mode)
+  // setup step, full list: owned atoms' vest before setup_pre_force, ghosts' vest as
+  // borders() left it (k_force's setup comment); nullptr otherwise
+  const double4 *vso = nullptr, *vsg = nullptr;
 };
 
 template <int G, int DIM, int VISC, int MODE, bool NT1>
@@ -72,7 +75,7 @@ inline void launch_force_t(hipStream_t s, const ForceArgs &a) {
   hipLaunchKernelGGL((k_force<G, DIM, VISC, MODE, NT1>), dim3(grid_for_rows(a.inum, G)),
                      dim3(256), 0, s, a.inum, a.nlocal, a.newton, a.ilist, a.off, a.nbr, a.xf,
                      a.vr, a.ty, a.en, a.fo, a.de, a.accum, a.cf, a.gx, a.gy, a.gz, a.virial,
-                     a.nojside);
+                     a.nojside, a.vso, a.vsg);
 }
 
 template <int G, int DIM, bool NT1>

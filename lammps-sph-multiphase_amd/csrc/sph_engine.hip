@@ -1149,9 +1149,9 @@ struct sph_engine {
     mx.reserve(8);
     // single pass into fixed-stride rows when a previous build sized them and nothing
     // needs the CSR form (the setup's half-list pass)
-    // (the multiphase passes index rows with 64-bit offsets: plain rows, any size)
-    const bool sfits = mp ? (long)n * list_stride < 0x7fffffffL
-                          : row2_fits((long)nall, (long)n * list_stride);
+    // (the multiphase passes index rows with 64-bit offsets, MpRow: plain rows, any size)
+    const bool sfits = mp ? true : row2_fits((long)nall, (long)n * list_stride);
+    bool sover = false;  // the strided fill overflowed: a CSR fill at the same stride would too
     if (!csr && list_stride > 0 && sfits) {
       // rows stored chunk-transposed for the row2 kernels' 16-B index loads; with several
       // types the neighbour's type rides in the entry's top bits
@@ -1167,6 +1167,7 @@ struct sph_engine {
         nbr_builds++;
         return;
       }
+      sover = true;
     }
     strided = false;
     list_tbits = false;
@@ -1174,7 +1175,7 @@ struct sph_engine {
     // (counts as a by-product) compacted into CSR after the scan -- instead of a count pass
     // and a fill pass (the C5 stack rebuilds every step); a row past the stride falls back
     bool filled = false;
-    if (list_stride > 0 && (long)n * list_stride < 0x7fffffffL) {  // (64-bit row offsets)
+    if (!sover && list_stride > 0 && (long)n * list_stride < 0x7fffffffL) {
       list_perm_g = 0;
       list_perm_pi = 0;
       nbs.reserve((size_t)n * list_stride);
@@ -1562,7 +1563,7 @@ struct sph_engine {
       hipLaunchKernelGGL(k_eos, dim3(blocks(nall)), dim3(BLK), 0, s, nall, xf.p, vr.p, ty.p, dc);
     }
     if (force_mode && setup) {
-      setup_forces_half();
+      setup_forces_full();
     } else if (force_mode && blk) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       blk_force(nt1(), cfg.tait_visc, force_mode, s, blk_args(), row_args());
@@ -1605,33 +1606,28 @@ struct sph_engine {
 
   // Force pass of Verlet::setup with the reference's half-list ownership (see
   // k_half_from_full): exact even though ghost vest is stale at this point.
-  void setup_forces_half() {
+  // The setup step's force pass (Verlet::setup, verlet.cpp:88-139): borders() ran before
+  // FixMeso::setup_pre_force, so the reference's half-list pass sees a ghost's vest as it
+  // was bordered.  Walked as a full-list gather (the global-index CSR rows of the setup
+  // build) that picks, for each ghost pair, the vest pair the reference's one evaluation
+  // uses (k_force: vso / vsg) -- no half list, no atomics, no reverse comm.
+  DBuf<double4> vso, vsg;  // owned vest before setup_pre_force; ghosts' vest as bordered
+  void setup_forces_full() {
     const int n = nlocal, nall = nlocal + nghost;
     if (force_mode == 0 || n == 0) return;
-    DBuf<int> hcnt, hoff, hnbr;
-    hcnt.reserve(n + 1);
-    hoff.reserve(n + 1);
-    hipLaunchKernelGGL((k_half_from_full<false>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
-                       nbr.p, xf.p, hcnt.p, (const int *)nullptr, (int *)nullptr);
-    hipLaunchKernelGGL(k_copy_counts, dim3(blocks(n + 1)), dim3(BLK), 0, s, n, hcnt.p, hoff.p);
-    size_t tb = 0;
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, hoff.p, hoff.p, n + 1, s));
-    tmp_reserve(tb);
-    SPH_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, hoff.p, hoff.p, n + 1, s));
-    const int tot = read_scalar(hoff.p + n);
-    hnbr.reserve(tot > 0 ? tot : 1);
-    hipLaunchKernelGGL((k_half_from_full<true>), dim3(blocks(n)), dim3(BLK), 0, s, n, off.p,
-                       nbr.p, xf.p, (int *)nullptr, hoff.p, hnbr.p);
+    vsg.reserve(nghost > 0 ? nghost : 1);
+    if (nghost)
+      SPH_HIP_TRY(hipMemcpyAsync(vsg.p, vr.p + n, (size_t)nghost * sizeof(double4),
+                                 hipMemcpyDeviceToDevice, s));
+    forward();  // the ghosts' vest as setup_pre_force left their owners' (x, rho, e unchanged)
     fo.reserve(nall, true, s);
     de.reserve(nall, true, s);
-    SPH_HIP_TRY(hipMemsetAsync(fo.p, 0, nall * sizeof(double4), s));
-    SPH_HIP_TRY(hipMemsetAsync(de.p, 0, nall * sizeof(double), s));
     ForceArgs a{};
     a.inum = n;
     a.nlocal = n;
     a.newton = 1;
-    a.off = hoff.p;
-    a.nbr = hnbr.p;
+    a.off = off.p;
+    a.nbr = nbr.p;
     a.xf = xf.p;
     a.vr = vr.p;
     a.ty = ty.p;
@@ -1639,21 +1635,12 @@ struct sph_engine {
     a.fo = fo.p;
     a.de = de.p;
     a.cf = dc;
-    launch_force(cfg.dim, nt1(), s, cfg.tait_visc, force_mode | M_HALF, a);
-    if (multi())
-      reverse_multi();
-    else if (nghost)
-      hipLaunchKernelGGL(k_reverse, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, n, gowner.p,
-                         fo.p, de.p);
-    // post_force body force (fix gravity style), as the full-list kernel applies it
-    if (cfg.gravity[0] != 0.0 || cfg.gravity[1] != 0.0 || cfg.gravity[2] != 0.0)
-      hipLaunchKernelGGL(k_add_gravity, dim3(blocks(n)), dim3(BLK), 0, s, n, sc,
-                         cfg.gravity[0], cfg.gravity[1], cfg.gravity[2], cfg.gravity_mask,
-                         ty.p, fo.p);
-    SPH_HIP_TRY(hipStreamSynchronize(s));  // scratch lists are freed on return
-    hcnt.release();
-    hoff.release();
-    hnbr.release();
+    a.gx = cfg.gravity[0];
+    a.gy = cfg.gravity[1];
+    a.gz = cfg.gravity[2];
+    a.vso = vso.p;
+    a.vsg = vsg.p;
+    launch_force(cfg.dim, nt1(), s, cfg.tait_visc, force_mode, a);
   }
 
   // ---- multiphase stack -------------------------------------------------------------
@@ -1987,6 +1974,10 @@ struct sph_engine {
     // borders() runs before setup_pre_force: ghosts carry vest as it was (reference order);
     // the setup force pass needs the global-index list for its half-list walk
     build_all(true);
+    vso.reserve(nlocal > 0 ? nlocal : 1);  // (vest before setup_pre_force: setup_forces_full)
+    if (nlocal)
+      SPH_HIP_TRY(hipMemcpyAsync(vso.p, vr.p, (size_t)nlocal * sizeof(double4),
+                                 hipMemcpyDeviceToDevice, s));
     hipLaunchKernelGGL(k_vest_from_v, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal,
                        cfg.stationary_mask, ty.p, vel.p, vr.p);
     pair_compute(rhosum_due(), /*setup=*/true);

@@ -237,6 +237,17 @@ static __global__ void k_eos(int n, double4 *__restrict__ xf, const double4 *__r
 // ------------------------------------------------------------------------------------
 enum { M_TAIT = 1, M_HEAT = 2, M_HALF = 4 };
 
+// Neighbor::half_from_full_newton's test for a ghost j (neigh_derive.cpp:113-121): the pair
+// stays in i's half row iff j lies above i in z, then y, then x
+__device__ __forceinline__ bool ghost_keep(const double4 &xi, const double4 &xj) {
+  if (xj.z < xi.z) return false;
+  if (xj.z == xi.z) {
+    if (xj.y < xi.y) return false;
+    if (xj.y == xi.y && xj.x < xi.x) return false;
+  }
+  return true;
+}
+
 template <int G, int DIM, int VISC, int MODE, bool NT1>
 __global__ void __launch_bounds__(256)
 k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
@@ -244,7 +255,8 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
         const double4 *__restrict__ xf, const double4 *__restrict__ vr,
         const int *__restrict__ ty, const double *__restrict__ en, double4 *__restrict__ fo,
         double *__restrict__ de, int accum, const Coefs *__restrict__ cf, double gx,
-        double gy, double gz, double *__restrict__ virial, int nojside) {
+        double gy, double gz, double *__restrict__ virial, int nojside,
+        const double4 *__restrict__ vso, const double4 *__restrict__ vsg) {
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr bool HALF = (MODE & M_HALF) != 0;
@@ -308,7 +320,21 @@ k_force(int inum, int nlocal, int newton, const int *__restrict__ ilist,
         const TaitPair c = NT1 ? t1 : s_t[pidx];
         double wfd = c.h - r;
         wfd = c.wK * (wfd * wfd);
-        const double velx = vi.x - vj[u].x, vely = vi.y - vj[u].y, velz = vi.z - vj[u].z;
+        // setup step (vso != nullptr, full list): the reference's half-list pass meets each
+        // ghost pair once, on the side half_from_full keeps -- (i, ghost j) with vest_i as
+        // setup_pre_force set it and vest_j as borders() left it, else (j, ghost i') with
+        // j's new vest and i's old one (Verlet::setup runs borders before setup_pre_force)
+        double3 va = make_double3(vi.x, vi.y, vi.z), vb = make_double3(vj[u].x, vj[u].y, vj[u].z);
+        if (vso && j >= nlocal) {
+          if (ghost_keep(xi, xj[u])) {
+            const double4 g = vsg[j - nlocal];
+            vb = make_double3(g.x, g.y, g.z);
+          } else {
+            const double4 o = vso[i];
+            va = make_double3(o.x, o.y, o.z);
+          }
+        }
+        const double velx = va.x - vb.x, vely = va.y - vb.y, velz = va.z - vb.z;
         const double dvdr = dx * velx + dy * vely + dz * velz;
         double fpair, deltaE, fvx = 0.0, fvy = 0.0, fvz = 0.0;
         if (VISC == SPH_VISC_MONAGHAN) {

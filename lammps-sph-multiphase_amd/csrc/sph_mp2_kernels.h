@@ -27,6 +27,11 @@
 
 namespace sph {
 
+// list entries per lane whose loads are issued together (study builds: -DSPH_MP2_NU=n)
+#ifndef SPH_MP2_NU
+#define SPH_MP2_NU 2
+#endif
+
 // quintic W(s) and dW/ds without the norm (s = 3 r / h)
 __device__ __forceinline__ double q5_w(double s) {
   const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
@@ -37,6 +42,16 @@ __device__ __forceinline__ double q5_dw(double s) {
   const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
   const double a2 = a * a, b2 = b * b, c2 = c * c;
   return fma(-75.0 * c2, c2, fma(30.0 * b2, b2, -5.0 * (a2 * a2)));
+}
+
+// r and 1/r from one v_rsq_f64 seed, one Newton step each (x + 1e-300: a coincident pair
+// gives a huge 1/r times a zero weight instead of NaN)
+__device__ __forceinline__ void mp2_r_ir(double x, double &r, double &ir) {
+  x += 1e-300;
+  const double y = __builtin_amdgcn_rsq(x);
+  const double r0 = x * y;
+  r = fma(fma(-r0, r0, x), 0.5 * y, r0);
+  ir = y * fma(-0.5 * x * y, y, 1.5);
 }
 
 // per pair type: the stack's cutoffs (squared), 1/h and the coefficients the pair terms use
@@ -108,8 +123,8 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
   const Mp2Pair *const pi = s_p + it * nt1;
   double acc = 0.0;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  constexpr int NU = 2;
-  for (int k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
+  constexpr int NU = SPH_MP2_NU;
+  for (long long k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
     double4 xj[NU];
     int tj[NU];
 #pragma unroll
@@ -124,7 +139,9 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
       const Mp2Pair &q = pi[tj[u]];
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
       const double rsq = dx * dx + dy * dy + dz * dz;
-      if (rsq < q.rcsq) acc += q5_w(3.0 * (sqrt(rsq) * q.rih)) * mp2_wnorm(dim, q.rih);
+      double r, ir;
+      mp2_r_ir(rsq, r, ir);
+      if (rsq < q.rcsq) acc += q5_w(3.0 * (r * q.rih)) * mp2_wnorm(dim, q.rih);
     }
   }
   acc = group_sum<G>(acc);
@@ -151,8 +168,8 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
   const double sigmai = xi.w;
   double gx = 0.0, gy = 0.0, gz = 0.0;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  constexpr int NU = 2;
-  for (int k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
+  constexpr int NU = SPH_MP2_NU;
+  for (long long k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
     double4 xj[NU];
     int tj[NU];
 #pragma unroll
@@ -169,10 +186,11 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
       const double rsq = dx * dx + dy * dy + dz * dz;
       if (!(rsq < q.ccsq)) continue;
-      const double r = sqrt(rsq);
+      double r, ir;
+      mp2_r_ir(rsq, r, ir);
       const double wfd = q5_dw(3.0 * (r * q.cih)) * mp2_dwnorm(dim, q.cih);
       const double sj = xj[u].w;
-      const double dphi = -wfd * q.calpha * mp_rcp(sj * sj) * sigmai * mp_rcp(r);
+      const double dphi = -wfd * q.calpha * mp_rcp(sj * sj) * sigmai * ir;
       gx += dphi * dx;
       gy += dphi * dy;
       if (dim == 3) gz += dphi * dz;
@@ -241,11 +259,12 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   const Mp2Type tyi = s_t[ti];
   const double mi = xi.w, Ti = v4i.w;
   const double4 cFi = a.pF[i], cSi = a.pS[i];
+  const double irFi = mp_rcp(cFi.w), irSi = mp_rcp(cSi.w);
   double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
-  constexpr int NU = 2;
+  constexpr int NU = SPH_MP2_NU;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  const int kend = rw.end;
-  for (int k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
+  const long long kend = rw.end;
+  for (long long k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
     int jrs[NU], tjs[NU];
     double4 xjs[NU], v4js[NU], cjs[NU];
 #pragma unroll
@@ -272,13 +291,14 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
       const double rsq = dx * dx + dy * dy + dz * dz;
       const bool ct = TAIT && rsq < q.tcsq, cs = SURF && rsq < q.scsq, ch = HEAT && rsq < q.hcsq;
       if (!(ct || cs || ch)) continue;
-      const double r = sqrt(rsq), ir = mp_rcp(r);
+      double r, ir;
+      mp2_r_ir(rsq, r, ir);
       const double qt = ct ? q5_dw(3.0 * (r * q.tih)) * mp2_dwnorm(dim, q.tih) : 0.0;
       const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt
                                     : q5_dw(3.0 * (r * q.sih)) * mp2_dwnorm(dim, q.sih);
       const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt
                                    : q5_dw(3.0 * (r * q.hih)) * mp2_dwnorm(dim, q.hih);
-      const double iri = mp_rcp(rhoi), irj = mp_rcp(rhoj);
+      const double iri = fi ? irFi : irSi, irj = mp_rcp(rhoj);
       const double Vi = mi * iri, Vj = mj * irj;
       const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
       if (ct) {  // pair_sph_taitwater_multiphase.cpp:128-170

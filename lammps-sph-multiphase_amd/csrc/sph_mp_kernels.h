@@ -138,10 +138,10 @@ struct MpArgs {
 };
 // a list row's entries [beg, end): CSR (off) or fixed-stride rows (stride, cnt)
 struct MpRow {
-  int beg, end;
+  long long beg, end;  // (64-bit: fixed-stride rows of any system size)
   __device__ __forceinline__ MpRow(const int *off, const int *cnt, int stride, int row) {
     if (stride > 0) {
-      beg = row * stride;
+      beg = (long long)row * stride;
       end = beg + cnt[row];
     } else {
       beg = off[row];
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
   const int dim = a.dim;
   double acc = 0.0;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  for (int k = rw.beg + lane; k < rw.end; k += G) {
+  for (long long k = rw.beg + lane; k < rw.end; k += G) {
     const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xf[j];
     const int jt = a.ty[j];
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
   const double sigmai = a.xs ? xi.w : a.vr[i].w / a.rm[i];
   double gx = 0.0, gy = 0.0, gz = 0.0;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  for (int k = rw.beg + lane; k < rw.end; k += G) {
+  for (long long k = rw.beg + lane; k < rw.end; k += G) {
     const int j = a.nbr[k] & MP_NMASK;
     const double4 xj = a.xs ? a.xs[j] : a.xf[j];
     const int jt = a.ty[j];
@@ -485,8 +485,8 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
   // (the loop is latency-bound on the index -> record chain otherwise)
   constexpr int NU = 2;
   const MpRow rw(a.off, a.cnt, a.stride, row);
-  const int kend = rw.end;
-  for (int k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
+  const long long kend = rw.end;
+  for (long long k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
     int jrs[NU];
     double4 xjs[NU], v4js[NU], cjs[NU];
     int tjs[NU];

@@ -99,7 +99,7 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
   int around = 0, mr = PC_NORANK;
   double W = 0.0, sv0 = 0.0, sv1 = 0.0, sv2 = 0.0, se0 = 0.0, se1 = 0.0, se2 = 0.0;
   const MpRow rw(off, lcnt, lstride, row);
-  for (int q = rw.beg + lane; q < rw.end; q += G) {
+  for (long long q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type) continue;
     const int r = rk(j);
@@ -164,7 +164,7 @@ k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wt
   const double4 xi = xf[i];
   const double W = Wtot[k];
   const MpRow rw(off, lcnt, lstride, row);
-  for (int q = rw.beg + lane; q < rw.end; q += G) {
+  for (long long q = rw.beg + lane; q < rw.end; q += G) {
     const int j = nbr[q] & MP_NMASK;
     if (ty[j] != p.from_type || !(rm[j] > 0.5 * p.to_mass)) continue;
     const int r = rk(j);

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-3 final lines into gpurun_out/r03/final: C2 bench (driver shape, with the CPU
+# baseline, and 100/20), rocprofv3 kernel stats of the driver shape, PMC traffic (FETCH/WRITE
+# passes), C5 4.02M bench + stats, C3.  Usage: tools/gpu_final3.sh COMMIT [skip-tests]
+cd "${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}" || exit 1
+R=$(pwd); O=$R/gpurun_out/r03/final; C=${1:-unknown}
+mkdir -p "$O"
+if [ "$2" != skip-tests ]; then
+  timeout -k 10 900 python -u -m pytest tests/ -m gpu -v --timeout 240 --timeout-method thread > "$O/tests.log" 2>&1
+  rc=$?; grep -E " passed| failed" "$O/tests.log" | tail -1; [ $rc -eq 0 ] || { grep -E "^FAILED" "$O/tests.log" | head; exit $rc; }
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -3 "$O/smoke.log"; exit 1; }
+  tail -1 "$O/smoke.log"
+fi
+timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > "$O/bench_c2_20.json" 2> "$O/bench_c2_20.err" || { tail -5 "$O/bench_c2_20.err"; exit 1; }
+echo "c2 20/5: $(cut -c1-200 "$O/bench_c2_20.json")"
+timeout -k 10 400 python3 bench.py --steps 100 --warmup 20 --no-cpu > "$O/bench_c2_100.json" 2> "$O/bench_c2_100.err" || exit 1
+echo "c2 100/20: $(cut -c1-200 "$O/bench_c2_100.json")"
+META="world=1 edge=100 path=0 steps=20 warmup=5 commit=$C" timeout -k 10 700 tools/pmc_traffic.sh "$O/pmc_c2" --steps 20 --warmup 5 --no-cpu || exit 1
+python3 -c "import json;d=json.load(open('$O/pmc_c2/pmc_traffic.json'));print({k:(v['traffic_bytes'] if isinstance(v,dict) and 'traffic_bytes' in v else v) for k,v in d.items()})"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c2" -o c2 -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu > "$O/bench_c2_prof.json" 2> "$O/prof_c2.err" || exit 1
+cd "$R" && python3 tools/kstats.py "$(find "$O/prof_c2" -name '*kernel_stats.csv' | head -1)" 8
+timeout -k 10 600 python3 bench.py --workload c5 --steps 10 --warmup 3 > "$O/bench_c5.json" 2> "$O/bench_c5.err" || { tail -5 "$O/bench_c5.err"; exit 1; }
+echo "c5: $(cut -c1-200 "$O/bench_c5.json")"
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_c5" -o c5 -- python3 "$R/bench.py" --workload c5 --steps 5 --warmup 2 --no-cpu > "$O/bench_c5_prof.json" 2> "$O/prof_c5.err" || exit 1
+cd "$R" && python3 tools/kstats.py "$(find "$O/prof_c5" -name '*kernel_stats.csv' | head -1)" 8
+timeout -k 10 400 python3 bench.py --workload c3 --steps 20 --warmup 5 > "$O/bench_c3.json" 2> "$O/bench_c3.err" || { tail -5 "$O/bench_c3.err"; exit 1; }
+echo "c3: $(cut -c1-200 "$O/bench_c3.json")"

@@ -10,7 +10,8 @@ import glob
 import json
 import sys
 
-FAMILIES = ("k_blk_force", "k_blk_rhosum", "k_blk_neigh", "k_mp_gather", "k_mp_rhosum",
+FAMILIES = ("k_blk_force", "k_blk_rhosum", "k_blk_build", "k_blk_neigh", "k_mp2_gather",
+            "k_mp2_rhosum", "k_mp2_colorgradient", "k_mp_gather", "k_mp_rhosum",
             "k_mp_colorgradient", "k_row2_force", "k_row2_rhosum", "k_force", "k_rhosum",
             "k_neigh3")
 

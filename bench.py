@@ -1166,6 +1166,12 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args):
                 f"tools/pmc_traffic.sh, profiles/{rnd}/pmc_traffic.json, commit "
                 f"{meta.get('commit', '?')})")
             out["roofline"]["algorithmic_GB_per_step"] = alg_bytes / 1e9
+            va = v.get("valu")
+            if va:  # what binds the pass: its fp64 VALU issue (PMC SQ_INSTS_VALU / duration)
+                out["roofline"]["valu_issue_frac"] = va["issue_frac_fp64"]
+                out["roofline"]["valu_issue_unit"] = (
+                    "VALU wave-instructions of the main launch / its duration / the fp64 issue "
+                    "peak (256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles), same PMC record")
             return
 
 

@@ -23,7 +23,7 @@ def family(name):
     return None
 
 
-def load(path, counter):
+def load(path, counter, scale=1024.0, dur=None):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"{path}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -31,8 +31,16 @@ def load(path, counter):
                 continue
             k = family(r["Kernel_Name"])
             if k:
-                agg[k][int(r.get("Grid_Size", 0) or 0)].append(float(r["Counter_Value"]) * 1024.0)
+                g = int(r.get("Grid_Size", 0) or 0)
+                agg[k][g].append(float(r["Counter_Value"]) * scale)
+                if dur is not None:
+                    dur[k][g].append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) * 1e-9)
     return agg
+
+
+# fp64 VALU issue peak of the chip: 256 CUs x 4 SIMDs at 2.4 GHz, one wave64 fp64
+# instruction per 4 cycles per SIMD (16 lanes/clk: the 78.6 TFLOP/s fp64 vector rate)
+FP64_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4.0
 
 
 def main(root, meta):
@@ -57,6 +65,17 @@ def main(root, meta):
         # per step: all launches' bytes over the count of the largest-grid (main) launch
         nmain = per[str(max(grids))]["launches"] if ok and grids else 0
         out[k] = {"grids": per, "traffic_bytes": tot / nmain if ok and nmain else None}
+    dur = collections.defaultdict(lambda: collections.defaultdict(list))
+    valu = load(f"{root}/valu", "SQ_INSTS_VALU", 1.0, dur)
+    for k, grids in valu.items():
+        # the main (largest-grid) launch: VALU wave-instructions per second over its duration,
+        # every VALU instruction counted at the fp64 issue cost (an upper bound of the issue
+        # time: 32-bit ops issue twice as fast)
+        g = max(grids)
+        ins = sum(grids[g]) / len(grids[g])
+        d = sum(dur[k][g]) / len(dur[k][g])
+        out.setdefault(k, {})["valu"] = {"wave_instr_per_launch": ins, "launch_s": d,
+                                         "issue_frac_fp64": ins / d / FP64_WAVE_INSTR_PER_S}
     print(json.dumps(out, indent=1))
 
 

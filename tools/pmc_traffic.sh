@@ -14,4 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
   python3 "$R/bench.py" "$@" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o pmc -- \
   python3 "$R/bench.py" "$@" > "$OUT/write.log" 2>&1
+# VALU issue: wave-instructions and durations of the same launches (a third pass)
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES --output-format csv \
+  -d "$OUT/valu" -o pmc -- python3 "$R/bench.py" "$@" > "$OUT/valu.log" 2>&1
 python3 "$R/tools/pmc_traffic.py" "$OUT" $META > "$OUT/pmc_traffic.json"

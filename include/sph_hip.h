@@ -375,7 +375,9 @@ int sph_engine_get_atoms(sph_engine *e, double *x, double *v, double *rho, doubl
 /* per owned particle (set_atoms order): full-list count within cut+skin at last build */
 int sph_engine_neighbor_counts(sph_engine *e, int *numneigh);
 int sph_engine_stats_get(sph_engine *e, sph_engine_stats *s);
-/* enable/disable hipEvent timing of each kernel class (adds event records per launch) */
+/* hipEvent timing of the kernel classes (adds an event pair per timed scope): on = 0 off,
+   1 every class, (mask << 1) the classes in mask -- bit 0 rhosum, 1 taitwater (or the fused
+   multiphase gather), 2 heat, 3 integrate, 4 comm, 5 neighbor build / phase change */
 int sph_engine_set_timing(sph_engine *e, int on);
 /* synchronise the engine's stream */
 int sph_engine_sync(sph_engine *e);

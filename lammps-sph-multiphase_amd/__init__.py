@@ -594,8 +594,18 @@ class Engine:
     def sync(self):
         _chk(self.L.sph_engine_sync(self.h))
 
-    def set_timing(self, on):
-        _chk(self.L.sph_engine_set_timing(self.h, 1 if on else 0))
+    # timer classes of sph_engine_set_timing
+    T_RHO, T_TAIT, T_HEAT, T_INT, T_COMM, T_NEIGH = range(6)
+
+    def set_timing(self, on, classes=None):
+        """on: every kernel class timed with hipEvents; classes: only these (T_* bits)."""
+        if on and classes is not None:
+            mask = 0
+            for c in classes:
+                mask |= 1 << c
+            _chk(self.L.sph_engine_set_timing(self.h, mask << 1))
+        else:
+            _chk(self.L.sph_engine_set_timing(self.h, 1 if on else 0))
 
     @property
     def nlocal(self):

@@ -51,6 +51,17 @@ struct Transport {
     exchange(s1, sb1, d1, r1, rb1, src1, s);
   }
   virtual void barrier(hipStream_t s) = 0;
+  // exchange_count2 with the two send counts in DEVICE words dsend[0..1] (written by kernels
+  // on s): h[0..1] = the sends, h[2..3] = the receives (from src0, src1); one host sync
+  virtual void exchange_count2_dev(const int *dsend, int d0, int src0, int d1, int src1,
+                                   hipStream_t s, int h[4]) {
+    SPH_HIP_TRY(hipMemcpyAsync(h, dsend, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    int nr[2];
+    exchange_count2(h[0], d0, src0, h[1], d1, src1, s, nr);
+    h[2] = nr[0];
+    h[3] = nr[1];
+  }
   // every other rank r: send scnt[r] to r, receive rcnt[r] from r (scnt/rcnt hold size()
   // ints; the own entry is ignored); host-synchronous
   virtual void exchange_counts_all(const int *scnt, int *rcnt, hipStream_t s) = 0;
@@ -121,6 +132,19 @@ class RcclTransport : public Transport {
     SPH_HIP_TRY(hipStreamSynchronize(s));
     nrecv[0] = h[2];
     nrecv[1] = h[3];
+  }
+  // the counts straight from the device words: one RCCL group and one host read of all four
+  void exchange_count2_dev(const int *dsend, int d0, int src0, int d1, int src1, hipStream_t s,
+                           int h[4]) override {
+    SPH_HIP_TRY(hipMemcpyAsync(dcnt_, dsend, 2 * sizeof(int), hipMemcpyDeviceToDevice, s));
+    SPH_NCCL_TRY(ncclGroupStart());
+    SPH_NCCL_TRY(ncclSend(dcnt_, 1, ncclInt32, d0, comm_, s));
+    SPH_NCCL_TRY(ncclRecv(dcnt_ + 2, 1, ncclInt32, src0, comm_, s));
+    SPH_NCCL_TRY(ncclSend(dcnt_ + 1, 1, ncclInt32, d1, comm_, s));
+    SPH_NCCL_TRY(ncclRecv(dcnt_ + 3, 1, ncclInt32, src1, comm_, s));
+    SPH_NCCL_TRY(ncclGroupEnd());
+    SPH_HIP_TRY(hipMemcpyAsync(h, dcnt_, 4 * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
   }
   // one RCCL group for both directions of a dimension: one launch/sync round instead of two
   void exchange2(const void *s0, size_t sb0, int d0, void *r0, size_t rb0, int src0,

@@ -32,6 +32,7 @@ namespace sph {
 #ifndef SPH_INNER_FRAC
 #define SPH_INNER_FRAC 0.0625
 #endif
+int g_alloc_log = 0;
 static int env_int(const char *name, int dflt) {
   const char *s = getenv(name);
   return s ? atoi(s) : dflt;
@@ -264,6 +265,7 @@ struct sph_engine {
 
   // timing
   bool timing = false;
+  int timing_mask = 0;  // classes timed (bit k = TimerClass k)
   struct EvPair {
     hipEvent_t a, b;
     int cls;
@@ -286,15 +288,16 @@ struct sph_engine {
   struct Scope {
     sph_engine *e;
     EvPair p;
-    Scope(sph_engine *eng, int cls) : e(eng) {
-      if (!e->timing) return;
+    bool on;
+    Scope(sph_engine *eng, int cls) : e(eng), on(((eng->timing_mask >> cls) & 1) != 0) {
+      if (!on) return;
       p.a = e->get_ev();
       p.b = e->get_ev();
       p.cls = cls;
       SPH_HIP_TRY(hipEventRecord(p.a, e->s));
     }
     ~Scope() {
-      if (!e->timing) return;
+      if (!on) return;
       (void)hipEventRecord(p.b, e->s);
       e->pending.push_back(p);
     }
@@ -485,25 +488,39 @@ struct sph_engine {
         if (dir == 1 && myloc[d] == pg[d] - 1) pbc = -1;
         sw.shift = pbc * box.prd[d];
         sw.pbc = pbc;
-        int ns = 0;
+        // the selection's count stays on the device (nsel[dir]); both swaps' counts and the
+        // peers' are read back together below: one host sync per dimension
+        nsel.reserve(2);
+        sw.list.reserve(nlast > 0 ? nlast : 1);
         if (sendflag && nlast > 0) {
           flags.reserve(nlast);
           hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d,
                              sw.lo, sw.hi, xf.p, flags.p);
-          ns = select_flagged(flags.p, nlast, sw.list);
+          hipcub::CountingInputIterator<int> it(0);
+          size_t tb = 0;
+          SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tb, it, flags.p, sw.list.p,
+                                                    nsel.p + dir, nlast, s));
+          tmp_reserve(tb);
+          SPH_HIP_TRY(hipcub::DeviceSelect::Flagged(tmp.p, tb, it, flags.p, sw.list.p,
+                                                    nsel.p + dir, nlast, s));
+        } else {
+          SPH_HIP_TRY(hipMemsetAsync(nsel.p + dir, 0, sizeof(int), s));
         }
-        sw.nsend = ns;
       }
       Swap &a = *pair[0], &b = *pair[1];
       if (a.remote) {
-        int nr[2];
-        tr->exchange_count2(a.nsend, a.sendproc, a.recvproc, b.nsend, b.sendproc, b.recvproc,
-                            s, nr);
-        a.nrecv = nr[0];
-        b.nrecv = nr[1];
+        int h[4];
+        tr->exchange_count2_dev(nsel.p, a.sendproc, a.recvproc, b.sendproc, b.recvproc, s, h);
+        a.nsend = h[0];
+        b.nsend = h[1];
+        a.nrecv = h[2];
+        b.nrecv = h[3];
       } else {
-        a.nrecv = a.nsend;
-        b.nrecv = b.nsend;
+        int *const h = h_small;  // (pinned)
+        SPH_HIP_TRY(hipMemcpyAsync(h, nsel.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+        SPH_HIP_TRY(hipStreamSynchronize(s));
+        a.nsend = a.nrecv = h[0];
+        b.nsend = b.nrecv = h[1];
       }
       a.firstrecv = nall;
       b.firstrecv = nall + a.nrecv;
@@ -2084,6 +2101,7 @@ extern "C" {
 int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out) {
   SPH_API_BEGIN
   SPH_REQUIRE(cfg && out, SPH_HIP_EINVAL, "sph_engine_create: NULL argument");
+  g_alloc_log = env_int("SPH_ALLOC_LOG", 0);
   SPH_REQUIRE(cfg->dim == 2 || cfg->dim == 3, SPH_HIP_EINVAL, "dimension must be 2 or 3");
   SPH_REQUIRE(cfg->ntypes >= 1 && cfg->ntypes <= SPH_MAXTYPES, SPH_HIP_EINVAL,
               "ntypes %d outside [1,%d]", cfg->ntypes, SPH_MAXTYPES);
@@ -2690,7 +2708,10 @@ int sph_engine_set_timing(sph_engine *e, int on) {
   SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_set_timing: NULL engine");
   SPH_HIP_TRY(hipSetDevice(e->device));
   e->harvest();
-  e->timing = on != 0;
+  // 1: every class; (mask << 1): the classes of mask (a timed run records an event pair per
+  // timed scope, which at small sizes is a visible share of a step)
+  e->timing_mask = on == 1 ? (1 << T_NCLASS) - 1 : (on > 1 ? (on >> 1) & ((1 << T_NCLASS) - 1) : 0);
+  e->timing = e->timing_mask != 0;
   for (int k = 0; k < T_NCLASS; k++) {
     e->ms[k] = 0.0;
     e->nlaunch[k] = 0;

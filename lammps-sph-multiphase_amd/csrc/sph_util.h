@@ -47,6 +47,9 @@ struct Failure {
   }                                                                                   \
   return SPH_HIP_OK;
 
+// allocation log (SPH_ALLOC_LOG=1 at engine creation): every device buffer growth to stderr
+extern int g_alloc_log;
+
 // Growable device buffer (never shrinks; contents not preserved on growth unless asked).
 template <class T>
 struct DBuf {
@@ -55,6 +58,9 @@ struct DBuf {
   void reserve(size_t n, bool keep = false, hipStream_t s = 0) {
     if (n <= cap) return;
     size_t nc = n + n / 8 + 64;
+    if (g_alloc_log)
+      fprintf(stderr, "[sph] DBuf<%zu B> %p grows %zu -> %zu%s\n", sizeof(T), (void *)this, cap,
+              nc, keep ? " (kept)" : "");
     T *q = nullptr;
     SPH_HIP_TRY(hipMalloc(&q, nc * sizeof(T)));
     if (keep && p && cap) SPH_HIP_TRY(hipMemcpyAsync(q, p, cap * sizeof(T), hipMemcpyDeviceToDevice, s));

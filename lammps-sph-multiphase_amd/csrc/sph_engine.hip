@@ -113,6 +113,22 @@ static bool direct_env() {
   return v;
 }
 static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
+// SPH_SORT_EVERY (default 10): steps between spatial sorts of the owned atoms at rebuilds
+static int sort_every() {
+  static int v = study_int("SPH_SORT_EVERY", 10);
+  return v;
+}
+// SPH_MP_TYPED (default 1): the multiphase passes take the neighbour's type from the entry
+static bool mp_typed_env() {
+  static bool v = study_int("SPH_MP_TYPED", 1) != 0;
+  return v;
+}
+// SPH_MP_RHOFUSE (default 1): the multiphase engine's list fill sums rhosum/multiphase over
+// the hits it finds when the list is built in the step whose forces follow (k_neigh3 RHO)
+static bool rhofuse_env() {
+  static bool v = study_int("SPH_MP_RHOFUSE", 1) != 0;
+  return v;
+}
 
 namespace {
 
@@ -189,6 +205,8 @@ struct sph_engine {
   bool ov_ready = false;  // rows_in / rows_bd describe the current list
   bool overlap = false;   // SPH_OVERLAP at creation
   int64_t step = 0;
+  int64_t rho_fused_step = -1;
+  int64_t last_sort = 0;  // step of the last spatial sort of the owned atoms  // step whose rhosum/multiphase the list fill summed (k_neigh3 RHO)
   bool setup_done = false;
   bool global_tags = false;
   int last_build = 0;
@@ -1144,6 +1162,13 @@ struct sph_engine {
   void list_q(bool csr, const double4 *xi = nullptr) {
     const int n = nlocal, nall = nlocal + nghost;
     const double4 *const xi_src = xi ? xi : xf.p;
+    // rhosum/multiphase fused into the fill passes (k_neigh3 RHO): current positions, due now
+    const bool rho = mp && !xi && rhofuse_env() && mpc.rhosum_nstep > 0 &&
+                     step % mpc.rhosum_nstep == 0;
+    SPH_REQUIRE(!mp || (long long)nall < MP_MAXALL, SPH_HIP_EOVERFLOW,
+                "multiphase lists index at most 2^28 atoms per rank (%d)", nall);
+    if (rho) rho_tmp.reserve(nlocal + nghost);
+    rho_fused_step = rho ? step : -1;  // (every path below ends in a fill pass)
     ccnt.reserve(n + 1);
     off.reserve(n + 1);
     constexpr int G = 8;
@@ -1159,9 +1184,16 @@ struct sph_engine {
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? rows : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,    \
                      list_perm_pi, mp ? 2 : ((stride > 0 && list_tbits) ? 1 : 0))
-      if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
+#define SPH_N3R(T)                                                                             \
+  hipLaunchKernelGGL((k_neigh3<G, 4, true, T, true>), grid, block, 0, s, n, qb, cfg.dim, xi_src, \
+                     ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
+                     stride == 0 ? off.p : (const int *)nullptr, rows, stride, mx.p, 0, 0, 2, \
+                     dm, rm.p, rho_tmp.p)
+      if (fill && rho) { if (t) SPH_N3R(true); else SPH_N3R(false); }
+      else if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
       else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
+#undef SPH_N3R
     };
     mx.reserve(8);
     // single pass into fixed-stride rows when a previous build sized them and nothing
@@ -1351,7 +1383,12 @@ struct sph_engine {
     // orientation, k_neigh3: CSR at setup, fixed-stride rows once the setup sized them)
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p, vel.p);
     if (multi()) exchange_multi();
-    if (cfg.sort) sort_owned();
+    // (at most every sort_every() steps, as atom_modify sort Nevery: the C5 stack rebuilds
+    // every step, and its rows keep their locality over a few steps of motion)
+    if (cfg.sort && (!setup_done || step == 0 || step - last_sort >= sort_every())) {
+      sort_owned();
+      last_sort = step;
+    }
     borders();
     bin_q();
     blk = false;
@@ -1689,6 +1726,7 @@ struct sph_engine {
     a.en = en.p;
     a.cv = cvv.p;
     a.mc = dm;
+    a.typed = mp_typed_env() ? 1 : 0;  // (k_neigh3 tbits 2 writes the types)
     // the stale version: rho and colorgradient as communicated (k_mp_gather)
     rhoS.reserve(nall);
     cgS.reserve(nall);
@@ -1701,7 +1739,8 @@ struct sph_engine {
       if (rdue) {
         rho_tmp.reserve(nall);
         a.rho = rho_tmp.p;
-        hipLaunchKernelGGL(k_mp2_rhosum<8>, mp_rows(n), dim3(256), 0, s, a);
+        if (rho_fused_step != step)  // (else the list fill of this step summed it)
+          hipLaunchKernelGGL(k_mp2_rhosum<8>, mp_rows(n), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_mp_rho_store, dim3(blocks(n)), dim3(BLK), 0, s, n, rho_tmp.p, vr.p);
       }
       if (cdue) {
@@ -2606,7 +2645,10 @@ int sph_engine_rebuild_passes(sph_engine *e, int n) {
   SPH_REQUIRE(e && n >= 0, SPH_HIP_EINVAL, "sph_engine_rebuild_passes: bad argument");
   SPH_REQUIRE(e->setup_done, SPH_HIP_EINVAL, "sph_engine_rebuild_passes: call setup first");
   SPH_HIP_TRY(hipSetDevice(e->device));
-  for (int k = 0; k < n; k++) e->rebuild();
+  for (int k = 0; k < n; k++) {
+    e->last_sort = e->step - sort_every();  // (the full rebuild, sort included)
+    e->rebuild();
+  }
   SPH_HIP_TRY(hipGetLastError());
   SPH_API_END
 }

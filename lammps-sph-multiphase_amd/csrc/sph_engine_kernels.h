@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sph_kernels.h"
+#include "sph_mp2_kernels.h"
 
 namespace sph {
 
@@ -515,21 +516,33 @@ __device__ __forceinline__ bool half_keep(int i, int j, int nlocal, const double
   return true;
 }
 
-template <int G, int U, bool FILL, bool NT1>
+// RHO (fill passes of the multiphase engine, the list built in the step whose forces follow,
+// skin 0 as bubble.lmp): rhosum/multiphase (pair_sph_rhosum_multiphase.cpp:118-167) summed
+// over the row's hits as they are found -- the pair set and positions k_mp2_rhosum would walk
+// right after -- into rho (owned rows; rm = rmass); the separate rhosum pass is then skipped
+template <int G, int U, bool FILL, bool NT1, bool RHO = false>
 __global__ void __launch_bounds__(256)
 k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
          const int *__restrict__ tb, const int *__restrict__ beg,
          const Coefs *__restrict__ cf, int *__restrict__ cnt, const int *__restrict__ off,
          int *__restrict__ nbr, int stride, int *__restrict__ ovf, int perm_g, int perm_pi,
-         int tbits) {
+         int tbits, const MpCoefs *__restrict__ mc = nullptr,
+         const double *__restrict__ rm = nullptr, double *__restrict__ rho = nullptr) {
   constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
   __shared__ double s_cns[NT2];
+  __shared__ double s_rcs[RHO ? NT2 : 1], s_rih[RHO ? NT2 : 1], s_rwn[RHO ? NT2 : 1];
   __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
   __shared__ int s_pre[GR][NB + 1];  // candidates before each bin-row (flat numbering)
   const int nt1 = cf->ntypes + 1;
   if (!NT1)
     for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) s_cns[t] = cf->cutneighsq[t];
+  if (RHO)
+    for (int t = threadIdx.x; t < nt1 * nt1; t += blockDim.x) {
+      s_rcs[t] = mc->rcutsq[t];
+      s_rih[t] = mc->rcut_inv[t];
+      s_rwn[t] = mp2_wnorm(dim, mc->rcut_inv[t]);
+    }
   const int i = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1), grp = threadIdx.x / G;
   const bool live = i < nlocal;
@@ -579,6 +592,8 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   const double *crow = s_cns + (NT1 ? 0 : ty[i] * nt1);
   const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
   const double di = (double)i;
+  const int rrow = RHO ? (NT1 ? 1 : ty[i]) * nt1 : 0;
+  double racc = 0.0;
   int n = 0;
   int *const row = FILL ? nbr + (stride > 0 ? (size_t)i * stride : (size_t)off[i]) : nullptr;
   const int cap = stride > 0 ? stride : 0x7fffffff;
@@ -602,18 +617,29 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       const double rsq = rsq_ref(xi.x - xj[u].x, xi.y - xj[u].y, xi.z - xj[u].z);
       const bool hit = (p0 + lane + u * G < T) && (xj[u].w != di) &&
                        rsq <= (NT1 ? cns1 : crow[tj[u]]);
+      if (RHO) {  // (k_mp2_rhosum's term)
+        const int pt = rrow + tj[u];
+        double r, ir;
+        mp2_r_ir(rsq, r, ir);
+        const double w = q5_w(3.0 * (r * s_rih[pt])) * s_rwn[pt];
+        racc += (hit && rsq < s_rcs[pt]) ? w : 0.0;
+      }
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
         // tbits 1 (strided rows, several types): the neighbour's type rides in the entry's
         // bits 28-30 (SPH_TBIT_SHIFT), so the pair passes need no type gather; tbits 2 (the
-        // multiphase engine's CSR rows): bit 31 = the pair is i's in the half list
-        // (k_mp_gather), frozen at this build as the reference's half list is
+        // multiphase engine's rows): bit 31 = the pair is i's in the half list
+        // (k_mp_gather), frozen at this build as the reference's half list is, and the
+        // type - 1 in bits 28-30 (MP_NMASK)
         if (hit && qq < cap) {
           const int j = (int)xj[u].w;
           int ent = j;
           if (tbits == 1) ent |= (tj[u] - 1) << SPH_TBIT_SHIFT;
-          if (tbits == 2 && half_keep(i, j, nlocal, xi, xj[u])) ent |= (int)0x80000000u;
+          if (tbits == 2) {  // (+ the type, MpArgs::typed)
+            ent |= (tj[u] - 1) << 28;
+            if (half_keep(i, j, nlocal, xi, xj[u])) ent |= (int)0x80000000u;
+          }
           row[perm_g > 0 ? tpos(qq, perm_g, perm_pi) : qq] = ent;
         }
         pos += __popcll(m);
@@ -628,6 +654,13 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   } else if (stride > 0 && lane == 0) {
     cnt[i] = pos;
     if (pos > stride) atomicOr(ovf, 1);
+  }
+  if (RHO) {
+    racc = group_sum<G>(racc);
+    if (lane == 0) {
+      const int pt = rrow + (NT1 ? 1 : ty[i]);
+      rho[i] = (q5_w(0.0) * s_rwn[pt] + racc) * rm[i];
+    }
   }
 }
 

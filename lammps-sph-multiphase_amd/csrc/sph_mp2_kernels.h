@@ -129,9 +129,9 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
     int tj[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) {
-      const int j = (k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg]) & MP_NMASK;
+      const int e = k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg], j = e & MP_NMASK;
       xj[u] = a.xf[j];
-      tj[u] = a.ty[j];
+      tj[u] = a.typed ? mp_etype(e) : a.ty[j];
     }
 #pragma unroll
     for (int u = 0; u < NU; u++) {
@@ -174,9 +174,9 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
     int tj[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) {
-      const int j = (k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg]) & MP_NMASK;
+      const int e = k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg], j = e & MP_NMASK;
       xj[u] = a.xs[j];
-      tj[u] = a.ty[j];
+      tj[u] = a.typed ? mp_etype(e) : a.ty[j];
     }
 #pragma unroll
     for (int u = 0; u < NU; u++) {
@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
       xjs[u] = a.pA[j];
       v4js[u] = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
       cjs[u] = (fj ? a.pF : a.pS)[j];
-      tjs[u] = a.ty[j];
+      tjs[u] = a.typed ? mp_etype(jrs[u]) : a.ty[j];
     }
 #pragma unroll
     for (int u = 0; u < NU; u++) {

@@ -19,10 +19,13 @@
 namespace sph {
 
 // Engine full lists carry the half list's orientation of each pair, frozen at the build as
-// the reference's half list is, in bit 31 of the entry: mask with MP_NMASK
-// (LAMMPS' NEIGHMASK idiom; written by k_neigh3's fill).  Lists from the pair-style layer
-// never set it.
-constexpr int MP_NMASK = 0x7fffffff;
+// the reference's half list is, in bit 31 of the entry, and the neighbour's type - 1 in bits
+// 28-30 (MpArgs::typed; written by k_neigh3's fill): mask with MP_NMASK (LAMMPS' NEIGHMASK
+// idiom).  Lists from the pair-style layer set neither; every multiphase list indexes fewer
+// than 2^28 atoms (MP_MAXALL, checked where lists are staged or built).
+constexpr int MP_NMASK = 0x0fffffff;
+constexpr long long MP_MAXALL = 1ll << 28;
+__device__ __forceinline__ int mp_etype(int e) { return ((e >> 28) & 7) + 1; }
 
 struct MpCoefs {
   int ntypes, dim;
@@ -118,6 +121,7 @@ struct MpArgs {
   double4 *cg;    // colorgradient out (nall)
   const double4 *cgi;  // surfacetension: colorgradient of every atom (nall, x y z used)
   int exp;             // study (SPH_MPX): 1 = skip the Newton-3 atomics onto j
+  int typed;           // entries carry the neighbour's type (engine lists, mp_etype)
   int rev;             // half list with its reverse list: j share gathered (k_mp_half REV)
   const int *roff, *rnbr;  // reverse half list: row j holds the atoms whose half row has j
   int nrows;               // reverse rows (nall with newton_pair, else nlocal)

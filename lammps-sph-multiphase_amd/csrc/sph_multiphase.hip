@@ -57,6 +57,8 @@ void mp_ready(sph_hip_ctx *c, const char *who, bool have) {
   SPH_REQUIRE(c->list_kind >= 0, SPH_HIP_EINVAL, "%s: no neighbor list staged", who);
   SPH_REQUIRE(c->have_mp_atoms, SPH_HIP_EINVAL,
               "%s: per-atom rmass/cv not staged (sph_hip_atoms_multiphase)", who);
+  SPH_REQUIRE((long long)c->nlocal + c->nghost < MP_MAXALL, SPH_HIP_EOVERFLOW,
+              "%s: the multiphase kernels index at most 2^28 atoms", who);
   SPH_HIP_TRY(hipSetDevice(c->device));
   if (!c->dm) SPH_HIP_TRY(hipMalloc(&c->dm, sizeof(MpCoefs)));
   c->hm.ntypes = c->ntypes;

@@ -29,6 +29,8 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
   SPH_REQUIRE(*seed > 0, SPH_HIP_EINVAL, "Invalid seed for Park random # generator");
   SPH_REQUIRE(c->list_kind == SPH_LIST_FULL, SPH_HIP_EINVAL,
               "sph_hip_phasechange: needs the fix's FULL neighbor list staged");
+  SPH_REQUIRE((long long)c->nlocal + c->nghost < MP_MAXALL, SPH_HIP_EOVERFLOW,
+              "sph_hip_phasechange: at most 2^28 atoms");
   SPH_REQUIRE(c->have_mp_atoms, SPH_HIP_EINVAL,
               "sph_hip_phasechange: per-atom rmass/cv not staged (sph_hip_atoms_multiphase)");
   SPH_REQUIRE(p->to_mass > 0.0 && p->maxattempt >= 1, SPH_HIP_EINVAL,

@@ -530,8 +530,11 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          int tbits, const MpCoefs *__restrict__ mc = nullptr,
          const double *__restrict__ rm = nullptr, double *__restrict__ rho = nullptr) {
   constexpr int R = 2, NB = (2 * R + 1) * (2 * R + 1), GR = 256 / G, KB = (NB + G - 1) / G;
+  static_assert(!RHO || FILL, "the rhosum terms ride on the fill passes");
   __shared__ double s_cns[NT2];
   __shared__ double s_rcs[RHO ? NT2 : 1], s_rih[RHO ? NT2 : 1], s_rwn[RHO ? NT2 : 1];
+  __shared__ double s_hr[RHO ? GR : 1][RHO ? G * U : 1];  // a chunk's hits: rsq
+  __shared__ int s_hp[RHO ? GR : 1][RHO ? G * U : 1];     //   and pair type
   __shared__ int s_rs[GR][NB];       // first candidate (position in xb) of each bin-row
   __shared__ int s_pre[GR][NB + 1];  // candidates before each bin-row (flat numbering)
   const int nt1 = cf->ntypes + 1;
@@ -602,6 +605,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   const unsigned long long gmask = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
   int ptr = 0;  // bin-row holding this lane's next candidate (monotone)
   for (int p0 = 0; p0 < T; p0 += G * U) {  // group-uniform trip count
+    const int pos0 = pos;
     double4 xj[U];
     int tj[U];
 #pragma unroll
@@ -617,16 +621,13 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       const double rsq = rsq_ref(xi.x - xj[u].x, xi.y - xj[u].y, xi.z - xj[u].z);
       const bool hit = (p0 + lane + u * G < T) && (xj[u].w != di) &&
                        rsq <= (NT1 ? cns1 : crow[tj[u]]);
-      if (RHO) {  // (k_mp2_rhosum's term)
-        const int pt = rrow + tj[u];
-        double r, ir;
-        mp2_r_ir(rsq, r, ir);
-        const double w = q5_w(3.0 * (r * s_rih[pt])) * s_rwn[pt];
-        racc += (hit && rsq < s_rcs[pt]) ? w : 0.0;
-      }
       if (FILL) {
         const unsigned long long m = (__ballot(hit) >> gbase) & gmask;
         const int qq = pos + __popcll(m & ((1ull << lane) - 1ull));
+        if (RHO && hit) {  // the chunk's hits, compacted, for the rhosum terms below
+          s_hr[grp][qq - pos0] = rsq;
+          s_hp[grp][qq - pos0] = rrow + tj[u];
+        }
         // tbits 1 (strided rows, several types): the neighbour's type rides in the entry's
         // bits 28-30 (SPH_TBIT_SHIFT), so the pair passes need no type gather; tbits 2 (the
         // multiphase engine's rows): bit 31 = the pair is i's in the half list
@@ -646,6 +647,18 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       } else {
         n += hit ? 1 : 0;
       }
+    }
+    if (RHO) {  // (k_mp2_rhosum's term) over the chunk's hits only: G lanes, <= G*U hits
+      __builtin_amdgcn_wave_barrier();
+      for (int k = lane; k < pos - pos0; k += G) {
+        const double rsq = s_hr[grp][k];
+        const int pt = s_hp[grp][k];
+        double r, ir;
+        mp2_r_ir(rsq, r, ir);
+        const double w = q5_w(3.0 * (r * s_rih[pt])) * s_rwn[pt];
+        racc += rsq < s_rcs[pt] ? w : 0.0;
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
   if (!FILL) {

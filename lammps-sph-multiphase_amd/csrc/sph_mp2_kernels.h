@@ -243,6 +243,8 @@ __device__ __forceinline__ double3 mp2_svec(int dim, const double4 &w, double3 e
 // j = entry; bit 31 = the pair is i's in the half list): i's values fresh unless j is a ghost
 // whose image pair belongs to j's owner, j's fresh if owned or if the pair is not i's -- the
 // pair terms themselves with i first.
+// (108 VGPRs, 4 waves per SIMD: asking for 5 or 6 spills -- 32 / 40 ms per C5 step instead
+// of 12.8, profiles/r03/README.md)
 template <int G, bool TAIT, bool SURF, bool HEAT>
 __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];

@@ -169,14 +169,25 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
   double gx = 0.0, gy = 0.0, gz = 0.0;
   const MpRow rw(a.off, a.cnt, a.stride, row);
   constexpr int NU = SPH_MP2_NU;
+  int jn[NU];  // (next round's entries in flight, as k_mp2_gather)
+#pragma unroll
+  for (int u = 0; u < NU; u++) {
+    const long long k = rw.beg + lane + u * G;
+    jn[u] = k < rw.end ? a.nbr[k] : 0;
+  }
   for (long long k0 = rw.beg + lane; k0 < rw.end; k0 += NU * G) {
     double4 xj[NU];
     int tj[NU];
 #pragma unroll
     for (int u = 0; u < NU; u++) {
-      const int e = k0 + u * G < rw.end ? a.nbr[k0 + u * G] : a.nbr[rw.beg], j = e & MP_NMASK;
+      const int e = k0 + u * G < rw.end ? jn[u] : jn[0], j = e & MP_NMASK;
       xj[u] = a.xs[j];
       tj[u] = a.typed ? mp_etype(e) : a.ty[j];
+    }
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const long long k = k0 + (NU + u) * G;
+      jn[u] = k < rw.end ? a.nbr[k] : 0;
     }
 #pragma unroll
     for (int u = 0; u < NU; u++) {
@@ -266,11 +277,24 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   constexpr int NU = SPH_MP2_NU;
   const MpRow rw(a.off, a.cnt, a.stride, row);
   const long long kend = rw.end;
+  // the next round's entries are read while this round computes (the rows stream from HBM:
+  // one dependent miss per round instead of two)
+  int jn[NU];
+#pragma unroll
+  for (int u = 0; u < NU; u++) {
+    const long long k = rw.beg + lane + u * G;
+    jn[u] = k < kend ? a.nbr[k] : 0;
+  }
   for (long long k0 = rw.beg + lane; k0 < kend; k0 += NU * G) {
     int jrs[NU], tjs[NU];
     double4 xjs[NU], v4js[NU], cjs[NU];
 #pragma unroll
-    for (int u = 0; u < NU; u++) jrs[u] = k0 + u * G < kend ? a.nbr[k0 + u * G] : a.nbr[rw.beg];
+    for (int u = 0; u < NU; u++) jrs[u] = k0 + u * G < kend ? jn[u] : jn[0];
+#pragma unroll
+    for (int u = 0; u < NU; u++) {
+      const long long k = k0 + (NU + u) * G;
+      jn[u] = k < kend ? a.nbr[k] : 0;
+    }
 #pragma unroll
     for (int u = 0; u < NU; u++) {
       const int j = jrs[u] & MP_NMASK;

@@ -113,6 +113,11 @@ static bool direct_env() {
   return v;
 }
 static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
+// SPH_HIL_POW2 (default 1): power-of-two Hilbert cells per axis of the owned sub-box
+static bool hil_pow2() {
+  static bool v = study_int("SPH_HIL_POW2", 1) != 0;
+  return v;
+}
 // SPH_SORT_EVERY (default 10): steps between spatial sorts of the owned atoms at rebuilds
 static int sort_every() {
   static int v = study_int("SPH_SORT_EVERY", 10);
@@ -389,8 +394,16 @@ struct sph_engine {
           kbn.inv[k] = 0.0;
           continue;
         }
-        int nc = std::max(1, (int)std::ceil(ext / (cutneighmax / div)));
-        nc = std::min(nc, 1024);
+        // a power of two per axis: a cubic sub-box (and the 2x1x1 / 2x2x1 / 2x2x2 bricks
+        // of a cubic box) is then whole octants of the curve's cube, which the curve leaves
+        // only between octants -- with any other count it exits and re-enters the
+        // rows' region, and a block of consecutive rows spanning such a jump outgrows the
+        // build's candidate image (seen at 125k particles per brick: the whole build fell
+        // back to 32-row blocks)
+        const int nc0 = std::max(1, (int)std::ceil(ext / (cutneighmax / div)));
+        int nc = 1;
+        while (nc < nc0 && nc < 1024) nc *= 2;
+        if (!hil_pow2()) nc = std::min(nc0, 1024);
         kbn.lo[k] = sublo[k];
         kbn.nb[k] = nc;
         kbn.inv[k] = nc / ext;

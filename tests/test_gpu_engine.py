@@ -179,3 +179,28 @@ def test_full_size_properties(gpu, sph_amd, path):
     eng.run(3)
     got = eng.get_atoms()
     assert np.isfinite(got["x"]).all() and np.isfinite(got["f"]).all()
+
+
+def test_timing_classes(gpu, sph_amd):
+    """sph_engine_set_timing's class mask (bench.py's timed region): only the asked classes
+    are timed, the results do not depend on it, and "all" times every class."""
+    s = c2_system(12)
+    ph = po.c2_physics()
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(12)
+    eng = engine_for(sph_amd, s, ph)
+    eng.setup()
+    eng.set_timing(True, classes=(eng.T_RHO, eng.T_TAIT))
+    eng.run(12)                                # (a rebuild at step 10)
+    eng.sync()
+    st = eng.stats()
+    assert st["n_rhosum"] >= 12 and st["n_tait"] >= 12
+    assert st["ms_rhosum"] > 0 and st["ms_tait"] > 0
+    assert st["n_neigh"] == 0 and st["ms_neigh"] == 0 and st["ms_integrate"] == 0
+    compare(eng, ref, path=0)
+    eng.set_timing(True)
+    eng.run(2)
+    eng.sync()
+    st = eng.stats()
+    assert st["ms_integrate"] > 0

@@ -236,7 +236,7 @@ struct sph_engine {
   bool dr_ok = false;
   std::vector<int> dr_peer;
   std::vector<size_t> dr_soff, dr_roff;
-  DBuf<int> dr_sidx, dr_rslot, dr_self;
+  DBuf<int> dr_sidx, dr_rslot, dr_self, dr_req;
   int dr_nself = 0;
   std::vector<const void *> dr_sb;
   std::vector<void *> dr_rb;
@@ -657,7 +657,7 @@ struct sph_engine {
     }
     const int np = (int)dr_peer.size();
     const size_t S = dr_soff.back(), R = dr_roff.back();
-    DBuf<int> req;
+    DBuf<int> &req = dr_req;  // (persistent: no hipMalloc / synchronising hipFree per rebuild)
     req.reserve(R > 0 ? R : 1);
     dr_sidx.reserve(S > 0 ? S : 1);
     dr_rslot.reserve(R > 0 ? R : 1);
@@ -681,8 +681,7 @@ struct sph_engine {
     dr_self.reserve(dr_nself > 0 ? dr_nself : 1);
     if (dr_nself)
       SPH_HIP_TRY(hipMemcpyAsync(dr_self.p, byg.data() + beg[me], dr_nself * sizeof(int), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));  // (req and the host vectors go out of scope)
-    req.release();
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host vectors go out of scope)
     dr_ok = true;
   }
   // one direct forward of rec-byte records: pack the send lists, one exchange, unpack
@@ -2295,7 +2294,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
   for (auto *b : {&e->cg, &e->cgS, &e->cgF, &e->recA, &e->recK, &e->recF, &e->recS}) b->release();
   if (e->dm) (void)hipFree(e->dm);
-  for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->pc_flag,
+  for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->dr_req, &e->pc_flag,
                   &e->pc_cand, &e->pc_otag, &e->pc_idx})
     b->release();
   for (auto *b : {&e->pc_rec, &e->pc_gat, &e->pc_Wd, &e->pc_vals, &e->pc_nrec}) b->release();

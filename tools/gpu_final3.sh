@@ -27,3 +27,5 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
 cd "$R" && python3 tools/kstats.py "$(find "$O/prof_c5" -name '*kernel_stats.csv' | head -1)" 8
 timeout -k 10 400 python3 bench.py --workload c3 --steps 20 --warmup 5 > "$O/bench_c3.json" 2> "$O/bench_c3.err" || { tail -5 "$O/bench_c3.err"; exit 1; }
 echo "c3: $(cut -c1-200 "$O/bench_c3.json")"
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu --edge 50 --comm-loopback > "$O/bench_lb125k.json" 2> "$O/bench_lb125k.err" || { tail -5 "$O/bench_lb125k.err"; exit 1; }
+echo "lb125k: $(cut -c1-200 "$O/bench_lb125k.json")"

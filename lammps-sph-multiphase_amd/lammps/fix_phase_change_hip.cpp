@@ -70,6 +70,8 @@ FixPhaseChangeHIP::FixPhaseChangeHIP(LAMMPS *lmp, int narg, char **arg)
       maxattempt = atoi(arg[iarg + 1]);
       iarg += 2;
     } else if (strcmp(arg[iarg], "units") == 0 && iarg + 2 <= narg) {
+      // the reference rejects 'units lattice' itself (fix_phase_change.cpp:381-386), and its
+      // scaleflag (:83) is read nowhere: no length of the fix is lattice-scaled either way
       if (strcmp(arg[iarg + 1], "lattice") == 0)
         error->all(FLERR, "Illegal fix phase_change command: 'units lattice' is not implemented");
       else if (strcmp(arg[iarg + 1], "box") != 0)

@@ -1165,7 +1165,7 @@ struct sph_engine {
                        0, bkey2.p, qbeg.p);
     xpos.reserve(nall);
     hipLaunchKernelGGL(k_bin_copy, dim3(blocks(nall)), dim3(BLK), 0, s, nall, bidx2.p, xf.p,
-                       ty.p, xb.p, tb.p, xpos.p);
+                       ty.p, xb.p, tb.p, xpos.p, mp ? 1 : 0);
   }
   // Global-index full list (k_neigh3, Neighbor::full_bin membership) of the owned rows at
   // positions xi (default: the current ones, as binned by bin_q): CSR (count pass, scan,
@@ -1190,21 +1190,30 @@ struct sph_engine {
       const bool t = nt1();
       int *const cnt_out = (!fill || stride > 0) ? ccnt.p : (int *)nullptr;
       int *const rows = dst ? dst : nbr.p;
-#define SPH_N3(F, T)                                                                           \
-  hipLaunchKernelGGL((k_neigh3<G, 4, F, T>), grid, block, 0, s, n, qb, cfg.dim, xi_src, ty.p, \
+#define SPH_N3P(F, T, P)                                                                       \
+  hipLaunchKernelGGL((k_neigh3<G, 4, F, T, false, P>), grid, block, 0, s, n, qb, cfg.dim,       \
+                     xi_src, ty.p,                                                             \
                      xb.p, tb.p, qbeg.p, dc, cnt_out,                                          \
                      (F && stride == 0) ? off.p : (const int *)nullptr,                        \
                      F ? rows : (int *)nullptr, stride, mx.p, stride > 0 ? list_perm_g : 0,    \
                      list_perm_pi, mp ? 2 : ((stride > 0 && list_tbits) ? 1 : 0))
 #define SPH_N3R(T)                                                                             \
-  hipLaunchKernelGGL((k_neigh3<G, 4, true, T, true>), grid, block, 0, s, n, qb, cfg.dim, xi_src, \
+  hipLaunchKernelGGL((k_neigh3<G, 4, true, T, true, true>), grid, block, 0, s, n, qb, cfg.dim,  \
+                     xi_src,                                                                   \
                      ty.p, xb.p, tb.p, qbeg.p, dc, cnt_out,                                    \
                      stride == 0 ? off.p : (const int *)nullptr, rows, stride, mx.p, 0, 0, 2, \
                      dm, rm.p, rho_tmp.p)
+      // (mp: xb packs the types, k_bin_copy tpack)
+#define SPH_N3(F, T)                                                                           \
+  do {                                                                                        \
+    if (mp) SPH_N3P(F, T, true);                                                              \
+    else SPH_N3P(F, T, false);                                                                \
+  } while (0)
       if (fill && rho) { if (t) SPH_N3R(true); else SPH_N3R(false); }
       else if (fill) { if (t) SPH_N3(true, true); else SPH_N3(true, false); }
       else { if (t) SPH_N3(false, true); else SPH_N3(false, false); }
 #undef SPH_N3
+#undef SPH_N3P
 #undef SPH_N3R
     };
     mx.reserve(8);

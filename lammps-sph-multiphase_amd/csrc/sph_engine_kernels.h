@@ -474,15 +474,17 @@ struct QBins {
 };
 
 // (xpos, if given: the inverse, atom -> position in xb)
+// (tpack: .w = j | (type - 1) << 28 -- the multiphase engine's list entry itself, so its
+// builds need no type gather; nall < MP_MAXALL there)
 static __global__ void k_bin_copy(int n, const int *__restrict__ perm,
                                   const double4 *__restrict__ xf, const int *__restrict__ ty,
                                   double4 *__restrict__ xb, int *__restrict__ tb,
-                                  int *__restrict__ xpos = nullptr) {
+                                  int *__restrict__ xpos = nullptr, int tpack = 0) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const int j = perm[p];
   const double4 x = xf[j];
-  xb[p] = make_double4(x.x, x.y, x.z, (double)j);
+  xb[p] = make_double4(x.x, x.y, x.z, (double)(tpack ? j | ((ty[j] - 1) << 28) : j));
   tb[p] = ty[j];
   if (xpos) xpos[j] = p;
 }
@@ -520,7 +522,7 @@ __device__ __forceinline__ bool half_keep(int i, int j, int nlocal, const double
 // skin 0 as bubble.lmp): rhosum/multiphase (pair_sph_rhosum_multiphase.cpp:118-167) summed
 // over the row's hits as they are found -- the pair set and positions k_mp2_rhosum would walk
 // right after -- into rho (owned rows; rm = rmass); the separate rhosum pass is then skipped
-template <int G, int U, bool FILL, bool NT1, bool RHO = false>
+template <int G, int U, bool FILL, bool NT1, bool RHO = false, bool TP = false>
 __global__ void __launch_bounds__(256)
 k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
          const int *__restrict__ ty, const double4 *__restrict__ xb,
@@ -594,7 +596,8 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
   const int T = s_pre[grp][NB];
   const double *crow = s_cns + (NT1 ? 0 : ty[i] * nt1);
   const double cns1 = NT1 ? cf->cutneighsq[3] : 0.0;
-  const double di = (double)i;
+  // (TP: xb.w packs the type, k_bin_copy tpack)
+  const double di = TP ? (double)(i | ((NT1 ? 0 : ty[i] - 1) << 28)) : (double)i;
   const int rrow = RHO ? (NT1 ? 1 : ty[i]) * nt1 : 0;
   double racc = 0.0;
   int n = 0;
@@ -614,7 +617,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       while (pp >= s_pre[grp][ptr + 1]) ptr++;
       const int p = s_rs[grp][ptr] + (pp - s_pre[grp][ptr]);
       xj[u] = xb[p];
-      tj[u] = NT1 ? 1 : tb[p];
+      tj[u] = NT1 ? 1 : TP ? ((int)xj[u].w >> 28) + 1 : tb[p];
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -634,7 +637,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
         // (k_mp_gather), frozen at this build as the reference's half list is, and the
         // type - 1 in bits 28-30 (MP_NMASK)
         if (hit && qq < cap) {
-          const int j = (int)xj[u].w;
+          const int j = (int)xj[u].w & (TP ? MP_NMASK : 0x7fffffff);
           int ent = j;
           if (tbits == 1) ent |= (tj[u] - 1) << SPH_TBIT_SHIFT;
           if (tbits == 2) {  // (+ the type, MpArgs::typed)

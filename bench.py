@@ -138,6 +138,23 @@ def share_uid(dist, rank, make_uid):
     return obj[0]
 
 
+def attach_comm(eng, sph, args, dist, rank, world):
+    """The communicator of a multi-rank run: RCCL (default: one rank per GPU, ncclSend/Recv
+    over xGMI) or the node-local process world (--transport ipc: hipIpc-exported device
+    outboxes; ipc-host: host shared memory), which lets several ranks share one GPU (RCCL
+    refuses that).  The name / unique id goes from rank 0 to every rank the same way."""
+    if args.transport == "rccl":
+        eng.comm_init(share_uid(dist, rank, sph.comm_uid), world, rank)
+    else:
+        name = share_uid(dist, rank, lambda: f"/sphbench_{os.getpid()}_{time.time_ns() % 10**9}")
+        eng.comm_ipc(name, world, rank, 0 if args.transport == "ipc" else 1)
+
+
+def transport_name(args):
+    return {"rccl": "RCCL", "ipc": "hipIpc process-world",
+            "ipc-host": "host-shared-memory process-world"}[args.transport]
+
+
 class stdout_to_stderr:
     """RCCL prints its version banner on fd 1 at communicator init; keep stdout for the one
     JSON line of the bench contract."""
@@ -769,15 +786,13 @@ def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
     eng.phase_change(pc["Tc"], pc["Tt"], pc["Hwv"], pc["dr"], pc["to_mass"], pc["cutoff"],
                      pc["from_type"], pc["to_type"], nevery=pc["nevery"], seed=pc["seed"],
                      prob=pc["prob"])
-    uid = share_uid(dist, rank, sph.comm_uid) if world > 1 else None
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
     with stdout_to_stderr():
         if world > 1:
-            eng.comm_init(uid, world, rank)
+            attach_comm(eng, sph, args, dist, rank, world)
         eng.setup()
         eng.run(args.warmup)
     eng.sync()
@@ -816,8 +831,8 @@ def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
         tt = torch.tensor([ins], dtype=torch.int64)
         dist.all_reduce(tt)
         ins = int(tt.item())
-    par = (f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo exchange + migration + "
-           "fix phase_change dmass reverse comm and tag_extend, one rank per GPU"
+    par = (f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, {transport_name(args)} halo exchange "
+           "+ migration + fix phase_change dmass reverse comm and tag_extend, one rank per GPU"
            if world > 1 else "single GPU")
     out = {
         "metric": "particle-steps/s, C5 bubble_growth multiphase stack + fix phase_change",
@@ -984,6 +999,10 @@ def main():
                     help="one GPU: route the periodic self swaps through a one-rank RCCL "
                          "communicator (send/recv to itself) -- the multi-GPU halo path's cost "
                          "without the xGMI transfer")
+    ap.add_argument("--transport", choices=["rccl", "ipc", "ipc-host"], default="rccl",
+                    help="N > 1: rccl = one rank per GPU over RCCL/xGMI (default); ipc / "
+                         "ipc-host = the node-local process world (hipIpc device outboxes / "
+                         "host shared memory), ranks may share a GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="host path only (rank launch, decomposition, timing reduction), no "
                          "HIP device: prints the JSON line with value null")
@@ -1052,7 +1071,7 @@ def main():
                     "sph/taitwater, periodic, skin 0.3, rebuild every 10")
     parallelism = (("single GPU, halos through RCCL loopback" if args.comm_loopback
                     else "single GPU") if world == 1 else
-                   f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, RCCL halo exchange + "
+                   f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, {transport_name(args)} halo exchange + "
                    "migration, one rank per GPU")
     base = {
         "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
@@ -1090,10 +1109,9 @@ def main():
     eng.set_atoms(x, v, t, rho, e, cv)
     if world > 1:
         eng.set_tags(tags)
-    uid = share_uid(dist, rank, sph.comm_uid) if world > 1 else None
     with stdout_to_stderr():  # communicator init, first exchanges and warmup
         if world > 1:
-            eng.comm_init(uid, world, rank)
+            attach_comm(eng, sph, args, dist, rank, world)
         elif args.comm_loopback:
             eng.comm_init(sph.comm_uid(), 1, 0)
             eng.comm_loopback(True)

@@ -297,6 +297,12 @@ typedef struct {
   int stage_max;               /* block path: largest block union (LDS records) */
   double ms_rhosum, ms_tait, ms_heat, ms_integrate, ms_comm, ms_neigh; /* event-timed */
   int64_t n_rhosum, n_tait, n_heat, n_neigh;  /* launches timed */
+  int blk_nbig;                /* block path: blocks of the last build whose union exceeds the
+                                  force pass's LDS image (walked by the second launch) */
+  int inner_rows;              /* block path: inner rows were built at the last rebuild */
+  int inner_live;              /* ... and no atom has moved past their margin since (the pair
+                                  passes walk them) */
+  int pad_;
 } sph_engine_stats;
 
 typedef struct sph_engine sph_engine;
@@ -322,6 +328,13 @@ typedef struct sph_local_world sph_local_world;
 int sph_local_world_create(int nranks, sph_local_world **out);
 int sph_local_world_destroy(sph_local_world *w);
 int sph_engine_comm_local(sph_engine *e, sph_local_world *w, int rank);
+/* Node-local world of PROCESSES without RCCL (one process per brick, any devices of the
+   node, incl. several processes on one GPU, which RCCL refuses): `name` ("/word", chosen by
+   rank 0 and distributed by the caller like the RCCL uid) names a POSIX shared-memory
+   control segment; mode 0 moves halos device-to-device through hipIpc-exported outboxes,
+   mode 1 stages them through host shared memory.  Same Transport calls, same order, as
+   RCCL (comm_brick.cpp:444-506, 696-864, 999-1030).  Collective: every rank calls it. */
+int sph_engine_comm_ipc(sph_engine *e, const char *name, int nranks, int rank, int mode);
 int sph_engine_set_tags(sph_engine *e, const int *tags);
 
 /* Owned particles of this rank (tag order is the caller's order; results are returned in

@@ -89,7 +89,8 @@ class EngineStats(C.Structure):
         ("ms_rhosum", C.c_double), ("ms_tait", C.c_double), ("ms_heat", C.c_double),
         ("ms_integrate", C.c_double), ("ms_comm", C.c_double), ("ms_neigh", C.c_double),
         ("n_rhosum", C.c_int64), ("n_tait", C.c_int64), ("n_heat", C.c_int64),
-        ("n_neigh", C.c_int64),
+        ("n_neigh", C.c_int64), ("blk_nbig", C.c_int), ("inner_rows", C.c_int),
+        ("inner_live", C.c_int), ("pad_", C.c_int),
     ]
 
     def as_dict(self):
@@ -138,6 +139,7 @@ EXPORTS = {
     "sph_local_world_create": (_i, [_i, C.POINTER(_vp)]),
     "sph_local_world_destroy": (_i, [_vp]),
     "sph_engine_comm_local": (_i, [_vp, _vp, _i]),
+    "sph_engine_comm_ipc": (_i, [_vp, C.c_char_p, _i, _i, _i]),
     "sph_engine_set_tags": (_i, [_vp, _ip]),
     "sph_engine_set_atoms": (_i, [_vp, _i, _dp, _dp, _ip, _dp, _vp, _vp]),
     "sph_engine_setup": (_i, [_vp]),
@@ -634,6 +636,14 @@ class Engine:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = C.create_string_buffer(bytes(uid), 128)
         _chk(self.L.sph_engine_comm_init(self.h, buf, nranks, rank))
+
+    IPC_DEVICE, IPC_HOST = 0, 1
+
+    def comm_ipc(self, name: str, nranks: int, rank: int, mode: int = 0):
+        """Node-local world of processes (sph_engine_comm_ipc): `name` = "/word" chosen by
+        rank 0 and shared by the launcher; mode IPC_DEVICE (hipIpc outboxes, device copies)
+        or IPC_HOST (host shared-memory staging).  Collective over the ranks."""
+        _chk(self.L.sph_engine_comm_ipc(self.h, name.encode(), nranks, rank, int(mode)))
 
     def comm_loopback(self, on: bool = True):
         """One brick, self swaps through the attached communicator (RCCL send/recv to self)."""

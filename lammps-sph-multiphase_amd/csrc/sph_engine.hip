@@ -21,6 +21,7 @@
 #include "sph_blk_kernels.h"
 #include "sph_engine_kernels.h"
 #include "sph_engine_mp.h"
+#include "sph_ipc.h"
 #include "sph_mp2_kernels.h"
 #include "sph_pc.h"
 #include "sph_row2_kernels.h"
@@ -2763,6 +2764,16 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->n_tait = e->nlaunch[T_TAIT];
   st->n_heat = e->nlaunch[T_HEAT];
   st->n_neigh = e->nlaunch[T_NEIGH];
+  st->blk_nbig = e->blk ? e->blk_nbig : 0;
+  st->inner_rows = e->inner ? 1 : 0;
+  st->inner_live = 0;
+  if (e->inner && e->moved.p) {
+    int mv = 1;
+    SPH_HIP_TRY(hipMemcpyAsync(&mv, e->moved.p, sizeof(int), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipStreamSynchronize(e->s));
+    st->inner_live = mv == 0 ? 1 : 0;
+  }
+  st->pad_ = 0;
   SPH_API_END
 }
 
@@ -2850,6 +2861,14 @@ int sph_engine_comm_local(sph_engine *e, sph_local_world *w, int rank) {
   LocalWorld *lw = reinterpret_cast<LocalWorld *>(w);
   SPH_REQUIRE(rank >= 0 && rank < lw->n, SPH_HIP_EINVAL, "rank %d outside [0,%d)", rank, lw->n);
   attach(e, new LocalTransport(lw, rank));
+  SPH_API_END
+}
+
+int sph_engine_comm_ipc(sph_engine *e, const char *name, int nranks, int rank, int mode) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e && name, SPH_HIP_EINVAL, "sph_engine_comm_ipc: NULL argument");
+  SPH_HIP_TRY(hipSetDevice(e->device));
+  attach(e, new IpcTransport(name, nranks, rank, mode, e->device));
   SPH_API_END
 }
 

@@ -155,3 +155,16 @@ def test_bench_two_gpus(workload):
         args += ["--edge", "60"]
     out = _bench_json(args)
     assert out["n_gpus"] == 2 and out["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload,edge", [("c2", "24"), ("c5", "30")])
+def test_bench_two_processes_ipc(workload, edge):
+    """`bench.py --gpus 2 --transport ipc` on the one GPU of the test box: bench's own rank
+    launch (fresh processes before any HIP call), the world name broadcast from rank 0,
+    hipIpc halos between the two processes, barrier + max-over-ranks timing, ONE JSON line
+    from rank 0 -- the multi-GPU bench path with only the byte mover swapped."""
+    out = _bench_json(["--gpus", "2", "--transport", "ipc", "--steps", "3", "--warmup", "1",
+                       "--no-cpu", "--workload", workload, "--edge", edge])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert "hipIpc" in out["config"]["parallelism"]

@@ -302,7 +302,8 @@ typedef struct {
   int inner_rows;              /* block path: inner rows were built at the last rebuild */
   int inner_live;              /* ... and no atom has moved past their margin since (the pair
                                   passes walk them) */
-  int pad_;
+  int flags;                   /* bit 0: the last rhosum/multiphase was summed inside the
+                                  list fill (C5: its time is in ms_neigh, not ms_rhosum) */
 } sph_engine_stats;
 
 typedef struct sph_engine sph_engine;
@@ -335,6 +336,14 @@ int sph_engine_comm_local(sph_engine *e, sph_local_world *w, int rank);
    mode 1 stages them through host shared memory.  Same Transport calls, same order, as
    RCCL (comm_brick.cpp:444-506, 696-864, 999-1030).  Collective: every rank calls it. */
 int sph_engine_comm_ipc(sph_engine *e, const char *name, int nranks, int rank, int mode);
+/* Schedule choices that do not change results (parity-tested both ways), set explicitly
+   rather than through the environment; before sph_engine_setup.
+   SPH_TUNE_OVERLAP: bricks on the row path overlap interior rows' passes with the halo
+   exchange (1) or not (0, default).  SPH_TUNE_BLKUMF: cap the block force pass's LDS image
+   at `value` records, blocks with larger unions going to its second launch (0 = auto). */
+#define SPH_TUNE_OVERLAP 1
+#define SPH_TUNE_BLKUMF 2
+int sph_engine_tune(sph_engine *e, int key, int value);
 int sph_engine_set_tags(sph_engine *e, const int *tags);
 
 /* Owned particles of this rank (tag order is the caller's order; results are returned in

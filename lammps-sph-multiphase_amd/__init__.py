@@ -90,7 +90,7 @@ class EngineStats(C.Structure):
         ("ms_integrate", C.c_double), ("ms_comm", C.c_double), ("ms_neigh", C.c_double),
         ("n_rhosum", C.c_int64), ("n_tait", C.c_int64), ("n_heat", C.c_int64),
         ("n_neigh", C.c_int64), ("blk_nbig", C.c_int), ("inner_rows", C.c_int),
-        ("inner_live", C.c_int), ("pad_", C.c_int),
+        ("inner_live", C.c_int), ("flags", C.c_int),
     ]
 
     def as_dict(self):
@@ -140,6 +140,7 @@ EXPORTS = {
     "sph_local_world_destroy": (_i, [_vp]),
     "sph_engine_comm_local": (_i, [_vp, _vp, _i]),
     "sph_engine_comm_ipc": (_i, [_vp, C.c_char_p, _i, _i, _i]),
+    "sph_engine_tune": (_i, [_vp, _i, _i]),
     "sph_engine_set_tags": (_i, [_vp, _ip]),
     "sph_engine_set_atoms": (_i, [_vp, _i, _dp, _dp, _ip, _dp, _vp, _vp]),
     "sph_engine_setup": (_i, [_vp]),
@@ -636,6 +637,12 @@ class Engine:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = C.create_string_buffer(bytes(uid), 128)
         _chk(self.L.sph_engine_comm_init(self.h, buf, nranks, rank))
+
+    TUNE_OVERLAP, TUNE_BLKUMF = 1, 2
+
+    def tune(self, key: int, value: int):
+        """sph_engine_tune: a schedule choice that does not change results (before setup)."""
+        _chk(self.L.sph_engine_tune(self.h, key, int(value)))
 
     IPC_DEVICE, IPC_HOST = 0, 1
 

@@ -15,14 +15,18 @@
 
 using namespace sph;
 
-// SPH_MPREV (default 1): half-list styles gather the j share through the reverse half list
-// instead of scattering it with fp64 atomics
+// half-list styles gather the j share through the reverse half list; study builds only
+// (SPH_MPREV=0) scatter it with fp64 atomics instead
 inline bool sph_rev_on() {
+#ifdef SPH_STUDY
   static const bool v = [] {
     const char *e = getenv("SPH_MPREV");
     return e ? atoi(e) != 0 : true;
   }();
   return v;
+#else
+  return true;
+#endif
 }
 
 // a neighbor list parked in the context while another kind is active (sph_hip_list_keyed)

@@ -107,13 +107,12 @@ static int blk_shape_env() {
   static int v = study_int("SPH_BLK", 0);
   return v;
 }
-// (read per engine at sph_engine_create)
-// SPH_DIRECT (default 1): bricks forward the per-step halos owner -> ghost in one exchange
+// SPH_DIRECT (study builds; default 1): bricks forward the per-step halos owner -> ghost in
+// one exchange
 static bool direct_env() {
-  static bool v = env_int("SPH_DIRECT", 1) != 0;
+  static bool v = study_int("SPH_DIRECT", 1) != 0;
   return v;
 }
-static bool overlap_env() { return env_int("SPH_OVERLAP", 0) != 0; }
 // SPH_HIL_POW2 (default 1): power-of-two Hilbert cells per axis of the owned sub-box
 static bool hil_pow2() {
   static bool v = study_int("SPH_HIL_POW2", 1) != 0;
@@ -209,10 +208,11 @@ struct sph_engine {
   DBuf<unsigned char> fl_in, fl_bd;
   int n_in = 0, n_bd = 0;
   bool ov_ready = false;  // rows_in / rows_bd describe the current list
-  bool overlap = false;   // SPH_OVERLAP at creation
+  bool overlap = false;   // halo/compute overlap (sph_engine_tune SPH_TUNE_OVERLAP)
+  int blkumf = 0;         // force pass LDS image cap in records (SPH_TUNE_BLKUMF; 0 = auto)
   int64_t step = 0;
-  int64_t rho_fused_step = -1;
-  int64_t last_sort = 0;  // step of the last spatial sort of the owned atoms  // step whose rhosum/multiphase the list fill summed (k_neigh3 RHO)
+  int64_t rho_fused_step = -1;  // step whose rhosum/multiphase the list fill summed (k_neigh3 RHO)
+  int64_t last_sort = 0;        // step of the last spatial sort of the owned atoms
   bool setup_done = false;
   bool global_tags = false;
   int last_build = 0;
@@ -1154,6 +1154,9 @@ struct sph_engine {
     qbeg.reserve(nqbins + 1);
     xb.reserve(nall);
     tb.reserve(nall);
+    // (mp: k_bin_copy packs the type into xb.w above bit 28, the list entries' MP_NMASK)
+    SPH_REQUIRE(!mp || (long long)nall < MP_MAXALL, SPH_HIP_EOVERFLOW,
+                "multiphase lists index at most 2^28 atoms per rank (%d)", nall);
     hipLaunchKernelGGL(k_bin_keys, dim3(blocks(nall)), dim3(BLK), 0, s, nall, 0, b, xf.p,
                        bkey.p, bidx.p, 0);
     int endbit = 1;
@@ -1340,7 +1343,7 @@ struct sph_engine {
       // the force pass's image size and its large-union blocks, then ONE read-back
       bl.reserve(nb);
       hipLaunchKernelGGL(k_blk_large_dev, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p,
-                         env_int("SPH_BLKUMF", 0), mx.p, bl.p);
+                         blkumf, mx.p, bl.p);
       int *const hm = h_small;
       SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
@@ -2287,7 +2290,7 @@ int sph_engine_create(int device, const sph_engine_config *cfg, sph_engine **out
     delete e;
     throw;
   }
-  e->overlap = overlap_env();
+  e->overlap = false;
   *out = e;
   SPH_API_END
 }
@@ -2773,7 +2776,7 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
     SPH_HIP_TRY(hipStreamSynchronize(e->s));
     st->inner_live = mv == 0 ? 1 : 0;
   }
-  st->pad_ = 0;
+  st->flags = (e->rho_fused_step >= 0 && e->rho_fused_step == e->step) ? 1 : 0;
   SPH_API_END
 }
 
@@ -2869,6 +2872,21 @@ int sph_engine_comm_ipc(sph_engine *e, const char *name, int nranks, int rank, i
   SPH_REQUIRE(e && name, SPH_HIP_EINVAL, "sph_engine_comm_ipc: NULL argument");
   SPH_HIP_TRY(hipSetDevice(e->device));
   attach(e, new IpcTransport(name, nranks, rank, mode, e->device));
+  SPH_API_END
+}
+
+int sph_engine_tune(sph_engine *e, int key, int value) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_tune: NULL engine");
+  SPH_REQUIRE(!e->setup_done, SPH_HIP_EINVAL, "sph_engine_tune: before sph_engine_setup");
+  switch (key) {
+    case SPH_TUNE_OVERLAP: e->overlap = value != 0; break;
+    case SPH_TUNE_BLKUMF:
+      SPH_REQUIRE(value >= 0, SPH_HIP_EINVAL, "sph_engine_tune: BLKUMF %d < 0", value);
+      e->blkumf = value;
+      break;
+    default: SPH_REQUIRE(false, SPH_HIP_EINVAL, "sph_engine_tune: unknown key %d", key);
+  }
   SPH_API_END
 }
 

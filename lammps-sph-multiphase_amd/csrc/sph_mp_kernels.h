@@ -24,6 +24,9 @@ namespace sph {
 // idiom).  Lists from the pair-style layer set neither; every multiphase list indexes fewer
 // than 2^28 atoms (MP_MAXALL, checked where lists are staged or built).
 constexpr int MP_NMASK = 0x0fffffff;
+// type - 1 in bits 28-30: three bits, so at most 8 types (the self-exclusion test xj.w != di
+// and the j decode would alias otherwise)
+static_assert(SPH_MAXTYPES <= 8, "packed list entries hold type - 1 in three bits");
 constexpr long long MP_MAXALL = 1ll << 28;
 __device__ __forceinline__ int mp_etype(int e) { return ((e >> 28) & 7) + 1; }
 

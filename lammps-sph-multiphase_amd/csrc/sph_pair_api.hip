@@ -26,7 +26,9 @@ void set_error(const char *fmt, ...) {
   va_end(ap);
 }
 
+// lanes per row of the pair layer's kernels: 8; study builds take SPH_GROUP (4, 8, 16)
 int group_lanes() {
+#ifdef SPH_STUDY
   static int g = [] {
     const char *s = getenv("SPH_GROUP");
     int v = s ? atoi(s) : 8;
@@ -34,6 +36,9 @@ int group_lanes() {
     return v;
   }();
   return g;
+#else
+  return 8;
+#endif
 }
 
 void require_device(int device) {

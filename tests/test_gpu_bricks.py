@@ -42,7 +42,7 @@ def at_rest(s):
     return s
 
 
-def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0):
+def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0, overlap=False):
     nt = s.ntypes
     P = int(np.prod(pg))
     kw = {}
@@ -64,6 +64,8 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0):
         eng.set_atoms(s.x[sel], s.v[sel], s.type[sel], s.rho[sel], s.e[sel], s.cv[sel])
         eng.set_tags(sel)
         eng.comm_local(world, r)
+        if overlap:
+            eng.tune(eng.TUNE_OVERLAP, 1)
         engines.append(eng)
     errors = []
 
@@ -241,26 +243,24 @@ def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving, path):
 
 
 @pytest.mark.parametrize("pg", [(2, 1, 1), (2, 2, 2)])
-def test_bricks_halo_overlap(gpu, sph_amd, monkeypatch, pg):
-    """SPH_OVERLAP=1 (read at engine creation): interior rows' rhosum / force passes run on a
+def test_bricks_halo_overlap(gpu, sph_amd, pg):
+    """sph_engine_tune(SPH_TUNE_OVERLAP, 1): interior rows' rhosum / force passes run on a
     second stream while the forward and rho halos are in flight, boundary rows after them.
     Same per-row arithmetic, so the same bar as the serial path: counts bit-exact, fields
     within 1e-10 of the single-process oracle over rebuilds."""
-    monkeypatch.setenv("SPH_OVERLAP", "1")
     s = at_rest(c2_system(14))
     ph = po.c2_physics()
     ph.every = 4
     ref = po.RefRun(s, ph)
     ref.setup()
     ref.run(9)
-    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=1)   # (overlap: row path)
+    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=1, overlap=True)  # (row path)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
 
 
-def test_rccl_loopback_overlap(gpu, sph_amd, monkeypatch):
+def test_rccl_loopback_overlap(gpu, sph_amd):
     """The overlapped step through real RCCL send/recv (one-rank loopback), moving particles."""
-    monkeypatch.setenv("SPH_OVERLAP", "1")
     s = c2_system(12)
     ph = po.c2_physics()
     ph.every = 4
@@ -277,6 +277,7 @@ def test_rccl_loopback_overlap(gpu, sph_amd, monkeypatch):
         eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)
         eng.comm_init(sph_amd.comm_uid(), 1, 0)
         eng.comm_loopback(True)
+        eng.tune(eng.TUNE_OVERLAP, 1)
         eng.setup()
         eng.run(9)
         out, counts, _ = collect([eng], s)

@@ -55,19 +55,22 @@ PATHS = [0, 1]   # 0 = block-staged LDS unions (production), 1 = row path (globa
 
 @pytest.mark.parametrize("sort,path,umf", [(1, 0, 0), (1, 0, 64), (0, 0, 0), (1, 1, 0),
                                            (0, 1, 0)])
-def test_setup_c2(gpu, sph_amd, monkeypatch, sort, path, umf):
+def test_setup_c2(gpu, sph_amd, sort, path, umf):
     """path 0 = block-staged passes (LDS unions, 16-bit slot rows built from the bins), 1 =
-    the row path.  umf = 64 caps the force pass's LDS image at 64 records, so nearly every
-    block runs in the large-union launch; unsorted rows (sort 0) make blocks too wide for
-    the build's candidate image, so the build takes its large-image variant."""
-    if umf:
-        monkeypatch.setenv("SPH_BLKUMF", str(umf))
+    the row path.  umf = 64 caps the force pass's LDS image at 64 records (sph_engine_tune
+    SPH_TUNE_BLKUMF), so nearly every block runs in the large-union launch; unsorted rows
+    (sort 0) make blocks too wide for the build's candidate image, so the build takes its
+    large-image variant."""
     s = c2_system(12)
     ph = po.c2_physics()
     ref = po.RefRun(s, ph)
     ref.setup()
     eng = engine_for(sph_amd, s, ph, sort=sort, kernel_path=path)
+    if umf:
+        eng.tune(eng.TUNE_BLKUMF, umf)
     eng.setup()
+    if umf:
+        assert eng.stats()["blk_nbig"] > 0
     assert eng.stats()["staged"] == (1 if path == 0 else 0)
     # neighbor membership: bit-exact counts per particle
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())

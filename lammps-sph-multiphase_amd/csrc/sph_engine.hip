@@ -170,7 +170,11 @@ struct sph_engine {
   std::vector<int> gswap_first;  // one brick: first ghost of each swap (+ nghost at the end)
   int gcap_hint = 0;              // one brick: ghost room of the next borders
   DBuf<int> gnall;                // one brick: nall before each swap (+ the overflow word)
-  DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec;
+  DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec, pc_v0, pc_v1;
+  DBuf<unsigned long long> pc_k0, pc_k1;  // the donations' (donor, candidate) sort keys
+  DBuf<int> pc_cnt;
+  bool pc_order_warned = false;
+  int64_t migrations = 0;  // atoms that left this brick at exchanges so far
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
   sph_phasechange_params pcp{};
@@ -882,6 +886,7 @@ struct sph_engine {
         hipLaunchKernelGGL(k_flag_leave, dim3(blocks(n)), dim3(BLK), 0, s, n, d, sublo[d],
                            subhi[d], xf.p, flags.p, flag2.p);
       const int nl = select_flagged(flags.p, n, sel);
+      migrations += nl;
       const int nst = select_flagged(flag2.p, n, sel2);
       cbs.reserve((size_t)(nl > 0 ? nl : 1) * sizeof(MigRec));
       if (nl)
@@ -1945,7 +1950,20 @@ struct sph_engine {
       SPH_HIP_TRY(hipStreamSynchronize(s));
     }
     // the reference meets the candidates in its atom order: tag order (one process, or one
-    // rank's owned atoms while none has migrated)
+    // rank's owned atoms while none has migrated).  LAMMPS' local order leaves tag order once
+    // CommBrick::exchange has filled a departed atom's hole with the last atom
+    // (comm_brick.cpp:600-625) or Atom::sort has run (every 1000 steps by default,
+    // atom.cpp:63): from then on the draws can meet the candidates in another order than the
+    // reference's -- same statistics, other particles.  Said once.
+    if (!pc_order_warned && (migrations > 0 || step >= 1000)) {
+      pc_order_warned = true;
+      fprintf(stderr,
+              "[sph] fix phase_change: candidates meet the random stream in tag order; the "
+              "reference's local atom order differs after %s (step %lld), so the inserted "
+              "atoms can differ from the reference's from here on\n",
+              migrations > 0 ? "an atom migrated between bricks" : "Atom::sort (sortfreq 1000)",
+              (long long)step);
+    }
     std::vector<int> ord(ncand);
     for (int k = 0; k < ncand; k++) ord[k] = k;
     std::sort(ord.begin(), ord.end(), [&](int a, int b) { return ht[a] < ht[b]; });
@@ -2018,9 +2036,11 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemcpyAsync(nrec.p, ins_rec.data(), ins_rec.size() * sizeof(double), hipMemcpyHostToDevice, s));
       // e_i = (e_i - Hwv)/2 of the atoms that changed phase, the donors' dmass
       hipLaunchKernelGGL(k_pc_set_e, dim3(blocks(nins)), dim3(BLK), 0, s, nins, idx.p, vals.p, en.p);
-      hipLaunchKernelGGL(k_pc_dmass<8>, mp_rows(nins), dim3(256), 0, s, nins, idx.p, Wd.p,
-                         (const int *)nullptr, off.p, nbr.p, xf.p, ty.p, rm.p, pd, dmass.p,
-                         lst, ccnt.p, rk);
+      // (in candidate order per donor: the reference's sum, fix_phase_change.cpp:289-299)
+      const long long cap = (long long)nins * std::max(lst > 0 ? lst : nbr_maxrow, 1);
+      pc_dmass_ordered<8>(s, nins, idx.p, Wd.p, (const int *)nullptr, off.p, nbr.p, xf.p, ty.p,
+                          rm.p, pd, lst, ccnt.p, rk, cap, pc_k0, pc_k1, pc_v0, pc_v1, pc_cnt,
+                          tmp, dmass.p);
     }
     // its reverse comm, rmass -= dmass and e renormalised, then the new atoms
     reverse1(dmass.p);

@@ -11,7 +11,9 @@
 //    :466-520) and the sub-domain test (insert_one_atom, :425-456), which must consume the
 //    stream exactly in the reference's order;
 //  * device again: the mass taken from the donors (dmass[j] += to_mass w_j / W) for the
-//    candidates that did change phase, scattered with fp64 atomics onto owned and ghost j.
+//    candidates that did change phase: one record per donation, sorted by (donor,
+//    candidate) and summed per donor in candidate order -- the reference's summation
+//    order, deterministic (k_pc_dmass_emit / k_pc_dmass_sum; pc_dmass_ordered).
 //
 // The reference's memory behaviour is reproduced: it creates the k-th new atom of a call at
 // index nlocal + k (AtomVecMesoMultiPhase::create_atom, atom_vec_meso_multiphase.cpp:968-997),
@@ -33,8 +35,11 @@
 #include <stdexcept>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "../../include/sph_hip.h"
 #include "sph_mp_kernels.h"
+#include "sph_util.h"
 
 namespace sph {
 
@@ -148,14 +153,22 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
 // dmass[j] += to_mass * w_j / W over the donors of every inserted candidate; the k-th
 // inserted candidate's donors exclude the ghosts of slot rank <= k (overwritten before its
 // donor loops), and donations to ghosts of slot rank < nins are dropped (create_atom zeroes
-// their drho later in the call)
+// their drho later in the call).  The reference sums dmass[j] over the inserted
+// candidates in candidate order (fix_phase_change.cpp:289-299; a donor appears once per
+// row).  Every donation becomes a record (key = j << 32 | k, value), the records are sorted
+// by key, and each donor's run is summed in order from zero -- the reference's own
+// summation order, so dmass is bit-identical to it and to every other run.  `key` and `val`
+// hold `cap` records (an upper bound on the donations, e.g. nins x the longest row); unused
+// keys stay ~0 and sort last.
 template <int G>
 __global__ void __launch_bounds__(256)
-k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wtot,
-           const int *__restrict__ ilist, const int *__restrict__ off,
-           const int *__restrict__ nbr, const double4 *__restrict__ xf,
-           const int *__restrict__ ty, const double *__restrict__ rm, PcDev p,
-           double *__restrict__ dmass, int lstride, const int *__restrict__ lcnt, PcRank rk) {
+k_pc_dmass_emit(int nins, const int *__restrict__ rows, const double *__restrict__ Wtot,
+                const int *__restrict__ ilist, const int *__restrict__ off,
+                const int *__restrict__ nbr, const double4 *__restrict__ xf,
+                const int *__restrict__ ty, const double *__restrict__ rm, PcDev p,
+                int lstride, const int *__restrict__ lcnt, PcRank rk,
+                unsigned long long *__restrict__ key, double *__restrict__ val,
+                int *__restrict__ cnt, long long cap) {
   const int k = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (k >= nins) return;
@@ -172,8 +185,26 @@ k_pc_dmass(int nins, const int *__restrict__ rows, const double *__restrict__ Wt
     const double4 xj = xf[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
-    atomicAdd(&dmass[j], p.to_mass * pc_w(p.dim, sqrt(rsq) * p.cutoff) / W);
+    const int slot = atomicAdd(cnt, 1);
+    if (slot >= cap) continue;  // (cap is an upper bound: never taken)
+    key[slot] = ((unsigned long long)(unsigned)j << 32) | (unsigned)k;
+    val[slot] = p.to_mass * pc_w(p.dim, sqrt(rsq) * p.cutoff) / W;
   }
+}
+// after the sort: the first record of each donor's run sums the run in candidate order
+static __global__ void k_pc_dmass_sum(long long cap, const unsigned long long *__restrict__ key,
+                                      const double *__restrict__ val,
+                                      double *__restrict__ dmass) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= cap) return;
+  const unsigned long long kq = key[q];
+  if (kq == ~0ull) return;
+  const unsigned j = (unsigned)(kq >> 32);
+  if (q > 0 && (unsigned)(key[q - 1] >> 32) == j) return;
+  double s = 0.0;
+  for (long long t = q; t < cap && key[t] != ~0ull && (unsigned)(key[t] >> 32) == j; t++)
+    s += val[t];
+  dmass[j] = s;
 }
 
 // one swap of a brick's ghosts: key = LAMMPS index of the atom each ghost was copied from
@@ -215,6 +246,40 @@ static __global__ void k_pc_keys_in(int n, const int *__restrict__ in, int *__re
   if (k >= n) return;
   key[k] = in[k];
   val[k] = k;
+}
+
+// The donors' dmass of the nins inserted candidates (rows[k], total weights Wtot[k], in
+// candidate order) into dmass (zeroed by the caller), deterministically.  cap: an upper
+// bound on the donations (nins x the longest row).  Scratch grows in the given buffers.
+template <int G>
+inline void pc_dmass_ordered(hipStream_t s, int nins, const int *rows, const double *Wtot,
+                             const int *ilist, const int *off, const int *nbr,
+                             const double4 *xf, const int *ty, const double *rm, PcDev p,
+                             int lstride, const int *lcnt, PcRank rk, long long cap,
+                             DBuf<unsigned long long> &k0, DBuf<unsigned long long> &k1,
+                             DBuf<double> &v0, DBuf<double> &v1, DBuf<int> &cnt,
+                             DBuf<unsigned char> &tmp, double *dmass) {
+  if (nins <= 0 || cap <= 0) return;
+  SPH_REQUIRE(cap < (1ll << 31), SPH_HIP_EOVERFLOW, "fix phase_change: %lld donations", cap);
+  k0.reserve(cap);
+  k1.reserve(cap);
+  v0.reserve(cap);
+  v1.reserve(cap);
+  cnt.reserve(1);
+  SPH_HIP_TRY(hipMemsetAsync(k0.p, 0xff, cap * sizeof(unsigned long long), s));
+  SPH_HIP_TRY(hipMemsetAsync(cnt.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_pc_dmass_emit<G>, dim3((unsigned)(((long long)nins * G + 255) / 256)),
+                     dim3(256), 0, s, nins, rows, Wtot, ilist, off, nbr, xf, ty, rm, p, lstride,
+                     lcnt, rk, k0.p, v0.p, cnt.p, cap);
+  size_t tb = 0;
+  SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, (int)cap,
+                                                 0, 64, s));
+  tmp.reserve(tb);
+  SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k0.p, k1.p, v0.p, v1.p, (int)cap, 0,
+                                                 64, s));
+  hipLaunchKernelGGL(k_pc_dmass_sum, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, s, cap,
+                     k1.p, v1.p, dmass);
+  SPH_HIP_TRY(hipGetLastError());
 }
 
 // ---- host side: the random stream, in the reference's order ----------------------------

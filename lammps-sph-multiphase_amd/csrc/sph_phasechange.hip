@@ -161,13 +161,21 @@ int sph_hip_phasechange(sph_hip_ctx *c, const sph_phasechange_params *p, int *se
     SPH_HIP_TRY(hipMemcpyAsync(rows.p, ins_rows.data(), nins * sizeof(int), hipMemcpyHostToDevice, c->stream));
     SPH_HIP_TRY(hipMemcpyAsync(Wd.p, ins_W.data(), nins * sizeof(double), hipMemcpyHostToDevice, c->stream));
     SPH_HIP_TRY(hipMemsetAsync(dm.p, 0, nall * sizeof(double), c->stream));
-    hipLaunchKernelGGL(k_pc_dmass<PCG>, dim3((unsigned)(((long long)nins * PCG + 255) / 256)),
-                       dim3(256), 0, c->stream, nins, rows.p, Wd.p, c->ilist.p, c->off.p,
-                       c->nbr.p, c->xf.p, c->ty.p, c->rm.p, pd, dm.p, 0, (const int *)nullptr,
-                       rk);
-    SPH_HIP_TRY(hipGetLastError());
+    long long cap = 0;  // the inserted candidates' row lengths
+    for (int q = 0; q < nins; q++) cap += c->hoff[ins_rows[q] + 1] - c->hoff[ins_rows[q]];
+    DBuf<unsigned long long> k0, k1;
+    DBuf<double> v0, v1;
+    DBuf<int> cnt;
+    pc_dmass_ordered<PCG>(c->stream, nins, rows.p, Wd.p, c->ilist.p, c->off.p, c->nbr.p,
+                          c->xf.p, c->ty.p, c->rm.p, pd, 0, (const int *)nullptr, rk, cap, k0,
+                          k1, v0, v1, cnt, tmp, dm.p);
     SPH_HIP_TRY(hipMemcpyAsync(dmass, dm.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+    k0.release();
+    k1.release();
+    v0.release();
+    v1.release();
+    cnt.release();
   }
   // the staged e follows the update (a later pair pass sees the new energies)
   SPH_HIP_TRY(hipMemcpyAsync(c->en.p, he.data(), nlocal * sizeof(double), hipMemcpyHostToDevice, c->stream));

@@ -65,12 +65,15 @@ __device__ __forceinline__ int blk_scan(int v, int *s_w, int *total) {
   return base + x - v;
 }
 
-// Slot rows are plain arrays: lane l of the row's G lanes takes entries U*l .. U*l + U-1 of
-// each U*G-entry chunk (one load), so a row written in entry order is written contiguously
-// (k_blk_build's coalesced stores).  (Kept as a function for the older writers.)
+// Slot rows are stored chunk-transposed: a chunk holds U*G consecutive entries (ascending
+// slots) of a row; lane l of the row's G lanes holds entries l, l+G, .., l+(U-1)G of it in
+// ONE word (U 16-bit slots: an 8-byte load for U = 4) at storage position U*l.  So the G
+// lanes of a walk step q take G consecutive entries (consecutive LDS records, and a row
+// that ends inside a chunk stops after ceil(rest/G) steps: granularity G, not U*G), and each
+// lane still reads its slots of a chunk with one load.  Logical entry e -> storage position:
 template <int G, int U>
-__host__ __device__ __forceinline__ int blk_tpos(int q) {
-  return q;
+__host__ __device__ __forceinline__ int blk_tpos(int e) {
+  return (e / (U * G)) * (U * G) + (e % G) * U + (e % (U * G)) / G;
 }
 
 // v_writelane_b32 through its LLVM intrinsic (no clang builtin here; the compiler then
@@ -702,12 +705,12 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   __syncthreads();
   if (BEXP == 3) return;
   // 5) the slot rows, full and inner: wave w writes rows w*RPW .. w*RPW + RPW-1 with LPR
-  // lanes per row; lane `part` of a row writes the row's entries [part*Q, part*Q + Q) (Q a
-  // multiple of 4: every store one aligned 8-byte word of 4 slots, no word shared by two
-  // lanes), walking the row's set bits from the chunk holding its first entry (ascending
-  // slots).  The lane holding the row's last entry also writes the sentinel up to a whole
-  // chunk.
+  // lanes per row; lane `part` of a row writes the row's chunks part, part + LPR, .. (U*G
+  // entries each, transposed as blk_tpos: entry q*G + l of the chunk into lane word l at
+  // bit 16q), walking the row's set bits from the chunk's first entry (ascending slots), and
+  // stores each chunk whole (the tail chunk zero-padded: the sentinel slot).
   constexpr int LPR = 64 / RPW;
+  static_assert(U * 16 <= 64, "a lane word of U 16-bit slots in 64 bits");
   const int r = wv * RPW + lane / LPR, part = lane % LPR;
   const bool live = r < nrow;
   auto word = [&](int c, int sel) -> unsigned long long {
@@ -718,44 +721,43 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     int cnt = 0;
     if (live)
       for (int c = 0; c < nch; c++) cnt += __popcll(word(c, sel));
-    const int Q = ((cnt + LPR - 1) / LPR + 3) & ~3;
-    const int k0 = min(part * Q, cnt), k1 = min(k0 + Q, cnt);
-    int c = 0;
-    unsigned long long w = 0ull;
-    if (k0 < k1) {  // the chunk holding entry k0, and its bits from that entry on
-      int acc = 0;
-      for (;;) {
-        w = word(c, sel);
-        const int pc = __popcll(w);
-        if (acc + pc > k0) break;
-        acc += pc;
-        c++;
+    const int nchunk = min((cnt + UG - 1) / UG, sstride / UG);
+    unsigned short *const out = rows + (size_t)(row0 + r) * sstride;
+    int c = 0, acc = 0;  // word c holds the entries from acc on
+    unsigned long long w = (live && nch > 0) ? word(0, sel) : 0ull;
+    for (int ch = part; ch < nchunk; ch += LPR) {
+      const int e0 = ch * UG;
+      while (acc + __popcll(w) <= e0) {  // (e0 < cnt: the word holding it exists)
+        acc += __popcll(w);
+        w = word(++c, sel);
       }
-      for (int j = k0 - acc; j > 0; j--) w &= w - 1ull;
-    }
-    unsigned long long *const out =
-        reinterpret_cast<unsigned long long *>(rows + (size_t)(row0 + r) * sstride);
-    unsigned long long buf = 0ull;
-    int pos = k0;
-    while (pos < k1) {
-      while (w == 0ull) w = word(++c, sel);
-      const int bit = __ffsll((long long)w) - 1;
-      w &= w - 1ull;
-      buf |= (unsigned long long)s_q[c][bit] << (16 * (pos & 3));
-      if ((pos & 3) == 3) {
-        if (pos < sstride) out[pos >> 2] = buf;
-        buf = 0ull;
+      unsigned long long m = w;
+      for (int j = e0 - acc; j > 0; j--) m &= m - 1ull;
+      int cc = c;
+      const int ne = min(cnt - e0, UG);
+      unsigned long long buf[G];
+#pragma unroll
+      for (int l = 0; l < G; l++) buf[l] = 0ull;
+#pragma unroll
+      for (int q = 0; q < U; q++)
+#pragma unroll
+        for (int l = 0; l < G; l++)
+          if (q * G + l < ne) {
+            while (m == 0ull) m = word(++cc, sel);
+            const int bit = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            buf[l] |= (unsigned long long)s_q[cc][bit] << (16 * q);
+          }
+      if (U == 4) {
+        ulonglong2 *const o = reinterpret_cast<ulonglong2 *>(out + e0);
+#pragma unroll
+        for (int t = 0; t < G / 2; t++) o[t] = make_ulonglong2(buf[2 * t], buf[2 * t + 1]);
+      } else {
+#pragma unroll
+        for (int l = 0; l < G; l++)
+#pragma unroll
+          for (int q = 0; q < U; q++) out[e0 + l * U + q] = (unsigned short)(buf[l] >> (16 * q));
       }
-      pos++;
-    }
-    if (k0 < k1 && k1 == cnt) {  // the row's last word (zero-padded) and the sentinel
-      const int e = min((cnt + UG - 1) / UG * UG, sstride);
-      int q = pos >> 2;
-      if (pos & 3) {
-        if (4 * q < e) out[q] = buf;
-        q++;
-      }
-      for (; 4 * q < e; q++) out[q] = 0ull;
     }
     if (live && part == 0) {
       cnt_out[row0 + r] = cnt;
@@ -783,12 +785,14 @@ struct SlotWord<4> {
   }
 };
 
-// A row's c slots for the row's G lanes, U consecutive slots per lane per chunk.  load() issues the lane's slot-word loads -- before the block's staging, so their
-// latency overlaps it; walk() calls body(slot, in) for every slot position of the lane
-// (in = position < c; padded positions hold the sentinel slot).  NCH > 0: all of the
-// row's chunks (at most NCH, the host guarantees c <= NCH*U*G) are held in registers;
-// NCH = 0 (long rows): the next chunk is prefetched while the current one is evaluated
-// (the slot array is padded by two chunks).
+// A row's c slots for the row's G lanes, chunk-transposed (blk_tpos): walk step (k, q) gives
+// lane l the row's entry k*U*G + q*G + l.  load() issues the lane's slot-word loads -- before
+// the block's staging, so their latency overlaps it; walk() calls body(slot, in) for the
+// lane's slot positions (in = entry < c; padded positions hold the sentinel slot 0) and skips
+// a step once every row of the wave has passed its count (steps of G entries, not U*G).
+// NCH > 0: all of the row's chunks (at most NCH, the host guarantees c <= NCH*U*G) are held
+// in registers; NCH = 0 (long rows): the next chunk is prefetched while the current one is
+// evaluated (the slot array is padded by two chunks).
 template <int G, int U, int NCH>
 struct BlkSlots {
   typedef typename SlotWord<U>::T SW;
@@ -812,7 +816,7 @@ struct BlkSlots {
         if (k * U * G >= c) break;
 #pragma unroll
         for (int q = 0; q < U; q++)
-          body(SlotWord<U>::get(w[k], q), k * U * G + U * lane + q < c);
+          if (k * U * G + q * G < c) body(SlotWord<U>::get(w[k], q), k * U * G + q * G + lane < c);
       }
     } else {
       SW wn = w[0];
@@ -820,13 +824,14 @@ struct BlkSlots {
         const SW cur = wn;
         wn = *reinterpret_cast<const SW *>(sl + k0 + U * G + U * lane);
 #pragma unroll
-        for (int q = 0; q < U; q++) body(SlotWord<U>::get(cur, q), k0 + U * lane + q < c);
+        for (int q = 0; q < U; q++)
+          if (k0 + q * G < c) body(SlotWord<U>::get(cur, q), k0 + q * G + lane < c);
       }
     }
   }
 };
 // walk2: the same slots, but each record is read by load(slot) and used by body(record); with
-// SPH_BLK_PIPE a lane's U records of a chunk are all read before the first is used (U
+// SPH_BLK_PIPE a lane's records of a chunk are all read before the first is used (U
 // independent pair evaluations in flight, the LDS latency covered by the next pairs' reads)
 #ifndef SPH_BLK_PIPE
 #define SPH_BLK_PIPE 1
@@ -840,9 +845,11 @@ __device__ __forceinline__ void blk_walk2(BlkSlots<G, U, NCH> &sw, int c, int la
       if (k * U * G >= c) break;
       decltype(load(0)) r[U];
 #pragma unroll
-      for (int q = 0; q < U; q++) r[q] = load(SlotWord<U>::get(sw.w[k], q));
+      for (int q = 0; q < U; q++)
+        if (k * U * G + q * G < c) r[q] = load(SlotWord<U>::get(sw.w[k], q));
 #pragma unroll
-      for (int q = 0; q < U; q++) body(r[q]);
+      for (int q = 0; q < U; q++)
+        if (k * U * G + q * G < c) body(r[q]);
     }
   } else {
     sw.walk(c, lane, [&](int q, bool) { body(load(q)); });
@@ -1251,17 +1258,13 @@ static __global__ void k_blk_large_dev(int nb, const int *__restrict__ ucnt, int
 #define SPH_BLK_SHAPES(X) X(0, 64, 8, 4) X(1, 32, 8, 4)
 #endif
 constexpr int BLK_NCH = 8;  // slot chunks preloaded per row (rows up to BLK_NCH*U*G entries)
-// The pair passes walk a row in chunks of BLK_WALK_U * G entries (the build pads rows to
-// U * G): with 16-entry chunks a row of c entries costs ceil(c/16)*16 pair evaluations
-// instead of ceil(c/32)*32 -- measured slower (16-entry walk: force 0.457 vs 0.287 ms at
-// C2, profiles/r03/README.md), so the walk stays at the build's U
-#ifndef SPH_BLK_WALK_U
-#define SPH_BLK_WALK_U 4
-#endif
+// The pair passes walk a row's chunks of U * G entries in steps of G (the transposed layout,
+// blk_tpos, ties the walk's U to the build's; round 3's 16-entry chunks with U = 2 were
+// slower, profiles/r03/README.md)
 template <int U>
 struct BlkWalk {
-  static constexpr int UW = (U > SPH_BLK_WALK_U) ? SPH_BLK_WALK_U : U;
-  static constexpr int NCH = BLK_NCH * U / UW;
+  static constexpr int UW = U;
+  static constexpr int NCH = BLK_NCH;
 };
 struct BlkShape {
   int R, G, U;

@@ -103,22 +103,3 @@ def test_engine_c5_no_phase_change_every2(gpu, sph_amd):
     eng.run(5)
     _compare(eng, ref)
 
-
-@pytest.mark.gpu
-def test_phase_change_dmass_deterministic(gpu, sph_amd):
-    """The donors' dmass is summed per donor in candidate order (the reference's order,
-    fix_phase_change.cpp:289-299) after a sort, not with fp64 atomics: two runs of the same
-    C5 system give bit-identical rmass and e, with atoms inserted."""
-    from c5_util import mp_engine, mp_state
-    out = []
-    for _ in range(2):
-        s = bubble_system(10, slab=True)
-        ph = bubble_physics(10, prob=0.5, Tt=-1.0)
-        eng = mp_engine(sph_amd, s, ph)
-        eng.setup()
-        eng.run(4)
-        out.append(mp_state(eng))
-        eng.close()
-    assert out[0]["ninserted"] >= 5
-    for k in ("rmass", "e", "x", "rho", "f"):
-        assert np.array_equal(out[0][k], out[1][k]), k

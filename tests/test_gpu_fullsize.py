@@ -23,22 +23,29 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-10
 
 
-def _check_block_paths(eng):
+def _check_block_paths(eng, large):
     st = eng.stats()
     assert st["staged"] == 1, "the block path (production) did not run"
-    assert st["blk_nbig"] > 0, "no block took the large-union launch at full size"
+    if large:
+        assert st["blk_nbig"] > 0, "no block took the large-union launch"
     assert st["inner_rows"] == 1 and st["inner_live"] == 1, \
         "the pair passes are not walking the inner rows after the rebuild"
     return st
 
 
-@pytest.mark.parametrize("system,physics", [("c2", po.c2_physics), ("c3", po.c3_physics)])
-def test_full_size_fields(gpu, sph_amd, system, physics):
-    """Setup plus 11 steps: the step-10 rebuild and one step on its inner rows."""
+@pytest.mark.parametrize("system,physics,umf", [("c2", po.c2_physics, 0),
+                                                ("c3", po.c3_physics, 640)])
+def test_full_size_fields(gpu, sph_amd, system, physics, umf):
+    """Setup plus 11 steps: the step-10 rebuild and one step on its inner rows.  At 1M the
+    Hilbert-sorted blocks' unions all fit the force pass's default LDS image (no second
+    launch); the C3 run caps the image at 640 records (sph_engine_tune SPH_TUNE_BLKUMF) so
+    that the blocks above it take the large-union launch at full size."""
     s = (c2_system if system == "c2" else c3_system)(100)
     ph = physics()
     ph.every = 10
     eng = engine_for(sph_amd, s, ph)
+    if umf:
+        eng.tune(eng.TUNE_BLKUMF, umf)
     eng.setup()
     ref = po.RefRun(s, ph)
     ref.setup()
@@ -49,7 +56,7 @@ def test_full_size_fields(gpu, sph_amd, system, physics):
     ref.run(11)
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     compare(eng, ref, path=0)
-    st = _check_block_paths(eng)
+    st = _check_block_paths(eng, large=umf > 0)
     assert st["step"] == 11 and st["nlocal"] == 100 ** 3
 
 

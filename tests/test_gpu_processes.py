@@ -100,10 +100,11 @@ def test_processes_c2_rebuilds_migration(gpu, tmp_path, mode, pg):
         got = merge(snaps, k, s.n)
         assert sum(got["nlocal"]) == s.n
         assert np.array_equal(got["counts"], ref.numneigh_full()), k
-        for f, want in (("rho", s.rho), ("f", ref.f), ("drho", ref.drho), ("de", ref.de),
-                        ("x", s.x), ("v", s.v)):
+        rs = ref.s
+        for f, want in (("rho", rs.rho), ("f", ref.f), ("drho", ref.drho), ("de", ref.de),
+                        ("x", rs.x), ("v", rs.v)):
             assert rel_err(got[f], want) < TOL, (k, f)
-    assert ((s.x[:, 0] < 6.0) != side0).any(), "no atom migrated: migration not exercised"
+    assert ((ref.s.x[:, 0] < 6.0) != side0).any(), "no atom migrated: migration not exercised"
     assert all(int(sn["staged"]) == 1 for sn in snaps)   # the block path ran on every rank
     assert all(int(sn["nghost"]) > 0 for sn in snaps)
 

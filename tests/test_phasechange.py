@@ -221,3 +221,18 @@ def test_gpu_phase_change_vs_reference_fixture(gpu, sph_amd, name):
     assert np.array_equal(rg[:, 10], d["c0_out_rmass"][n:])
     assert rel_err(rm, d["c0_out_rmass"][:n]) < 1e-12
     assert rel_err(e, d["c0_out_e"][:n]) < 1e-12
+
+
+@pytest.mark.gpu
+def test_gpu_phase_change_dmass_deterministic(gpu, sph_amd):
+    """The donors' dmass is summed per donor in candidate order (the reference's order,
+    fix_phase_change.cpp:289-299) after a sort of the donations, not with fp64 atomics: two
+    calls on the same staged atoms and list give bit-identical rmass and e."""
+    d, p = two_phase_box()
+    g = d["g"]
+    arrays = dict(x=g.x, v=d["v"], vest=d["vest"], cg=d["cg"], e=d["e"], rmass=d["rmass"],
+                  rho=d["rho"], cv=d["cv"], type=g.type)
+    a = _pair_layer_call(sph_amd, p, 4242, g, arrays, d["foff"], d["fnb"])
+    b = _pair_layer_call(sph_amd, p, 4242, g, arrays, d["foff"], d["fnb"])
+    assert a[1] > 0
+    assert np.array_equal(a[4], b[4]) and np.array_equal(a[5], b[5])

@@ -98,6 +98,14 @@ __device__ __forceinline__ unsigned writelane(unsigned v, unsigned val) {
 // LDS cycle).  The rho pass keeps a compact image of its own (x, y at 16 s; z at 16 S + 8 s
 // for S slots) and decodes s from q.
 constexpr int BLK_CH = 1024, BLK_CHE = 1280;
+// Newton-3 inside the blocks (k_blk_build N3 + the passes' LDS share accumulators): measured
+// slower on gfx950 (force 0.291 -> 0.313 ms, build 1.60 -> 2.18 ms at C2 1M),
+// so only study builds carry it (SPH_N3=1)
+#ifdef SPH_STUDY
+constexpr bool BLK_N3_BUILT = true;
+#else
+constexpr bool BLK_N3_BUILT = false;
+#endif
 __host__ __device__ inline int blk_q(int s, int cq) { return (s >> 4) * cq + (s & 15); }
 template <int CQ>
 __device__ __forceinline__ int blk_s(int q) { return (q / CQ) * 16 + (q % CQ); }
@@ -446,7 +454,13 @@ __device__ __forceinline__ unsigned long long blk_uniform64(unsigned long long x
 // BEXP (study builds, SPH_BEXP with the build v2): 1 = return after the bin table, 2 = after
 // the candidates, 3 = no emit (rows not written), 4 = no tests (every word 0).  Outputs
 // meaningless.
-template <int R, int G, int U, bool NT1, bool INNER, int BEXP = 0>
+// N3 (Newton's third law inside the block): the union puts the block's own rows first
+// (slot r + 1 = row r, whether or not a list names it), and a row keeps a neighbour that is
+// another row of the block only if that row comes after it -- each such pair is evaluated
+// once, by its earlier row, which also accumulates the later row's share (the pair passes'
+// LDS accumulators).  rcnt/icnt then hold the rows' stored (N3) counts and fcnt the full
+// counts (Neighbor::full_bin's, for the neighbour statistics).
+template <int R, int G, int U, bool NT1, bool INNER, bool N3, int BEXP = 0>
 __global__ void __launch_bounds__(256)
 k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             const int *__restrict__ ty, const double4 *__restrict__ xb,
@@ -454,7 +468,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             const Coefs *__restrict__ cf, int ucap, int sstride, int *__restrict__ ulist,
             int *__restrict__ ucnt, int *__restrict__ rcnt, unsigned short *__restrict__ snbr,
             int *__restrict__ icnt, unsigned short *__restrict__ snbi,
-            int *__restrict__ ovf, int *__restrict__ umax, int cq) {
+            int *__restrict__ ovf, int *__restrict__ umax, int cq, int *__restrict__ fcnt) {
   constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
   constexpr int RPW = R / NW, UG = U * G, WS = INNER ? 2 : 1;
   static_assert(R <= 64 && R % 32 == 0, "one lane per row, rows in steps of 8 per wave");
@@ -473,6 +487,8 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   __shared__ double4 s_row[R];
   __shared__ int s_rty[R];
   __shared__ int s_self[NW][64];
+  __shared__ unsigned long long s_rowm[N3 ? SCH : 1];  // N3: kept candidates that are rows
+  __shared__ int s_fc[N3 ? R : 1];                      // N3: the rows' full counts
   __shared__ double s_bb[6];
   __shared__ double s_cns[NT1 ? 1 : NT2], s_cin[(NT1 || !INNER) ? 1 : NT2];
   __shared__ int s_sc[NW];
@@ -486,6 +502,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
       s_cns[t] = cf->cutneighsq[t];
       if (INNER) s_cin[t] = cf->cutinsq[t];
     }
+  if (N3 && tid < R) s_fc[tid] = 0;
   // 1) the rows (far away past the last row: never a hit) and their bounding box (wave 0)
   if (wv == 0) {
     double lo[3], hi[3];
@@ -625,6 +642,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   };
   double4 xn;
   int tn = 1;
+  int fc = 0;  // N3: lane r's share of row r's full count
   if (wv < nch) cload(wv, xn, tn);
   for (int c = wv; c < nch; c += NW) {
     const int p = c * 64 + lane;
@@ -664,8 +682,21 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     });
     // (rows past the last one sit at 1e300: their words are 0 already)
     const int self = s_self[wv][lane];
-    const unsigned long long keep = ~((unsigned long long)(self >= 0) << (self & 63));
-    const unsigned long long mine = (((unsigned long long)my_hi << 32) | my_lo) & keep;
+    const unsigned long long sbit = (unsigned long long)(self >= 0) << (self & 63);
+    unsigned long long keep = ~sbit;
+    if (N3) {  // lane r also drops the rows before it: prefix OR of the rows' own bits
+      unsigned long long lo = sbit;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned a = (unsigned)__shfl_up((int)(unsigned)lo, d, 64);
+        const unsigned h = (unsigned)__shfl_up((int)(unsigned)(lo >> 32), d, 64);
+        if (lane >= d) lo |= ((unsigned long long)h << 32) | a;
+      }
+      keep = ~lo;
+    }
+    const unsigned long long full = (((unsigned long long)my_hi << 32) | my_lo) & ~sbit;
+    const unsigned long long mine = full & keep;
+    if (N3 && lane < R) fc += __popcll(full);
     if (lane < R) {
       if (INNER)
         reinterpret_cast<ulonglong2 *>(s_w)[c * R + lane] =
@@ -676,24 +707,37 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     unsigned long long u = mine;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) u |= __shfl_xor(u, d, 64);
+    if (N3) {  // the rows have fixed slots: the union proper is the other used candidates
+      const unsigned long long rm = __ballot(cid >= row0 && cid < row0 + nrow);
+      u &= ~rm;
+      if (lane == 0) s_rowm[c] = rm;
+    }
     if (lane == 0) s_used[c] = u;
   }
+  if (N3 && lane < R) atomicAdd(&s_fc[lane], fc);
   __syncthreads();
-  // 4) the union: used candidates in candidate order (slot = rank + 1)
+  // 4) the union: used candidates in candidate order (slot = rank + 1); N3: the block's rows
+  // first (slot r + 1), then the other used candidates
   int u = 0;
   {
     const int v = tid < nch ? __popcll(s_used[tid]) : 0;
     const int ex = blk_scan<NT>(v, s_sc, &u);
     if (tid < nch) s_upre[tid] = ex;
   }
+  const int ubase = N3 ? nrow : 0;
+  u += ubase;
+  if (N3 && tid < nrow) ulist[(size_t)b * ucap + tid] = row0 + tid;
   __syncthreads();
   // the union list, and each chunk's slot words: candidate l of chunk c, if used, has slot
-  // s_upre[c] + 1 + (used candidates below it)
+  // ubase + s_upre[c] + 1 + (used candidates below it); a row (N3) has slot r + 1
   for (int c = wv; c < nch; c += NW) {
     const unsigned long long used = s_used[c];
     const int below = blk_mbcnt(used);
-    s_q[c][lane] = (unsigned short)blk_q(s_upre[c] + 1 + below, cq);
-    if ((used >> lane) & 1ull) ulist[(size_t)b * ucap + s_upre[c] + below] = s_cpos[c * 64 + lane];
+    int sl = ubase + s_upre[c] + 1 + below;
+    if (N3 && ((s_rowm[c] >> lane) & 1ull)) sl = s_cpos[c * 64 + lane] - row0 + 1;
+    s_q[c][lane] = (unsigned short)blk_q(sl, cq);
+    if ((used >> lane) & 1ull)
+      ulist[(size_t)b * ucap + ubase + s_upre[c] + below] = s_cpos[c * 64 + lane];
   }
   if (tid == 0) {
     ucnt[b] = u;
@@ -713,18 +757,31 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   static_assert(U * 16 <= 64, "a lane word of U 16-bit slots in 64 bits");
   const int r = wv * RPW + lane / LPR, part = lane % LPR;
   const bool live = r < nrow;
-  auto word = [&](int c, int sel) -> unsigned long long {
+  auto word0 = [&](int c, int sel) -> unsigned long long {
     return INNER ? s_w[(c * R + r) * 2 + sel] : s_w[c * R + r];
+  };
+  // N3: a row's entries that are rows of the block come first (virtual words 0 .. nch-1),
+  // then the others (nch .. 2 nch-1), each part in candidate order -- the pair passes meet a
+  // row's Newton-3 pairs in its first walk steps only
+  const int nv = N3 ? 2 * nch : nch;
+  auto word = [&](int v, int sel) -> unsigned long long {
+    if (!N3) return word0(v, sel);
+    const int c = v < nch ? v : v - nch;
+    const unsigned long long m = s_rowm[c];
+    return word0(c, sel) & (v < nch ? m : ~m);
+  };
+  auto qof = [&](int v, int bit) -> unsigned short {
+    return s_q[(N3 && v >= nch) ? v - nch : v][bit];
   };
   bool over = false;
   auto emit = [&](int sel, unsigned short *__restrict__ rows, int *__restrict__ cnt_out) {
     int cnt = 0;
     if (live)
-      for (int c = 0; c < nch; c++) cnt += __popcll(word(c, sel));
+      for (int c = 0; c < nch; c++) cnt += __popcll(word0(c, sel));
     const int nchunk = min((cnt + UG - 1) / UG, sstride / UG);
     unsigned short *const out = rows + (size_t)(row0 + r) * sstride;
-    int c = 0, acc = 0;  // word c holds the entries from acc on
-    unsigned long long w = (live && nch > 0) ? word(0, sel) : 0ull;
+    int c = 0, acc = 0;  // (virtual) word c holds the entries from acc on
+    unsigned long long w = (live && nv > 0) ? word(0, sel) : 0ull;
     for (int ch = part; ch < nchunk; ch += LPR) {
       const int e0 = ch * UG;
       while (acc + __popcll(w) <= e0) {  // (e0 < cnt: the word holding it exists)
@@ -746,7 +803,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             while (m == 0ull) m = word(++cc, sel);
             const int bit = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            buf[l] |= (unsigned long long)s_q[cc][bit] << (16 * q);
+            buf[l] |= (unsigned long long)qof(cc, bit) << (16 * q);
           }
       if (U == 4) {
         ulonglong2 *const o = reinterpret_cast<ulonglong2 *>(out + e0);
@@ -764,6 +821,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
       over |= cnt > sstride;
     }
   };
+  if (N3 && live && part == 0) fcnt[row0 + r] = s_fc[r];
   emit(0, snbr, rcnt);
   if (INNER) emit(1, snbi, icnt);
   if (over) atomicMax(ovf, 1 << 21);
@@ -877,7 +935,7 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
              const int *__restrict__ rcnt, double4 *__restrict__ xf,
              const int *__restrict__ ty, double4 *__restrict__ vr,
              const Coefs *__restrict__ cf, int um, const unsigned short *__restrict__ snbi,
-             const int *__restrict__ icnt, const int *__restrict__ moved) {
+             const int *__restrict__ icnt, const int *__restrict__ moved, int n3) {
   constexpr int NTH = R * G;
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
@@ -885,11 +943,17 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   }
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
+  __shared__ double s_acc[R];  // n3: the later rows' shares (k_blk_build N3)
   const int nt1 = cf->ntypes + 1;
   const int b = (int)xcd_block(), tid = threadIdx.x;
   const int row = b * R + tid / G, lane = tid & (G - 1);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
+  // n3: slots 1 .. nrow are the block's rows (q <= qn3); a row's entries among them are the
+  // later rows, whose share (m_i W_ij) goes to their accumulator
+  const bool n3on = BLK_N3_BUILT && n3;
+  const int qn3 = n3on ? blk_q(min(R, n - b * R), CQ) : -1;
+  if (n3on && tid < R) s_acc[tid] = 0.0;
   // loads first: the row's count, the union's atom ids, then the row's slots and the
   // union's positions, so that one latency covers them all
   const int u = ucnt[b];
@@ -948,8 +1012,14 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
     wf = wf * wf;
     wf = wf * wf;
     acc = NT1 ? acc + wf : fma(cc.mK, wf, acc);
+    if (q > 0 && q <= qn3)  // a later row of this block: its share (cut and weight symmetric)
+      atomicAdd(&s_acc[sj - 1], NT1 ? wf : s_c[s_t[sj] * nt1 + it].mK * wf);
   });
   acc = group_sum<G>(acc);
+  if (n3on) {  // (workgroup-uniform) the earlier rows' shares of this row
+    __syncthreads();
+    acc += s_acc[tid / G];
+  }
   if (lane == 0 && live) {
     const double rho = ((cf->rho_keep >> it) & 1) ? vr[row].w
                                                    : cf->self_rho[it] + (NT1 ? c1.mK * acc : acc);
@@ -1061,7 +1131,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
             double gz, int um, const int *__restrict__ blist, int cq,
             const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,
-            const int *__restrict__ moved) {
+            const int *__restrict__ moved, int n3) {
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
     rcnt = icnt;
@@ -1069,14 +1139,24 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr int NTH = R * G;
+  constexpr int CQ = (HEAT ? BLK_CHE : BLK_CH) / 16;  // (= cq)
+  constexpr int NA = HEAT ? 6 : 5;  // a row's shares: F (3), D, E [, EH]
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ TaitPair s_tp[(TAIT && !NT1) ? NT2 : 1];
   __shared__ HeatPair s_hp[(HEAT && !NT1) ? NT2 : 1];
+  __shared__ double s_acc[R * NA];  // n3: the later rows' shares (k_blk_build N3)
   const int nt1 = cf->ntypes + 1;
   const int b = blist ? blist[blockIdx.x] : (int)xcd_block();
   const int tid = threadIdx.x;
   const int u = EXP == 3 ? 0 : ucnt[b];
   if (!blist && u > um) return;  // (workgroup-uniform) left to the large-union launch
+  // n3: slots 1 .. nrow are the block's rows (q <= qn3); a row's entries among them are the
+  // later rows, whose shares go to their accumulators (Newton's third law: F and the heat
+  // term change sign, D and E do not)
+  const bool n3on = BLK_N3_BUILT && n3;
+  const int qn3 = n3on ? blk_q(min(R, n - b * R), CQ) : -1;
+  if (n3on)
+    for (int t = tid; t < R * NA; t += NTH) s_acc[t] = 0.0;
   const int row = b * R + tid / G, lane = tid & (G - 1);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
@@ -1170,6 +1250,8 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     const double rsq = dx * dx + dy * dy + dz * dz;
     const int pidx = NT1 ? 3 : it * nt1 + s_t[q];
     const double r = sqrt1(rsq);
+    // this pair's terms (i side); a later row of the block takes its share too (n3)
+    double tfx = 0.0, tfy = 0.0, tfz = 0.0, tD = 0.0, tDj = 0.0, tE = 0.0, tEH = 0.0;
     if (TAIT) {
       const TaitPair cc = NT1 ? t1 : s_tp[pidx];
       const double d = fmax(cc.h - r, 0.0);
@@ -1181,20 +1263,26 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
         const double fv =
             (cc.viscC * fmin(dvdr, 0.0)) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
         const double sp = NT1 ? (xi.w + a1.y + fv) * w : cc.mm * ((xi.w + a1.y + fv) * w);
-        fx += dx * sp;
-        fy += dy * sp;
-        fz += dz * sp;
-        E += sp * dvdr;
+        tfx = dx * sp;
+        tfy = dy * sp;
+        tfz = dz * sp;
+        tE = sp * dvdr;
       } else {
         const double sp = NT1 ? (xi.w + a1.y) * w : cc.mm * ((xi.w + a1.y) * w);
         const double cv = cc.viscC * rcp1(vi.w * a3.y);
         const double sv = NT1 ? cv * w : cc.mm * (cv * w);
-        fx += dx * sp - velx * sv;
-        fy += dy * sp - vely * sv;
-        fz += dz * sp - velz * sv;
-        E += sp * dvdr - sv * (velx * velx + vely * vely + velz * velz);
+        tfx = dx * sp - velx * sv;
+        tfy = dy * sp - vely * sv;
+        tfz = dz * sp - velz * sv;
+        tE = sp * dvdr - sv * (velx * velx + vely * vely + velz * velz);
       }
-      D += NT1 ? dvdr * w : cc.mj * (dvdr * w);
+      tD = NT1 ? dvdr * w : cc.mj * (dvdr * w);
+      tDj = NT1 ? tD : cc.mi * (dvdr * w);  // (the share of row j: m_i instead of m_j)
+      fx += tfx;
+      fy += tfy;
+      fz += tfz;
+      E += tE;
+      D += tD;
     }
     if (HEAT) {
       const HeatPair cc = NT1 ? h1 : s_hp[pidx];
@@ -1202,7 +1290,19 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       const double w = NT1 ? d * d : cc.wK * (d * d);
       const double ej = rc.e;
       const double t = ((vi.w + a3.y) * rcp1(vi.w * a3.y)) * ((ei - ej) * w);
-      EH += NT1 ? t : cc.hmD * t;
+      tEH = NT1 ? t : cc.hmD * t;
+      EH += tEH;
+    }
+    if (q > 0 && q <= qn3) {
+      double *const a = s_acc + (blk_s<CQ>(q) - 1) * NA;
+      if (TAIT) {
+        atomicAdd(a + 0, -tfx);
+        atomicAdd(a + 1, -tfy);
+        atomicAdd(a + 2, -tfz);
+        atomicAdd(a + 3, tDj);
+        atomicAdd(a + 4, tE);
+      }
+      if (HEAT) atomicAdd(a + 5, -tEH);
     }
   });
   if (TAIT) {
@@ -1213,6 +1313,18 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     E = group_sum<G>(E);
   }
   if (HEAT) EH = group_sum<G>(EH);
+  if (n3on) {  // (workgroup-uniform) the earlier rows' shares of this row
+    __syncthreads();
+    const double *const a = s_acc + (tid / G) * NA;
+    if (TAIT) {
+      fx += a[0];
+      fy += a[1];
+      fz += a[2];
+      D += a[3];
+      E += a[4];
+    }
+    if (HEAT) EH += a[5];
+  }
   if (lane == 0 && live) {
     double dE = 0.0;
     if (TAIT) {
@@ -1294,6 +1406,7 @@ struct BlkArgs {
   // inner rows (k_blk_inner) and the device flag that retires them; snbi == nullptr: none
   const unsigned short *snbi = nullptr;
   const int *icnt = nullptr, *moved = nullptr;
+  bool n3 = false;      // rows built with Newton-3 inside the blocks (k_blk_build N3)
   bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
 };
 
@@ -1336,49 +1449,78 @@ inline void blk_neigh(int shape, bool big, bool nt1, hipStream_t s, int n, const
 }
 
 // k_blk_build (the default block build; k_blk_neigh remains the large-image fallback)
-template <int R, int G, int U, bool NT1, bool INNER>
+template <int R, int G, int U, bool NT1, bool INNER, bool N3>
 inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const double4 *xf,
                         const int *ty, const double4 *xb, const int *tb, const int *qbeg,
                         const Coefs *cf, int ucap, int sstride, int *ulist, int *ucnt,
                         int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
-                        int *ovf, int *umax, int cq, int bexp) {
+                        int *ovf, int *umax, int cq, int bexp, int *fcnt) {
 #ifdef SPH_STUDY
-  auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, 1>
-          : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, 2>
-          : bexp == 3 ? k_blk_build<R, G, U, NT1, INNER, 3>
-          : bexp == 4 ? k_blk_build<R, G, U, NT1, INNER, 4>
-                      : k_blk_build<R, G, U, NT1, INNER, 0>;
+  auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, N3, 1>
+          : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, N3, 2>
+          : bexp == 3 ? k_blk_build<R, G, U, NT1, INNER, N3, 3>
+          : bexp == 4 ? k_blk_build<R, G, U, NT1, INNER, N3, 4>
+                      : k_blk_build<R, G, U, NT1, INNER, N3, 0>;
 #else
   (void)bexp;
-  auto fn = k_blk_build<R, G, U, NT1, INNER, 0>;
+  auto fn = k_blk_build<R, G, U, NT1, INNER, N3, 0>;
 #endif
   hipLaunchKernelGGL(fn, dim3(blk_blocks(n, R)), dim3(256), 0, s, n, q, dim, xf, ty, xb, tb,
-                     qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq);
+                     qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
+                     fcnt);
 }
-inline void blk_build(int shape, bool nt1, bool inner, hipStream_t s, int n, const QBins &q,
-                      int dim, const double4 *xf, const int *ty, const double4 *xb,
-                      const int *tb, const int *qbeg, const Coefs *cf, int ucap, int sstride,
-                      int *ulist, int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
-                      unsigned short *snbi, int *ovf, int *umax, int cq, int bexp) {
+template <int R, int G, int U, bool N3>
+inline void blk_build_n(bool nt1, bool inner, hipStream_t s, int n, const QBins &q, int dim,
+                        const double4 *xf, const int *ty, const double4 *xb, const int *tb,
+                        const int *qbeg, const Coefs *cf, int ucap, int sstride, int *ulist,
+                        int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
+                        unsigned short *snbi, int *ovf, int *umax, int cq, int bexp, int *fcnt) {
+  if (nt1 && inner)
+    blk_build_t<R, G, U, true, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
+                                         ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp,
+                                         fcnt);
+  else if (nt1)
+    blk_build_t<R, G, U, true, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
+                                          ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
+                                          bexp, fcnt);
+  else if (inner)
+    blk_build_t<R, G, U, false, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
+                                          ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
+                                          bexp, fcnt);
+  else
+    blk_build_t<R, G, U, false, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,
+                                           sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf,
+                                           umax, cq, bexp, fcnt);
+}
+// n3: Newton-3 inside the blocks (rows first in the union, the later rows' share; fcnt gets
+// the full counts)
+inline void blk_build(int shape, bool nt1, bool inner, bool n3, hipStream_t s, int n,
+                      const QBins &q, int dim, const double4 *xf, const int *ty,
+                      const double4 *xb, const int *tb, const int *qbeg, const Coefs *cf,
+                      int ucap, int sstride, int *ulist, int *ucnt, int *rcnt,
+                      unsigned short *snbr, int *icnt, unsigned short *snbi, int *ovf, int *umax,
+                      int cq, int bexp, int *fcnt) {
+#ifdef SPH_STUDY
+#define SPH_IF_N3(R, G, U)                                                                  \
+  if (n3)                                                                                 \
+    blk_build_n<R, G, U, true>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,    \
+                               sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
+                               bexp, fcnt);                                                \
+  else
+#else
+#define SPH_IF_N3(R, G, U) (void)n3;
+#endif
   switch (shape) {
 #define SPH_CASE(k, R, G, U)                                                                \
   case k:                                                                                 \
-    if (nt1 && inner)                                                                     \
-      blk_build_t<R, G, U, true, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                       ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
-    else if (nt1)                                                                         \
-      blk_build_t<R, G, U, true, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
-    else if (inner)                                                                       \
-      blk_build_t<R, G, U, false, true>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride, \
-                                        ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp); \
-    else                                                                                  \
-      blk_build_t<R, G, U, false, false>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,     \
-                                         sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, \
-                                         umax, cq, bexp);                                 \
+    SPH_IF_N3(R, G, U)                                                                    \
+    blk_build_n<R, G, U, false>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,   \
+                                sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
+                                bexp, fcnt);                                               \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE
+#undef SPH_IF_N3
   }
 }
 
@@ -1392,7 +1534,7 @@ inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int
                                   (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um, k.snbi, k.icnt,
-                     k.moved);
+                     k.moved, k.n3 ? 1 : 0);
 }
 template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
@@ -1429,11 +1571,12 @@ inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
                      a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq, k.snbi,
-                     k.icnt, k.moved);
+                     k.icnt, k.moved, k.n3 ? 1 : 0);
   if (k.nbig > 0)
     hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
                        k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
-                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq, k.snbi, k.icnt, k.moved);
+                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq, k.snbi, k.icnt, k.moved,
+                       k.n3 ? 1 : 0);
 }
 
 // the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum

@@ -128,6 +128,12 @@ static bool mp_typed_env() {
   static bool v = study_int("SPH_MP_TYPED", 1) != 0;
   return v;
 }
+// SPH_N3 (study builds only; default 0): the block build keeps each pair of rows of one
+// block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
+static bool n3_env() {
+  static bool v = BLK_N3_BUILT && study_int("SPH_N3", 0) != 0;
+  return v;
+}
 // SPH_MP_RHOFUSE (default 1): the multiphase engine's list fill sums rhosum/multiphase over
 // the hits it finds when the list is built in the step whose forces follow (k_neigh3 RHO)
 static bool rhofuse_env() {
@@ -284,6 +290,8 @@ struct sph_engine {
   bool inner = false, inner_written = false;  // (written: by k_blk_build, with the full rows)
   DBuf<int> nbs;  // fixed-stride scratch rows of a CSR build (list_q)
   DBuf<int> mx, ccnt;  // scratch scalars; full-list row counts of the current build
+  DBuf<int> pcnt;      // block path with Newton-3 (blk_n3): the rows' stored counts
+  bool blk_n3 = false;
   DBuf<long long> blen;
   // cub scratch
   DBuf<unsigned char> tmp;
@@ -1336,10 +1344,15 @@ struct sph_engine {
         snbi.reserve((size_t)n * blk_sstride + 2 * chunk);
         icnt.reserve(n);
       }
+      // Newton-3 inside the blocks (k_blk_build N3): the passes walk the stored rows (pcnt),
+      // ccnt keeps the full counts
+      blk_n3 = v2 && n3_env();
+      if (blk_n3) pcnt.reserve(n + 1);
       if (v2)
-        blk_build(shape, nt1(), want_inner, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p,
-                  dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, icnt.p, snbi.p,
-                  mx.p, mx.p + 1, blk_cq(), study_int("SPH_BEXP", 0));
+        blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
+                  qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
+                  blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
+                  study_int("SPH_BEXP", 0), ccnt.p);
       else
         blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
@@ -1394,7 +1407,8 @@ struct sph_engine {
     k.sstride = blk_sstride;
     k.ulist = ulist.p;
     k.ucnt = ucnt.p;
-    k.rcnt = ccnt.p;
+    k.rcnt = blk_n3 ? pcnt.p : ccnt.p;
+    k.n3 = blk_n3;
     k.snbr = snbr.p;
     if (inner) {
       k.snbi = snbi.p;
@@ -2330,10 +2344,15 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->dr_req, &e->pc_flag,
                   &e->pc_cand, &e->pc_otag, &e->pc_idx})
     b->release();
-  for (auto *b : {&e->pc_rec, &e->pc_gat, &e->pc_Wd, &e->pc_vals, &e->pc_nrec}) b->release();
+  for (auto *b : {&e->pc_rec, &e->pc_gat, &e->pc_Wd, &e->pc_vals, &e->pc_nrec, &e->pc_v0,
+                  &e->pc_v1})
+    b->release();
+  e->pc_k0.release();
+  e->pc_k1.release();
+  e->pc_cnt.release();
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
-                  &e->ccnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
+                  &e->ccnt, &e->pcnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
                   &e->tcnt, &e->ulist, &e->ucnt, &e->bl})
     b->release();
   for (auto *b : {&e->bkey, &e->bkey2}) b->release();

@@ -468,19 +468,38 @@ def c2_pair_main(args, sph):
     # (sph_hip_list_keyed, key = neighbor->ncalls); a rebuild every `every` steps
     nl_full, nl_half = sph.NeighList(foff, fnb), sph.NeighList(hoff, hnb)
     every = 10
+    cns = np.zeros((2, 2))
+    cns[1, 1] = 3.3 * 3.3   # Neighbor::cutneighsq = (h + skin)^2
 
-    def lammps_step(k):
+    xs, vs, rs, es = (np.ascontiguousarray(a, dtype=np.float64).copy() for a in (x, v, rho, e))
+
+    def lammps_step(k, device_lists):
         t0 = time.perf_counter()
         key = k // every
-        ctx.atoms(N, 0, x, t, vest=v, rho=rho, e=e)
-        ctx.list_neighlist(sph.SPH_LIST_FULL, nl_full, key)
-        ctx.rhosum(r)
+        if not device_lists:
+            ctx.atoms(N, 0, x, t, vest=v, rho=rho, e=e)
+            ctx.list_neighlist(sph.SPH_LIST_FULL, nl_full, key)
+            ctx.rhosum(r)
+            kms = ctx.last_kernel_ms()
+            ctx.atoms_rho(rho)     # (same step: the shim restages rho only)
+            ctx.list_neighlist(sph.SPH_LIST_HALF, nl_half, key)
+            ctx.taitwater(f, drho, de)
+            return time.perf_counter() - t0, kms + ctx.last_kernel_ms()
+        # the shim's device-list path: LAMMPS' arrays registered as mapped host memory (once,
+        # sph_hip_host_arrays), the whole atom set restaged at a rebuild, positions / vest /
+        # rho / e between rebuilds (sph_hip_atoms_update), the lists built on the device at a
+        # new key (sph_hip_build_list), rho written and f / drho / de added in place
+        if k % every == 0:
+            ctx.atoms(N, 0, xs, t, vest=vs, rho=rs, e=es)
+        else:
+            ctx.atoms_update(xs, vest=vs, rho=rs, e=es)
+        ctx.build_list(sph.SPH_LIST_FULL, cns, key)
+        ctx.rhosum(rs)
         kms = ctx.last_kernel_ms()
-        ctx.atoms_rho(rho)     # (same step: the shim restages rho only)
-        ctx.list_neighlist(sph.SPH_LIST_HALF, nl_half, key)
+        ctx.atoms_rho(rs)
+        ctx.build_list(sph.SPH_LIST_HALF, cns, key)
         ctx.taitwater(f, drho, de)
-        kms += ctx.last_kernel_ms()
-        return time.perf_counter() - t0, kms
+        return time.perf_counter() - t0, kms + ctx.last_kernel_ms()
 
     for _ in range(args.warmup):
         step()
@@ -491,12 +510,18 @@ def c2_pair_main(args, sph):
         wall += w
         for k, val in ms.items():
             acc[k] = acc.get(k, 0.0) + val / args.steps
-    lw, lk = 0.0, 0.0
     nls = max(args.steps, every) // every * every   # whole rebuild periods
-    for k in range(nls):
-        w, km = lammps_step(k)
-        lw += w
-        lk += km
+    pattern = {}
+    for dl in (False, True):
+        if dl:
+            ctx.host_arrays(N, x=xs, vest=vs, rho=rs, e=es, f=f, drho=drho, de=de)
+        lw, lk = 0.0, 0.0
+        for k in range(nls):
+            w, km = lammps_step(k + (1000 if dl else 0), dl)
+            lw += w
+            lk += km
+        pattern[dl] = (lw, lk)
+    lw, lk = pattern[False]
     n_full, n_half = foff[-1] / N, hoff[-1] / N
     by = {"rhosum": 40 + 4 * n_half, "taitwater": 104 + 4 * n_half}
     by["taitwater_list_reused"] = by["taitwater"]
@@ -522,7 +547,17 @@ def c2_pair_main(args, sph):
                        "steps": nls,
                        "wall_ms_per_step_incl_pcie": lw / nls * 1e3,
                        "kernel_ms_per_step": lk / nls,
-                       "wall_over_kernel": lw * 1e3 / max(lk, 1e-12)}},
+                       "wall_over_kernel": lw * 1e3 / max(lk, 1e-12)},
+                   "lammps_pattern_device_lists": {
+                       "what": "the shim's device-list path: LAMMPS' arrays registered as "
+                               "mapped host memory (sph_hip_host_arrays), sph_hip_atoms at a "
+                               "rebuild else sph_hip_atoms_update, sph_hip_build_list FULL / "
+                               "HALF at each new key (no host list copy or upload), rho "
+                               "written and f / drho / de added in place by the device",
+                       "steps": nls,
+                       "wall_ms_per_step_incl_pcie": pattern[True][0] / nls * 1e3,
+                       "kernel_ms_per_step": pattern[True][1] / nls,
+                       "wall_over_kernel": pattern[True][0] * 1e3 / max(pattern[True][1], 1e-12)}},
         "roofline": {"bound": "hbm", "kernel": "taitwater (half list: forward + reverse "
                                                "gather)",
                      "achieved": kern["taitwater"]["achieved_GBs"], "peak": PEAK_HBM_GBS,

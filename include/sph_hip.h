@@ -98,6 +98,19 @@ int sph_hip_atoms(sph_hip_ctx *ctx, int nlocal, int nghost, const double *x,
    and later pair computes of one step under hybrid/overlay, after forward_comm_pair of the
    density (the shim keys it on ntimestep + neighbor->ncalls + nlocal/nghost). */
 int sph_hip_atoms_rho(sph_hip_ctx *ctx, const double *rho);
+/* Restage x (and vest, rho, e where non-NULL) of the SAME atom set as the last
+   sph_hip_atoms (same nlocal/nghost and types: a step between rebuilds) -- no type upload or
+   check, staged lists kept. */
+int sph_hip_atoms_update(sph_hip_ctx *ctx, const double *x, const double *vest,
+                         const double *rho, const double *e);
+/* Register the caller's per-atom arrays (capacity nmax atoms: x, vest, f nmax*3, the others
+   nmax; any may be NULL) as mapped host memory: the staging kernels then read x/vest/rho/e
+   straight from them over PCIe and the styles write rho / add f, drho, de straight into
+   them, instead of a host copy, a PCIe copy and a host loop per call.  Call again whenever
+   the arrays move (LAMMPS: atom->nmax or a pointer changed; the shim checks every compute);
+   nmax = 0 unregisters.  An array the runtime refuses to register keeps the copy path. */
+int sph_hip_host_arrays(sph_hip_ctx *ctx, int nmax, double *x, double *vest, double *rho,
+                        double *e, double *f, double *drho, double *de);
 
 /* Stage a LAMMPS NeighList (list->inum, ilist, numneigh, firstneigh; NEIGHMASK bits are
    stripped).  kind = SPH_LIST_FULL (gather-only kernels, nothing written to ghosts) or
@@ -116,6 +129,16 @@ int sph_hip_list(sph_hip_ctx *ctx, int kind, int inum, const int *ilist,
    uploads (= sph_hip_list). */
 int sph_hip_list_keyed(sph_hip_ctx *ctx, int kind, int64_t key, int inum, const int *ilist,
                        const int *numneigh, const int *const *firstneigh);
+/* The list built on the DEVICE from the staged atoms (SURVEY 8(b) device-list path; the GPU
+   package's GPU_NEIGH, src/GPU/pair_lj_cut_gpu.cpp:97-104): kind SPH_LIST_FULL =
+   Neighbor::full_bin membership (neigh_full.cpp:241-344: j != i, rsq <= cutneighsq[it][jt]),
+   SPH_LIST_HALF = half_from_full_newton of it (neigh_derive.cpp:83-150); owned rows, ilist
+   the identity.  cutneighsq = neighbor->cutneighsq ((nt+1)^2).  key as sph_hip_list_keyed:
+   a staged device-built list of this kind with the same key is reused (hybrid/overlay
+   sub-styles, the fix's copy).  Replaces the host NeighList copy and upload per rebuild. */
+int sph_hip_build_list(sph_hip_ctx *ctx, int kind, int64_t key, const double *cutneighsq);
+/* Row lengths of the staged list (inum values, in ilist order): LAMMPS' numneigh. */
+int sph_hip_list_numneigh(sph_hip_ctx *ctx, int *numneigh);
 /* Same, from a CSR list (row i = neigh[off[i]..off[i+1]) for owned atom i). */
 int sph_hip_list_csr(sph_hip_ctx *ctx, int kind, int inum, const int64_t *off,
                      const int *neigh);

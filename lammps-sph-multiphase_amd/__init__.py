@@ -111,7 +111,11 @@ EXPORTS = {
     "sph_hip_list": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
     "sph_hip_list_keyed": (_i, [_vp, _i, C.c_int64, _i, _vp, _vp, _vp]),
     "sph_hip_atoms_rho": (_i, [_vp, _dp]),
+    "sph_hip_atoms_update": (_i, [_vp, _dp, _vp, _vp, _vp]),
+    "sph_hip_host_arrays": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sph_hip_list_csr": (_i, [_vp, _i, _i, _lp, _ip]),
+    "sph_hip_build_list": (_i, [_vp, _i, C.c_int64, _dp]),
+    "sph_hip_list_numneigh": (_i, [_vp, _ip]),
     "sph_hip_rhosum": (_i, [_vp, _dp]),
     "sph_hip_taitwater": (_i, [_vp, _dp, _dp, _dp, _vp]),
     "sph_hip_heatconduction": (_i, [_vp, _dp]),
@@ -292,9 +296,40 @@ class PairContext:
             _chk(self.L.sph_hip_list_keyed(self.h, kind, int(key), len(ilist), ilist.ctypes.data,
                                            numneigh.ctypes.data, C.cast(ptrs, C.c_void_p)))
 
+    def atoms_update(self, x, vest=None, rho=None, e=None):
+        """Same atom set as the last atoms(): restage positions (and vest/rho/e)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        vest = None if vest is None else np.ascontiguousarray(vest, dtype=np.float64)
+        rho = None if rho is None else np.ascontiguousarray(rho, dtype=np.float64)
+        e = None if e is None else np.ascontiguousarray(e, dtype=np.float64)
+        _chk(self.L.sph_hip_atoms_update(self.h, x, _ptr(vest), _ptr(rho), _ptr(e)))
+        self._keep_u = (x, vest, rho, e)
+
+    def host_arrays(self, nmax, x=None, vest=None, rho=None, e=None, f=None, drho=None,
+                    de=None):
+        """Register the caller's arrays as mapped host memory (sph_hip_host_arrays); they must
+        stay alive (and in place) until host_arrays(0) or close()."""
+        arrs = [x, vest, rho, e, f, drho, de]
+        for a in arrs:
+            assert a is None or (a.dtype == np.float64 and a.flags["C_CONTIGUOUS"])
+        _chk(self.L.sph_hip_host_arrays(self.h, int(nmax),
+                                        *[None if a is None else a.ctypes.data for a in arrs]))
+        self._keep_h = arrs
+
     def atoms_rho(self, rho):
         """Restage rho only (sph_hip_atoms_rho)."""
         _chk(self.L.sph_hip_atoms_rho(self.h, np.ascontiguousarray(rho, dtype=np.float64)))
+
+    def build_list(self, kind, cutneighsq, key=-1):
+        """The list built on the device from the staged atoms (sph_hip_build_list):
+        cutneighsq = Neighbor::cutneighsq, (ntypes+1)^2; key as list_neighlist."""
+        c = np.ascontiguousarray(cutneighsq, dtype=np.float64).ravel()
+        _chk(self.L.sph_hip_build_list(self.h, kind, int(key), c))
+
+    def numneigh(self, inum):
+        out = np.zeros(max(inum, 1), dtype=np.int32)
+        _chk(self.L.sph_hip_list_numneigh(self.h, out))
+        return out[:inum]
 
     def list_neighlist(self, kind, nl, key=-1):
         """Stage a NeighList (sph_hip_list_keyed; key < 0: always upload)."""

@@ -35,7 +35,7 @@ struct StagedList {
   int64_t key = -1;
   DBuf<int> ilist, off, nbr, rkey, rnbr, rown, roff;
   std::vector<int> hoff, hilist;
-  bool rev_ok = false;
+  bool rev_ok = false, devbuilt = false;
 };
 
 struct sph_hip_ctx {
@@ -69,6 +69,36 @@ struct sph_hip_ctx {
   std::vector<double> h1;
   std::vector<int> hoff, hnbr, hilist;
   bool coef_dirty = true;
+  // the caller's host arrays registered as mapped host memory (sph_hip_host_arrays): the
+  // kernels read inputs from and add results into them directly over PCIe
+  struct HostMap {
+    void *host = nullptr;
+    size_t bytes = 0;
+    void *dev = nullptr;
+  };
+  std::vector<HostMap> hmaps;
+  // device address of [p, p + bytes) if a registered range holds it, else nullptr
+  void *mapped(const void *p, size_t bytes) const {
+    if (!p) return nullptr;
+    const char *q = static_cast<const char *>(p);
+    for (const auto &m : hmaps) {
+      const char *h = static_cast<const char *>(m.host);
+      if (q >= h && q + bytes <= h + m.bytes)
+        return static_cast<char *>(m.dev) + (q - h);
+    }
+    return nullptr;
+  }
+  void unmap_all() {
+    for (auto &m : hmaps) (void)hipHostUnregister(m.host);
+    hmaps.clear();
+  }
+  // device-built lists (sph_hip_build_list, sph_pair_lists.hip): the active list was built
+  // on the device; bins, bin-ordered copy, counts and the full list behind a half one
+  bool list_devbuilt = false;
+  DBuf<double> lbox;
+  DBuf<unsigned> bkey, bkey2;
+  DBuf<int> bidx, bidx2, qbeg, tb, lcnt, loff, lnbr;
+  DBuf<double4> xb;
   // the active list's build key (-1: not reusable) and the parked lists, one per kind
   int64_t list_key = -1;
   StagedList parked[2];
@@ -86,6 +116,7 @@ struct sph_hip_ctx {
     std::swap(hoff, p.hoff);
     std::swap(hilist, p.hilist);
     std::swap(rev_ok, p.rev_ok);
+    std::swap(list_devbuilt, p.devbuilt);
   }
   // make the kind-k list the active one: the active list is parked under its own kind,
   // the kind-k slot's list (if any) becomes active; a slot's stale buffers are kept for reuse
@@ -120,6 +151,11 @@ struct sph_hip_ctx {
     for (auto &p : parked)
       for (DBuf<int> *b : {&p.ilist, &p.off, &p.nbr, &p.rkey, &p.rnbr, &p.rown, &p.roff})
         b->release();
+    for (DBuf<int> *b : {&bidx, &bidx2, &qbeg, &tb, &lcnt, &loff, &lnbr}) b->release();
+    bkey.release();
+    bkey2.release();
+    xb.release();
+    lbox.release();
   }
   // optional device timing of each style call's kernels (sph_hip_set_timing)
   bool timing = false;

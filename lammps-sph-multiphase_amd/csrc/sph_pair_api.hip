@@ -110,6 +110,7 @@ int sph_hip_destroy(sph_hip_ctx *c) {
   if (!c) return SPH_HIP_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->unmap_all();
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   c->xf.release();
@@ -195,10 +196,83 @@ static __global__ void k_pack_atoms(int nall, const double *__restrict__ x,
   const int t = ty[i];
   if (t < 1 || t > ntypes) atomicOr(bad, 1);
 }
+static __global__ void k_pack_atoms_notype(int nall, const double *__restrict__ x,
+                                           const double *__restrict__ v,
+                                           const double *__restrict__ rho,
+                                           const double *__restrict__ e,
+                                           double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                           double *__restrict__ en) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nall) return;
+  xf[i] = make_double4(x[3 * i], x[3 * i + 1], x[3 * i + 2], 0.0);
+  vr[i] = make_double4(v ? v[3 * i] : 0.0, v ? v[3 * i + 1] : 0.0, v ? v[3 * i + 2] : 0.0,
+                       rho ? rho[i] : 0.0);
+  if (e) en[i] = e[i];
+}
+// results straight into the caller's (mapped host) arrays: rows r -> atom ilist[r] (nullptr:
+// r itself); rho written, f / drho / de added
+static __global__ void k_out_rho(int n, const int *__restrict__ ilist,
+                                 const double *__restrict__ src, double *__restrict__ rho) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int i = ilist ? ilist[r] : r;
+  rho[i] = src[i];
+}
+static __global__ void k_out_add(int n, const int *__restrict__ ilist,
+                                 const double4 *__restrict__ fo, const double *__restrict__ dd,
+                                 double *__restrict__ f, double *__restrict__ drho,
+                                 double *__restrict__ de) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const int i = ilist ? ilist[r] : r;
+  if (f) {
+    const double4 a = fo[i];
+    f[3 * i] += a.x;
+    f[3 * i + 1] += a.y;
+    f[3 * i + 2] += a.z;
+    if (drho) drho[i] += a.w;
+  }
+  if (de) de[i] += dd[i];
+}
 static __global__ void k_set_rho(int nall, const double *__restrict__ rho,
                                  double4 *__restrict__ vr) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nall) vr[i].w = rho[i];
+}
+
+int sph_hip_host_arrays(sph_hip_ctx *c, int nmax, double *x, double *vest, double *rho,
+                        double *e, double *f, double *drho, double *de) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && nmax >= 0, SPH_HIP_EINVAL, "sph_hip_host_arrays: bad argument");
+  SPH_HIP_TRY(hipSetDevice(c->device));
+  SPH_HIP_TRY(hipStreamSynchronize(c->stream));  // (nothing in flight reads the old ones)
+  c->unmap_all();
+  if (nmax == 0) return SPH_HIP_OK;
+  const struct {
+    void *p;
+    size_t n;
+  } arr[7] = {{x, 3}, {vest, 3}, {rho, 1}, {e, 1}, {f, 3}, {drho, 1}, {de, 1}};
+  for (const auto &a : arr) {
+    if (!a.p || c->mapped(a.p, a.n * nmax * sizeof(double))) continue;
+    const size_t bytes = a.n * (size_t)nmax * sizeof(double);
+    if (hipHostRegister(a.p, bytes, hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();  // (not registrable: that array takes the copy path)
+      continue;
+    }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, a.p, 0) != hipSuccess || !d) {
+      (void)hipGetLastError();
+      (void)hipHostUnregister(a.p);
+      continue;
+    }
+    c->hmaps.push_back(sph_hip_ctx::HostMap{a.p, bytes, d});
+  }
+  SPH_API_END
+}
+
+// mapped-host inputs -> the gather records (k_pack_atoms reads them over PCIe)
+static const double *in_dev(sph_hip_ctx *c, const double *h, size_t n) {
+  return static_cast<const double *>(c->mapped(h, n * sizeof(double)));
 }
 
 int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const double *vest,
@@ -226,15 +300,21 @@ int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const
   c->lbad.reserve(1);
   double *const rx = c->raw.p, *const rv = rx + 3 * nall, *const rr = rv + 3 * nall,
                *const re = rr + nall;
-  SPH_HIP_TRY(hipMemcpyAsync(rx, x, 3 * nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  if (vest) SPH_HIP_TRY(hipMemcpyAsync(rv, vest, 3 * nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  if (rho) SPH_HIP_TRY(hipMemcpyAsync(rr, rho, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  if (e) SPH_HIP_TRY(hipMemcpyAsync(re, e, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  // each array read straight from mapped host memory by the pack kernel when registered
+  // (sph_hip_host_arrays), else copied up first
+  auto up = [&](const double *h, size_t n, double *staging) -> const double * {
+    if (!h) return nullptr;
+    if (const double *d = in_dev(c, h, n)) return d;
+    SPH_HIP_TRY(hipMemcpyAsync(staging, h, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return staging;
+  };
+  const double *dx = up(x, 3 * nall, rx), *dv = up(vest, 3 * nall, rv),
+               *dr = up(rho, nall, rr), *de_ = up(e, nall, re);
   SPH_HIP_TRY(hipMemcpyAsync(c->ty.p, type, nall * sizeof(int), hipMemcpyHostToDevice, c->stream));
   SPH_HIP_TRY(hipMemsetAsync(c->lbad.p, 0, sizeof(int), c->stream));
   hipLaunchKernelGGL(k_pack_atoms, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, c->stream,
-                     (int)nall, rx, vest ? rv : nullptr, rho ? rr : nullptr, e ? re : nullptr,
-                     c->ty.p, c->ntypes, c->xf.p, c->vr.p, c->en.p, c->lbad.p);
+                     (int)nall, dx, dv, dr, de_, c->ty.p, c->ntypes, c->xf.p, c->vr.p, c->en.p,
+                     c->lbad.p);
   int bad = 0;
   SPH_HIP_TRY(hipMemcpyAsync(&bad, c->lbad.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -246,6 +326,31 @@ int sph_hip_atoms(sph_hip_ctx *c, int nlocal, int nghost, const double *x, const
   SPH_API_END
 }
 
+int sph_hip_atoms_update(sph_hip_ctx *c, const double *x, const double *vest,
+                         const double *rho, const double *e) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(c && x, SPH_HIP_EINVAL, "sph_hip_atoms_update: bad argument");
+  SPH_REQUIRE(c->have_atoms, SPH_HIP_EINVAL, "sph_hip_atoms_update: no atoms staged");
+  SPH_HIP_TRY(hipSetDevice(c->device));
+  const size_t nall = (size_t)c->nlocal + c->nghost;
+  if (nall == 0) return SPH_HIP_OK;  // (rmass / cv of the same atom set stay staged)
+  c->raw.reserve(8 * nall);
+  double *const rx = c->raw.p, *const rv = rx + 3 * nall, *const rr = rv + 3 * nall,
+               *const re = rr + nall;
+  auto up = [&](const double *h, size_t n, double *staging) -> const double * {
+    if (!h) return nullptr;
+    if (const double *d = in_dev(c, h, n)) return d;
+    SPH_HIP_TRY(hipMemcpyAsync(staging, h, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return staging;
+  };
+  const double *dx = up(x, 3 * nall, rx), *dv = up(vest, 3 * nall, rv),
+               *dr = up(rho, nall, rr), *de_ = up(e, nall, re);
+  hipLaunchKernelGGL(k_pack_atoms_notype, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0,
+                     c->stream, (int)nall, dx, dv, dr, de_, c->xf.p, c->vr.p, c->en.p);
+  SPH_HIP_TRY(hipGetLastError());
+  SPH_API_END
+}
+
 int sph_hip_atoms_rho(sph_hip_ctx *c, const double *rho) {
   SPH_API_BEGIN
   SPH_REQUIRE(c && rho, SPH_HIP_EINVAL, "sph_hip_atoms_rho: bad argument");
@@ -254,9 +359,13 @@ int sph_hip_atoms_rho(sph_hip_ctx *c, const double *rho) {
   const size_t nall = (size_t)c->nlocal + c->nghost;
   if (nall == 0) return SPH_HIP_OK;
   c->raw.reserve(8 * nall);
-  SPH_HIP_TRY(hipMemcpyAsync(c->raw.p, rho, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const double *dr = in_dev(c, rho, nall);
+  if (!dr) {
+    SPH_HIP_TRY(hipMemcpyAsync(c->raw.p, rho, nall * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    dr = c->raw.p;
+  }
   hipLaunchKernelGGL(k_set_rho, dim3((unsigned)((nall + 255) / 256)), dim3(256), 0, c->stream,
-                     (int)nall, c->raw.p, c->vr.p);
+                     (int)nall, dr, c->vr.p);
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   SPH_API_END
 }
@@ -285,6 +394,7 @@ static void upload_list(sph_hip_ctx *c, int kind, int inum, int64_t key) {
   SPH_REQUIRE(tot < (size_t)0x7fffffff, SPH_HIP_EOVERFLOW, "neighbor list too long (%zu)", tot);
   const int nall = c->nlocal + c->nghost;
   c->list_key = -1;  // (until the upload is checked)
+  c->list_devbuilt = false;
   c->off.reserve(inum + 1);
   c->nbr.reserve(tot > 0 ? tot : 1);
   c->ilist.reserve(inum > 0 ? inum : 1);
@@ -385,6 +495,14 @@ int sph_hip_rhosum(sph_hip_ctx *c, double *rho) {
   launch_rhosum(c->dim, false, c->ntypes == 1, c->stream, ra);
   c->tstop();
   SPH_HIP_TRY(hipGetLastError());
+  if (double *dr = static_cast<double *>(c->mapped(rho, (size_t)nall * sizeof(double)))) {
+    // straight into the caller's (mapped) rho
+    hipLaunchKernelGGL(k_out_rho, dim3((c->inum + 255) / 256), dim3(256), 0, c->stream, c->inum,
+                       (const int *)c->ilist.p, (const double *)c->rho_out.p, dr);
+    SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+    c->tread();
+    return SPH_HIP_OK;
+  }
   c->h1.resize(nall);
   SPH_HIP_TRY(hipMemcpyAsync(c->h1.data(), c->rho_out.p, nall * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -450,6 +568,26 @@ static void run_force(sph_hip_ctx *c, int mode, double *f, double *drho, double 
   c->tstop();
   SPH_HIP_TRY(hipGetLastError());
   double hv[6] = {0, 0, 0, 0, 0, 0};
+  {  // results added straight into the caller's (mapped) arrays when every one is registered
+    const size_t nb = (size_t)nall * sizeof(double);
+    double *mf = (mode & M_TAIT) ? static_cast<double *>(c->mapped(f, 3 * nb)) : nullptr;
+    double *md = (mode & M_TAIT) && drho ? static_cast<double *>(c->mapped(drho, nb)) : nullptr;
+    double *me = de ? static_cast<double *>(c->mapped(de, nb)) : nullptr;
+    const bool ok = (!(mode & M_TAIT) || (mf && (md || !drho))) && (me || !de);
+    if (ok) {
+      const bool half = c->list_kind == SPH_LIST_HALF;
+      const int rows = half ? nall : c->inum;
+      hipLaunchKernelGGL(k_out_add, dim3((rows + 255) / 256), dim3(256), 0, c->stream, rows,
+                         half ? (const int *)nullptr : (const int *)c->ilist.p,
+                         (const double4 *)c->fo.p, (const double *)c->de.p, mf, md, me);
+      if (virial) SPH_HIP_TRY(hipMemcpyAsync(hv, c->virial.p, 6 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+      c->tread();
+      if (virial)
+        for (int k = 0; k < 6; k++) virial[k] += hv[k];
+      return;
+    }
+  }
   if (mode & M_TAIT) {
     c->h4.resize(nall);
     SPH_HIP_TRY(hipMemcpyAsync(c->h4.data(), c->fo.p, nall * sizeof(double4), hipMemcpyDeviceToHost, c->stream));

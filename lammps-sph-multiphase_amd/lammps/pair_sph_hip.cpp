@@ -7,6 +7,7 @@
 ------------------------------------------------------------------------------------------ */
 #include "pair_sph_hip.h"
 
+#include <cmath>
 #include <cstdio>
 #include <vector>
 
@@ -18,6 +19,7 @@
 #include "memory.h"
 #include "neigh_list.h"
 #include "neighbor.h"
+#include "pair.h"
 #include "sph_hip.h"
 #include "update.h"
 
@@ -38,11 +40,16 @@ struct StageKey {
 };
 bigint g_epoch = 0;
 StageKey g_key = {-1, -1, -1, -1, -1, false};
+// lists built on the device (sph_hip_build_list) instead of copied from the NeighList
+bool g_device_lists = true;
+std::vector<double> g_cns;
 // the device list of a kind is reused while this key is unchanged
 int64_t list_key(LAMMPS *lmp) { return (int64_t)(g_epoch << 40) + (int64_t)lmp->neighbor->ncalls; }
 }
 
 void LAMMPS_NS::sph_hip_new_run() { g_epoch++; }
+
+extern "C" void sph_hip_shim_set_device_lists(int on) { g_device_lists = on != 0; }
 
 sph_hip_ctx *LAMMPS_NS::sph_hip_rank_ctx(LAMMPS *lmp) {
   // one context per rank; made again when the system it was made for changed (a `clear`
@@ -80,10 +87,43 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
   const int nall = nlocal + nghost;
   const StageKey key = {g_epoch, lmp->update->ntimestep, lmp->neighbor->ncalls, nlocal, nghost,
                         multiphase};
+  // LAMMPS' per-atom arrays as mapped host memory (sph_hip_host_arrays): the device reads
+  // x / vest / rho / e and writes rho, adds f / drho / de in place over PCIe.  Registered
+  // again whenever AtomVec::grow moved them (nmax or a pointer changed) and at every run
+  // (a `clear` may hand out the same addresses for new arrays).
+  {
+    static bigint reg_epoch = -1;
+    double *const p[7] = {atom->x ? &atom->x[0][0] : NULL, atom->vest ? &atom->vest[0][0] : NULL,
+                          atom->rho, atom->e, atom->f ? &atom->f[0][0] : NULL, atom->drho,
+                          atom->de};
+    static double *reg[7] = {NULL, NULL, NULL, NULL, NULL, NULL, NULL};
+    static int reg_nmax = -1;
+    static sph_hip_ctx *reg_ctx = NULL;
+    bool same = reg_nmax == atom->nmax && reg_ctx == ctx && reg_epoch == g_epoch;
+    for (int k = 0; k < 7; k++) same = same && reg[k] == p[k];
+    if (!same && atom->nmax > 0) {
+      sph_hip_check(lmp, sph_hip_host_arrays(ctx, atom->nmax, p[0], p[1], p[2], p[3], p[4], p[5],
+                                             p[6]),
+                    "sph_hip_host_arrays");
+      for (int k = 0; k < 7; k++) reg[k] = p[k];
+      reg_nmax = atom->nmax;
+      reg_ctx = ctx;
+      reg_epoch = g_epoch;
+    }
+  }
   if (key.epoch == g_key.epoch && key.step == g_key.step && key.ncalls == g_key.ncalls &&
       key.nlocal == g_key.nlocal && key.nghost == g_key.nghost && (g_key.mp || !multiphase) &&
       nall && atom->rho) {
     sph_hip_check(lmp, sph_hip_atoms_rho(ctx, atom->rho), "sph_hip_atoms_rho");
+  } else if (key.epoch == g_key.epoch && key.ncalls == g_key.ncalls &&
+             key.nlocal == g_key.nlocal && key.nghost == g_key.nghost &&
+             (g_key.mp || !multiphase) && nall) {
+    // a new step of the same atom set (no reneighbor since): positions, vest, rho, e only
+    sph_hip_check(lmp,
+                  sph_hip_atoms_update(ctx, &atom->x[0][0], atom->vest ? &atom->vest[0][0] : NULL,
+                                       atom->rho, atom->e),
+                  "sph_hip_atoms_update");
+    g_key = key;
   } else {
     // x and vest are memory->create 2-D arrays: contiguous nmax*3 backing (memory.h:124-137)
     sph_hip_check(lmp,
@@ -99,7 +139,23 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
   // the list build is the key (run epoch + neighbor->ncalls, neighbor.cpp:1423): between
   // rebuilds the staged device copy of this kind is reused -- no host copy, no upload, and a
   // half list keeps its reverse list; sub-styles of hybrid/overlay on the other kind keep
-  // theirs
+  // theirs.  Device-list path (default): the list is built on the device from
+  // the staged atoms with Neighbor::init's cutneighsq, (sqrt(pair->cutsq) + skin)^2
+  // (neighbor.cpp:251-268), full_bin membership and half_from_full_newton's half.
+  Pair *pair = lmp->force->pair;
+  if (g_device_lists && pair && pair->cutsq) {
+    const int nt = atom->ntypes;
+    g_cns.assign((size_t)(nt + 1) * (nt + 1), 0.0);
+    for (int i = 1; i <= nt; i++)
+      for (int j = 1; j <= nt; j++) {
+        const double cutoff = sqrt(pair->cutsq[i][j]);
+        const double cut = cutoff + (cutoff > 0.0 ? lmp->neighbor->skin : 0.0);
+        g_cns[(size_t)i * (nt + 1) + j] = cut * cut;
+      }
+    sph_hip_check(lmp, sph_hip_build_list(ctx, kind, list_key(lmp), g_cns.data()),
+                  "sph_hip_build_list");
+    return;
+  }
   sph_hip_check(lmp,
                 sph_hip_list_keyed(ctx, kind, list_key(lmp), list->inum, list->ilist,
                                    list->numneigh, list->firstneigh),

@@ -310,6 +310,29 @@ void free_list(NeighList *l) {
   l->firstneigh = NULL;
 }
 
+// Device-built lists through the /hip classes (sph_hip_build_list): while on, the pair
+// drivers below make their style force->pair and set neighbor->skin for the duration of
+// compute(), the shim's device-list path then builds the lists from cutsq + skin exactly
+// as Neighbor::init sizes them; off (default), the caller's lists are staged.
+int g_devlists = 0;
+double g_devskin = 0.0;
+#ifdef SPH_SHIM
+extern "C" void sph_hip_shim_set_device_lists(int on);
+#endif
+struct DevListScope {
+  World &w;
+  DevListScope(World &w_, Pair *p) : w(w_) {
+#ifdef SPH_SHIM
+    sph_hip_shim_set_device_lists(g_devlists);
+#endif
+    if (g_devlists) {
+      w.lmp->force->pair = p;
+      w.neigh->skin = g_devskin;
+    }
+  }
+  ~DevListScope() { w.lmp->force->pair = NULL; }
+};
+
 // Pair::init (pair.cpp:174-229) minus init_style (no neighbor request machinery here):
 // cutsq[i][j] = cutsq[j][i] = cut*cut with cut = init_one(i,j).
 void pair_init_cutsq(Pair *p, int ntypes) {
@@ -433,7 +456,10 @@ int REFNAME(rhosum)(int dim, int ntypes, int nlocal, int nghost, const double *x
   NeighList *l = make_list(w, nlocal, off, neigh);
   p->list = l;
   SPH_INIT(p);
-  p->compute(0, 0);
+  {
+    DevListScope dl(w, p);
+    p->compute(0, 0);
+  }
   for (int i = 0; i < nlocal; i++) rho[i] = w.lmp->atom->rho[i];
   free_list(l);
   return 0;
@@ -484,7 +510,10 @@ static int run_tait(int morris, int dim, int ntypes, int nlocal, int nghost, int
   NeighList *l = make_list(w, nlocal, off, neigh);
   p->list = l;
   SPH_INIT(p);
-  p->compute(0, 0);
+  {
+    DevListScope dl(w, p);
+    p->compute(0, 0);
+  }
   Atom *a = w.lmp->atom;
   for (int i = 0; i < nlocal + nghost; i++) {
     for (int k = 0; k < 3; k++) f[3 * i + k] = a->f[i][k];
@@ -534,10 +563,19 @@ int REFNAME(heatconduction)(int dim, int ntypes, int nlocal, int nghost, int new
   NeighList *l = make_list(w, nlocal, off, neigh);
   p->list = l;
   SPH_INIT(p);
-  p->compute(0, 0);
+  {
+    DevListScope dl(w, p);
+    p->compute(0, 0);
+  }
   for (int i = 0; i < nlocal + nghost; i++) de[i] = w.lmp->atom->de[i];
   free_list(l);
   return 0;
+}
+
+// the device-list switch of the single-phase drivers above (DevListScope)
+void REFNAME(set_device_lists)(int on, double skin) {
+  g_devlists = on;
+  g_devskin = skin;
 }
 
 // ---- multiphase styles (atom_style meso/multiphase: per-atom rmass) -------------------

@@ -4,6 +4,8 @@ inputs (owned+ghost arrays and a NeighList) and must reproduce the reference loo
 pair_sph_taitwater_morris.cpp:52-200, pair_sph_heatconduction.cpp:47-134) as restated in
 oracle/sph_oracle.c.  Tolerance: 1e-10 normwise relative (BASELINE.json north_star);
 the FULL-list path changes only the summation order, the HALF path adds atomic ordering."""
+import copy
+
 import numpy as np
 import pytest
 
@@ -211,3 +213,85 @@ def test_keyed_list_reuse(gpu, sph_amd):
               rho=P["rho_all"][:-1], e=P["e_all"][:-1])
     with pytest.raises(sph_amd.HipError):
         ctx.rhosum(np.zeros(nall))
+
+
+@pytest.mark.parametrize("system,dim", [("c2", 3), ("c2", 2), ("c3", 3)])
+def test_device_built_lists(gpu, sph_amd, system, dim):
+    """sph_hip_build_list (the device-list path of the shim): from the staged owned + ghost
+    atoms, the FULL list has Neighbor::full_bin's membership and the HALF list
+    half_from_full_newton's -- row lengths bit-exact against the oracle's lists -- and the
+    styles on them match the oracle (rhosum 1e-13; taitwater Newton-3 scatter incl. the
+    ghosts' shares, heat conduction 1e-10)."""
+    s = (c2_system(8 if dim == 3 else 24, dim=dim) if system == "c2" else c3_system(8))
+    ph = po.c2_physics(3.0) if system == "c2" else po.c3_physics(3.0)
+    P = prepared(s, ph)
+    g, n, nall = P["g"], s.n, P["g"].nall
+    cns = np.asarray(P["cns"], dtype=np.float64).reshape(s.ntypes + 1, s.ntypes + 1)
+    ctx = _ctx(sph_amd, s, ph, P)
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns, key=1)
+    assert np.array_equal(ctx.numneigh(n), np.diff(P["foff"]).astype(np.int32))
+    if ph.rhosum_nstep > 0:
+        rho = ctx.rhosum(np.zeros(nall))[:n]
+        want = po.rhosum(dim, g, s.ntypes, s.mass, ph.rhosum_cut, P["foff"], P["fnb"])
+        assert rel_err(rho, want) < 1e-13
+    ctx.build_list(sph_amd.SPH_LIST_HALF, cns, key=1)
+    assert np.array_equal(ctx.numneigh(n), np.diff(P["hoff"]).astype(np.int32))
+    f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    ctx.taitwater(f, drho, de)
+    if ph.heat:
+        ctx.heatconduction(de)
+    wf, wd, we = oracle_forces(s, ph, P, reverse=False)
+    assert rel_err(f, wf) < TOL
+    assert rel_err(drho, wd) < TOL
+    assert rel_err(de, we) < TOL
+    # the same key again: the staged device list is reused (no rebuild), same results
+    ctx.build_list(sph_amd.SPH_LIST_HALF, cns, key=1)
+    f2, d2, e2 = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    ctx.taitwater(f2, d2, e2)
+    assert rel_err(f2, wf) < TOL
+
+
+def test_mapped_host_arrays_and_update(gpu, sph_amd):
+    """sph_hip_host_arrays (the shim registers LAMMPS' arrays): the staging kernels read x /
+    vest / rho / e straight from mapped host memory, rhosum writes rho and taitwater / heat
+    add f / drho / de in place -- the same results as the copy path, added (not assigned) to
+    what the arrays held; sph_hip_atoms_update restages a moved atom set without types."""
+    s = c3_system(8)
+    ph = po.c3_physics(3.0)
+    P = prepared(s, ph)
+    g, n, nall = P["g"], s.n, P["g"].nall
+    cns = np.asarray(P["cns"], dtype=np.float64)
+    x = np.ascontiguousarray(g.x).copy()
+    vest, rho, e = (np.ascontiguousarray(P[k]).copy() for k in ("vest_all", "rho_all", "e_all"))
+    f, drho, de = np.full((nall, 3), 0.25), np.full(nall, -0.5), np.full(nall, 2.0)
+    ctx = sph_amd.PairContext(3, 2, 1)
+    ctx.host_arrays(nall, x=x, vest=vest, rho=rho, e=e, f=f, drho=drho, de=de)
+    ctx.atoms(g.nlocal, g.nghost, x, g.type, vest=vest, rho=rho, e=e)
+    ctx.taitwater_coeff(ph.rho0, ph.c0, ph.c0 * ph.c0 * ph.rho0 / 7.0, ph.visc, ph.tait_cut,
+                        s.mass, morris=ph.morris)
+    ctx.heatconduction_coeff(ph.alpha, ph.heat_cut, s.mass)
+    ctx.build_list(sph_amd.SPH_LIST_HALF, cns, key=3)
+    ctx.taitwater(f, drho, de)
+    ctx.heatconduction(de)
+    wf, wd, we = oracle_forces(s, ph, P, reverse=False)
+    assert rel_err(f - 0.25, wf) < TOL
+    assert rel_err(drho + 0.5, wd) < TOL
+    assert rel_err(de - 2.0, we) < TOL
+    # move the atoms (same set, ghosts too): update, rebuild the list, oracle on the moved set
+    x += 0.01 * np.sin(np.arange(x.size)).reshape(x.shape)
+    ctx.atoms_update(x, vest=vest, rho=rho, e=e)
+    ctx.build_list(sph_amd.SPH_LIST_HALF, cns, key=4)
+    f[:], drho[:], de[:] = 0.0, 0.0, 0.0
+    ctx.taitwater(f, drho, de)
+    g2 = copy.copy(g)
+    g2.x = x
+    foff, fnb = po.neigh_full(3, g2, s.ntypes, cns)
+    hoff, hnb = po.half_from_full(g2, foff, fnb)
+    assert np.array_equal(ctx.numneigh(n), np.diff(hoff).astype(np.int32))
+    wf2, wd2, _ = po.taitwater(3, g2, s.ntypes, 1, vest, rho, s.mass, ph.rho0, ph.c0, ph.visc,
+                               ph.tait_cut, hoff, hnb, morris=ph.morris,
+                               B=ph.c0 * ph.c0 * ph.rho0 / 7.0)
+    assert rel_err(f, wf2) < TOL
+    assert rel_err(drho, wd2) < TOL
+    ctx.host_arrays(0)
+    ctx.close()

@@ -144,3 +144,17 @@ def test_fix_phase_change_hip_vs_reference(S, name):
         for k in ("v", "vest", "e", "rmass", "rho", "cv"):
             assert rel_err(A[k][:nn], d[p + k]) < TOL, (name, c, k)
         assert rel_err(A["rmass"][:n0].sum(), d[p + "rmass"][:n0].sum()) < 1e-14
+
+
+@pytest.mark.parametrize("name", ["c2_n6", "c2_n7_h2.2", "c3_n6", "c2_2d_n14"])
+def test_single_phase_styles_device_lists(S, name):
+    """The same classes on the device-list path (the shim's default in LAMMPS):
+    the pair style is force->pair, its NeighList is NOT staged; the shim sizes cutneighsq
+    from cutsq + skin as Neighbor::init does and sph_hip_build_list builds full_bin's /
+    half_from_full_newton's lists on the device from the staged atoms.  Results against the
+    reference styles' own outputs at the same bar."""
+    S.ref_set_device_lists(1, 0.3)
+    try:
+        test_single_phase_styles(S, name)
+    finally:
+        S.ref_set_device_lists(0, 0.0)

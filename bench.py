@@ -472,6 +472,7 @@ def c2_pair_main(args, sph):
     cns[1, 1] = 3.3 * 3.3   # Neighbor::cutneighsq = (h + skin)^2
 
     xs, vs, rs, es = (np.ascontiguousarray(a, dtype=np.float64).copy() for a in (x, v, rho, e))
+    dl_parts = {}
 
     def lammps_step(k, device_lists):
         t0 = time.perf_counter()
@@ -489,17 +490,32 @@ def c2_pair_main(args, sph):
         # sph_hip_host_arrays), the whole atom set restaged at a rebuild, positions / vest /
         # rho / e between rebuilds (sph_hip_atoms_update), the lists built on the device at a
         # new key (sph_hip_build_list), rho written and f / drho / de added in place
-        if k % every == 0:
+        rb = k % every == 0
+        tt = [t0]
+
+        def lap():
+            tt.append(time.perf_counter())
+        if rb:
             ctx.atoms(N, 0, xs, t, vest=vs, rho=rs, e=es)
         else:
             ctx.atoms_update(xs, vest=vs, rho=rs, e=es)
+        lap()
         ctx.build_list(sph.SPH_LIST_FULL, cns, key)
+        lap()
         ctx.rhosum(rs)
         kms = ctx.last_kernel_ms()
+        lap()
         ctx.atoms_rho(rs)
+        lap()
         ctx.build_list(sph.SPH_LIST_HALF, cns, key)
+        lap()
         ctx.taitwater(f, drho, de)
-        return time.perf_counter() - t0, kms + ctx.last_kernel_ms()
+        lap()
+        part = dl_parts.setdefault("rebuild" if rb else "reuse", [0, [0.0] * 6])
+        part[0] += 1
+        for i in range(6):
+            part[1][i] += (tt[i + 1] - tt[i]) * 1e3
+        return tt[-1] - t0, kms + ctx.last_kernel_ms()
 
     for _ in range(args.warmup):
         step()
@@ -515,6 +531,9 @@ def c2_pair_main(args, sph):
     for dl in (False, True):
         if dl:
             ctx.host_arrays(N, x=xs, vest=vs, rho=rs, e=es, f=f, drho=drho, de=de)
+            for k in range(2):   # (untimed: first-use allocations of the device-list buffers)
+                lammps_step(2000 + k, dl)
+            dl_parts.clear()
         lw, lk = 0.0, 0.0
         for k in range(nls):
             w, km = lammps_step(k + (1000 if dl else 0), dl)
@@ -554,6 +573,11 @@ def c2_pair_main(args, sph):
                                "rebuild else sph_hip_atoms_update, sph_hip_build_list FULL / "
                                "HALF at each new key (no host list copy or upload), rho "
                                "written and f / drho / de added in place by the device",
+                       "wall_ms_by_call": {
+                           kind: dict(zip(("atoms", "build_full", "rhosum", "atoms_rho",
+                                           "build_half", "taitwater"),
+                                          [round(v / c, 4) for v in tot]), steps=c)
+                           for kind, (c, tot) in dl_parts.items()},
                        "steps": nls,
                        "wall_ms_per_step_incl_pcie": pattern[True][0] / nls * 1e3,
                        "kernel_ms_per_step": pattern[True][1] / nls,

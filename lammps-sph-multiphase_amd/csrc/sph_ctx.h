@@ -35,6 +35,7 @@ struct StagedList {
   int64_t key = -1;
   DBuf<int> ilist, off, nbr, rkey, rnbr, rown, roff;
   std::vector<int> hoff, hilist;
+  std::vector<double> cns;  // (a device-built list: the cutneighsq it was built with)
   bool rev_ok = false, devbuilt = false;
 };
 
@@ -95,6 +96,7 @@ struct sph_hip_ctx {
   // device-built lists (sph_hip_build_list, sph_pair_lists.hip): the active list was built
   // on the device; bins, bin-ordered copy, counts and the full list behind a half one
   bool list_devbuilt = false;
+  std::vector<double> list_cns;
   DBuf<double> lbox;
   DBuf<unsigned> bkey, bkey2;
   DBuf<int> bidx, bidx2, qbeg, tb, lcnt, loff, lnbr;
@@ -117,6 +119,7 @@ struct sph_hip_ctx {
     std::swap(hilist, p.hilist);
     std::swap(rev_ok, p.rev_ok);
     std::swap(list_devbuilt, p.devbuilt);
+    std::swap(list_cns, p.cns);
   }
   // make the kind-k list the active one: the active list is parked under its own kind,
   // the kind-k slot's list (if any) becomes active; a slot's stale buffers are kept for reuse

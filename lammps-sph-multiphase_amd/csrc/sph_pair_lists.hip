@@ -63,6 +63,44 @@ static __global__ void k_bbox_part(int n, const double4 *__restrict__ xf, double
   }
 }
 
+// Neighbor::half_from_full_newton (neigh_derive.cpp:83-150) over a full list, G lanes per
+// row: the row is read G entries at a time (coalesced), the kept entries keep their order
+// (ballot prefix within the lane group).  COUNT: hcnt[i] = kept; FILL: into hnbr from hoff[i]
+template <int G, bool FILL>
+__global__ __launch_bounds__(256) void k_half_rows(int nlocal, const int *__restrict__ off,
+                                                   const int *__restrict__ nbr,
+                                                   const double4 *__restrict__ xf,
+                                                   int *__restrict__ hcnt,
+                                                   const int *__restrict__ hoff,
+                                                   int *__restrict__ hnbr) {
+  static_assert(64 % G == 0, "lane groups tile the wave");
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t / G, lane = threadIdx.x % G;
+  const int gshift = (threadIdx.x & 63) & ~(G - 1);
+  const bool live = i < nlocal;
+  const int b = live ? off[i] : 0, e = live ? off[i + 1] : 0;
+  const double4 xi = live ? xf[i] : make_double4(0, 0, 0, 0);
+  int pos = FILL && live ? hoff[i] : 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  // every lane of the wave runs the longest row's trip count (the ballot is wave-wide)
+  int len = e - b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) len = max(len, __shfl_xor(len, d, 64));
+  for (int k0 = 0; k0 < len; k0 += G) {
+    const int k = b + k0 + lane;
+    bool keep = false;
+    int j = 0;
+    if (k < e) {
+      j = nbr[k];
+      keep = half_keep(i, j, nlocal, xi, xf[j]);
+    }
+    const unsigned long long m = (__ballot(keep) >> gshift) & ((G == 64) ? ~0ull : ((1ull << G) - 1));
+    if (FILL && keep) hnbr[pos + __popcll(m & below)] = j;
+    pos += __popcll(m);
+  }
+  if (!FILL && live && lane == 0) hcnt[i] = pos;
+}
+
 static __global__ void k_iota(int n, int *__restrict__ a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) a[i] = i;
@@ -82,6 +120,30 @@ long long scan_counts(sph_hip_ctx *c, const int *cnt, int n, DBuf<int> &off) {
   SPH_HIP_TRY(hipStreamSynchronize(c->stream));
   return tot;
 }
+// identity ilist, and the row offsets on the host too (the reverse half list and fix
+// phase_change read them)
+void finish_list(sph_hip_ctx *c, int nlocal) {
+  hipLaunchKernelGGL(k_iota, dim3((nlocal + 255) / 256), dim3(256), 0, c->stream, nlocal,
+                     c->ilist.p);
+  SPH_HIP_TRY(hipMemcpyAsync(c->hoff.data(), c->off.p, (nlocal + 1) * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  SPH_HIP_TRY(hipStreamSynchronize(c->stream));
+  SPH_HIP_TRY(hipGetLastError());
+}
+
+// the active list := Neighbor::half_from_full_newton of the full list (foff, fnbr)
+void derive_half(sph_hip_ctx *c, int nlocal, const int *foff, const int *fnbr) {
+  constexpr int G = 16;
+  const dim3 grid(grid_for_rows(nlocal, G)), block(256);
+  c->lcnt.reserve(nlocal + 1);
+  hipLaunchKernelGGL((k_half_rows<G, false>), grid, block, 0, c->stream, nlocal, foff, fnbr,
+                     (const double4 *)c->xf.p, c->lcnt.p, (const int *)nullptr, (int *)nullptr);
+  const long long tot = scan_counts(c, c->lcnt.p, nlocal, c->off);
+  c->nbr.reserve(tot > 0 ? tot : 1);
+  if (tot)
+    hipLaunchKernelGGL((k_half_rows<G, true>), grid, block, 0, c->stream, nlocal, foff, fnbr,
+                       (const double4 *)c->xf.p, (int *)nullptr, (const int *)c->off.p, c->nbr.p);
+  finish_list(c, nlocal);
+}
 }  // namespace
 
 extern "C" {
@@ -96,12 +158,21 @@ int sph_hip_build_list(sph_hip_ctx *c, int kind, int64_t key, const double *cutn
   const int nlocal = c->nlocal, nall = c->nlocal + c->nghost;
   // a build of this key is already the staged list of this kind (hybrid/overlay sub-styles
   // of one kind share it; the fix's full list is a copy of the pair's)
-  if (key >= 0 && c->list_key == key && c->inum == nlocal && c->list_devbuilt) return SPH_HIP_OK;
-  c->list_key = -1;
-  c->list_devbuilt = false;
-  // Neighbor::cutneighsq of the run (neighbor.cpp:261-268), into the coefficient block
   const int nt = c->ntypes, n1 = nt + 1;
   SPH_REQUIRE(n1 * n1 <= NT2, SPH_HIP_EINVAL, "sph_hip_build_list: %d types", nt);
+  const std::vector<double> cns(cutneighsq, cutneighsq + n1 * n1);
+  if (key >= 0 && c->list_key == key && c->inum == nlocal && c->list_devbuilt &&
+      c->list_cns == cns)
+    return SPH_HIP_OK;
+  c->list_key = -1;
+  c->list_devbuilt = false;
+  // a half list of the key whose full list is parked (built a moment ago for rhosum /
+  // colorgradient, as LAMMPS derives both from one build): derived from it, no new binning
+  StagedList &pf = c->parked[SPH_LIST_FULL];
+  const bool from_parked = kind == SPH_LIST_HALF && key >= 0 && pf.kind == SPH_LIST_FULL &&
+                           pf.key == key && pf.devbuilt && pf.inum == nlocal && pf.cns == cns &&
+                           nlocal > 0;
+  // Neighbor::cutneighsq of the run (neighbor.cpp:261-268), into the coefficient block
   double cmaxsq = 0.0;
   for (int i = 0; i <= nt; i++)
     for (int j = 0; j <= nt; j++) {
@@ -120,6 +191,16 @@ int sph_hip_build_list(sph_hip_ctx *c, int kind, int64_t key, const double *cutn
   c->hoff.assign(nlocal + 1, 0);
   c->hilist.resize(nlocal);
   for (int i = 0; i < nlocal; i++) c->hilist[i] = i;
+  if (from_parked) {
+    derive_half(c, nlocal, pf.off.p, pf.nbr.p);
+    c->list_kind = kind;
+    c->inum = nlocal;
+    c->rev_ok = false;
+    c->list_key = key;
+    c->list_devbuilt = true;
+    c->list_cns = cns;
+    return SPH_HIP_OK;
+  }
   if (nlocal == 0 || nall == 0) {
     SPH_HIP_TRY(hipMemsetAsync(c->off.p, 0, sizeof(int), c->stream));
     SPH_HIP_TRY(hipStreamSynchronize(c->stream));
@@ -128,6 +209,7 @@ int sph_hip_build_list(sph_hip_ctx *c, int kind, int64_t key, const double *cutn
     c->rev_ok = false;
     c->list_key = key;
     c->list_devbuilt = true;
+    c->list_cns = cns;
     return SPH_HIP_OK;
   }
   const double cm = std::sqrt(cmaxsq);
@@ -212,33 +294,19 @@ int sph_hip_build_list(sph_hip_ctx *c, int kind, int64_t key, const double *cutn
     else SPH_N3L(true, false, (const int *)foff.p, fnbr.p);
   }
 #undef SPH_N3L
-  long long tot = ftot;
   if (kind == SPH_LIST_FULL) {
     std::swap(c->off, foff);
     std::swap(c->nbr, fnbr);
-  } else {  // Neighbor::half_from_full_newton (neigh_derive.cpp:124-131)
-    const unsigned g1 = (unsigned)((nlocal + 255) / 256);
-    hipLaunchKernelGGL(k_half_from_full<false>, dim3(g1), dim3(256), 0, c->stream, nlocal,
-                       (const int *)foff.p, (const int *)fnbr.p, (const double4 *)c->xf.p,
-                       c->lcnt.p, (const int *)nullptr, (int *)nullptr);
-    tot = scan_counts(c, c->lcnt.p, nlocal, c->off);
-    c->nbr.reserve(tot > 0 ? tot : 1);
-    if (tot)
-      hipLaunchKernelGGL(k_half_from_full<true>, dim3(g1), dim3(256), 0, c->stream, nlocal,
-                         (const int *)foff.p, (const int *)fnbr.p, (const double4 *)c->xf.p,
-                         (int *)nullptr, (const int *)c->off.p, c->nbr.p);
+    finish_list(c, nlocal);
+  } else {
+    derive_half(c, nlocal, foff.p, fnbr.p);
   }
-  hipLaunchKernelGGL(k_iota, dim3((nlocal + 255) / 256), dim3(256), 0, c->stream, nlocal,
-                     c->ilist.p);
-  // the row offsets on the host too (the reverse half list and fix phase_change read them)
-  SPH_HIP_TRY(hipMemcpyAsync(c->hoff.data(), c->off.p, (nlocal + 1) * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  SPH_HIP_TRY(hipStreamSynchronize(c->stream));
-  SPH_HIP_TRY(hipGetLastError());
   c->list_kind = kind;
   c->inum = nlocal;
   c->rev_ok = false;
   c->list_key = key;
   c->list_devbuilt = true;
+  c->list_cns = cns;
   SPH_API_END
 }
 

@@ -913,6 +913,55 @@ __device__ __forceinline__ void blk_walk2(BlkSlots<G, U, NCH> &sw, int c, int la
     sw.walk(c, lane, [&](int q, bool) { body(load(q)); });
   }
 }
+// walk3 (SPH_BLK_WALK = 1, NCH > 0): the same slots as one flat sequence of steps (step s:
+// chunk s / U, position s % U), walked to the WAVE's longest row with scalar branches -- a
+// shorter row's extra steps read its padding (the sentinel slot, whose terms are exactly 0),
+// which costs nothing: a masked lane's issue slot is spent anyway -- and software-pipelined:
+// the records of steps s + 1 and s + 2 are read from LDS before step s is evaluated, so each
+// record's LDS latency is covered by two pair evaluations of the same wave (the LDS image
+// caps the pass at 4 waves per SIMD, which leaves the VGPRs for that).
+#ifndef SPH_BLK_WALK
+#define SPH_BLK_WALK 1
+#endif
+template <class F, int... I>
+__device__ __forceinline__ void blk_steps_(F &&f, std::integer_sequence<int, I...>) {
+  (void)(f(std::integral_constant<int, I>{}) && ...);
+}
+template <int G>
+__device__ __forceinline__ int wave_max_count(int c) {
+#pragma unroll
+  for (int d = G; d < 64; d <<= 1) c = max(c, __shfl_xor(c, d, 64));
+  return __builtin_amdgcn_readfirstlane(c);
+}
+template <int G, int U, int NCH, class Load, class Body>
+__device__ __forceinline__ void blk_walk3(BlkSlots<G, U, NCH> &sw, int cmax, Load load,
+                                          Body body) {
+  static_assert(NCH > 0, "walk3: rows held in registers");
+  constexpr int NS = NCH * U;
+  if (cmax <= 0) return;
+  typedef decltype(load(0)) Rec;
+  // (the reads ahead are unconditional: past a row's count its slot words hold the sentinel
+  // slot 0, a valid record)
+  Rec r0 = load(SlotWord<U>::get(sw.w[0], 0));
+  Rec r1 = load(SlotWord<U>::get(sw.w[1 / U], 1 % U));
+  // steps unrolled at compile time (the slot words stay in registers), left at the first
+  // step past the wave's longest row
+  auto step = [&](auto sc) -> bool {
+    constexpr int s = decltype(sc)::value;
+    if (s * G >= cmax) return false;  // (wave-uniform)
+    Rec r2{};
+    if constexpr (s + 2 < NS) r2 = load(SlotWord<U>::get(sw.w[(s + 2) / U], (s + 2) % U));
+    // (keeps the reads ahead of the evaluation: the scheduler would sink them to their use,
+    // tuning for an occupancy the LDS image does not allow)
+    __builtin_amdgcn_sched_barrier(0);
+    body(r0);
+    r0 = r1;
+    r1 = r2;
+    return true;
+  };
+  blk_steps_(step, std::make_integer_sequence<int, NS>{});
+}
+
 // a neighbour's record in the force pass's image (blk_put layout)
 struct BlkRec {
   double2 a0, a1, a2, a3;
@@ -1002,10 +1051,19 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   __syncthreads();
   const RhoPair c1 = NT1 ? cf->rho[3] : RhoPair{};
   double acc = 0.0;
-  sw.walk(c, lane, [&](int q, bool) {
+  struct RhoRec {
+    double2 xy;
+    double z;
+    int q;
+  };
+  auto load = [&](int q) {
     const int sj = blk_s<CQ>(q);
-    const double2 xy = s_xy[sj];
-    const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
+    return RhoRec{s_xy[sj], s_z[sj], q};
+  };
+  auto pair = [&](const RhoRec &rc) {
+    const int q = rc.q, sj = blk_s<CQ>(q);
+    const double2 xy = rc.xy;
+    const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - rc.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
     const RhoPair cc = NT1 ? c1 : s_c[it * nt1 + s_t[sj]];
     double wf = fmax(fma(-rsq, cc.ihsq, 1.0), 0.0);
@@ -1014,7 +1072,15 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
     acc = NT1 ? acc + wf : fma(cc.mK, wf, acc);
     if (q > 0 && q <= qn3)  // a later row of this block: its share (cut and weight symmetric)
       atomicAdd(&s_acc[sj - 1], NT1 ? wf : s_c[s_t[sj] * nt1 + it].mK * wf);
-  });
+  };
+  if constexpr (NCH > 0 && SPH_BLK_WALK == 1) {
+    if (!n3on)
+      blk_walk3(sw, wave_max_count<G>(c), load, pair);
+    else
+      sw.walk(c, lane, [&](int q, bool) { pair(load(q)); });
+  } else {
+    sw.walk(c, lane, [&](int q, bool) { pair(load(q)); });
+  }
   acc = group_sum<G>(acc);
   if (n3on) {  // (workgroup-uniform) the earlier rows' shares of this row
     __syncthreads();
@@ -1236,7 +1302,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     r.e = HEAT ? *reinterpret_cast<const double *>(rec + 1024) : 0.0;
     return r;
   };
-  blk_walk2(sw, c, lane, load, [&](const BlkRec &rc) {
+  auto pair = [&](const BlkRec &rc) {
     const int q = rc.q;
     const double2 a0 = rc.a0, a1 = rc.a1, a2 = rc.a2, a3 = rc.a3;
     if (EXP == 2) {
@@ -1304,7 +1370,15 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       }
       if (HEAT) atomicAdd(a + 5, -tEH);
     }
-  });
+  };
+  if constexpr (NCH > 0 && SPH_BLK_WALK == 1) {
+    if (!n3on)
+      blk_walk3(sw, wave_max_count<G>(c), load, pair);
+    else
+      blk_walk2(sw, c, lane, load, pair);
+  } else {
+    blk_walk2(sw, c, lane, load, pair);
+  }
   if (TAIT) {
     fx = group_sum<G>(fx);
     fy = group_sum<G>(fy);

@@ -923,6 +923,9 @@ __device__ __forceinline__ void blk_walk2(BlkSlots<G, U, NCH> &sw, int c, int la
 #ifndef SPH_BLK_WALK
 #define SPH_BLK_WALK 1
 #endif
+#ifndef SPH_BLK_PF
+#define SPH_BLK_PF 2  // (records read ahead)
+#endif
 template <class F, int... I>
 __device__ __forceinline__ void blk_steps_(F &&f, std::integer_sequence<int, I...>) {
   (void)(f(std::integral_constant<int, I>{}) && ...);
@@ -940,23 +943,27 @@ __device__ __forceinline__ void blk_walk3(BlkSlots<G, U, NCH> &sw, int cmax, Loa
   constexpr int NS = NCH * U;
   if (cmax <= 0) return;
   typedef decltype(load(0)) Rec;
+  // a ring of PF + 1 records: step s evaluates r[s % (PF + 1)] after reading step s + PF's
   // (the reads ahead are unconditional: past a row's count its slot words hold the sentinel
   // slot 0, a valid record)
-  Rec r0 = load(SlotWord<U>::get(sw.w[0], 0));
-  Rec r1 = load(SlotWord<U>::get(sw.w[1 / U], 1 % U));
+  constexpr int PF = SPH_BLK_PF, NR = PF + 1;
+  Rec r[NR];
+  blk_steps_([&](auto sc) -> bool {
+    constexpr int s = decltype(sc)::value;
+    if constexpr (s < PF && s < NS) r[s] = load(SlotWord<U>::get(sw.w[s / U], s % U));
+    return true;
+  }, std::make_integer_sequence<int, PF>{});
   // steps unrolled at compile time (the slot words stay in registers), left at the first
   // step past the wave's longest row
   auto step = [&](auto sc) -> bool {
     constexpr int s = decltype(sc)::value;
     if (s * G >= cmax) return false;  // (wave-uniform)
-    Rec r2{};
-    if constexpr (s + 2 < NS) r2 = load(SlotWord<U>::get(sw.w[(s + 2) / U], (s + 2) % U));
+    if constexpr (s + PF < NS)
+      r[(s + PF) % NR] = load(SlotWord<U>::get(sw.w[(s + PF) / U], (s + PF) % U));
     // (keeps the reads ahead of the evaluation: the scheduler would sink them to their use,
     // tuning for an occupancy the LDS image does not allow)
     __builtin_amdgcn_sched_barrier(0);
-    body(r0);
-    r0 = r1;
-    r1 = r2;
+    body(r[s % NR]);
     return true;
   };
   blk_steps_(step, std::make_integer_sequence<int, NS>{});

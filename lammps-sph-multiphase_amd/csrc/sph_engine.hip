@@ -1841,10 +1841,14 @@ struct sph_engine {
     h.pF = recF.p;
     h.pS = recS.p;
     const int sel = (mpc.tait_on ? 1 : 0) | (mpc.st_on ? 2 : 0) | (mpc.heat_on ? 4 : 0);
+    const bool g1 = mp2_gamma1(hm);
     switch (sel) {
 #define SPH_MPG(k, T, S, H)                                                                   \
   case k:                                                                                     \
-    if (sym) hipLaunchKernelGGL((k_mp2_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);  \
+    if (sym && g1)                                                                            \
+      hipLaunchKernelGGL((k_mp2_gather<8, T, S, H, false>), mp_rows(n), dim3(256), 0, s, h);  \
+    else if (sym)                                                                             \
+      hipLaunchKernelGGL((k_mp2_gather<8, T, S, H, true>), mp_rows(n), dim3(256), 0, s, h);   \
     else hipLaunchKernelGGL((k_mp_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);       \
     break;
       SPH_MPG(1, true, false, false)

@@ -256,7 +256,9 @@ __device__ __forceinline__ double3 mp2_svec(int dim, const double4 &w, double3 e
 // pair terms themselves with i first.
 // (108 VGPRs, 4 waves per SIMD: asking for 5 or 6 spills -- 32 / 40 ms per C5 step instead
 // of 12.8, profiles/r03/README.md)
-template <int G, bool TAIT, bool SURF, bool HEAT>
+// POW = false: every gamma is 1 (bubble.lmp), the pressures are linear in rho and the pow()
+// code (and its registers) is not instantiated.
+template <int G, bool TAIT, bool SURF, bool HEAT, bool POW = true>
 __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
@@ -329,10 +331,12 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
       const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
       if (ct) {  // pair_sph_taitwater_multiphase.cpp:128-170
         const Mp2Type tyj = s_t[tjs[u]];
-        const double pI = tyi.B * ((tyi.gamma == 1.0 ? rhoi * tyi.rho0i
-                                                      : pow(rhoi * tyi.rho0i, tyi.gamma)) - tyi.rbg);
-        const double pJ = tyj.B * ((tyi.gamma == 1.0 ? rhoj * tyj.rho0i
-                                                      : pow(rhoj * tyj.rho0i, tyi.gamma)) - tyj.rbg);
+        const double pI = tyi.B * ((!POW || tyi.gamma == 1.0 ? rhoi * tyi.rho0i
+                                                              : pow(rhoi * tyi.rho0i, tyi.gamma)) -
+                                   tyi.rbg);
+        const double pJ = tyj.B * ((!POW || tyi.gamma == 1.0 ? rhoj * tyj.rho0i
+                                                              : pow(rhoj * tyj.rho0i, tyi.gamma)) -
+                                   tyj.rbg);
         const double pij = (rhoj * pI + rhoi * pJ) * mp_rcp(rhoi + rhoj);
         const double wfd = qt * ir, V2 = Vi2 + Vj2;
         const double fvisc = V2 * q.tvisc * wfd, fpair = -V2 * pij * wfd;
@@ -367,6 +371,11 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
 
 // the styles are symmetric under exchanging a pair's atoms (k_mp2_gather applies): every
 // gamma equal, and no type pinned to Tc against its own type
+inline bool mp2_gamma1(const MpCoefs &c) {
+  for (int t = 1; t <= c.ntypes; t++)
+    if (c.gamma[t] != 1.0) return false;
+  return true;
+}
 inline bool mp2_symmetric(const MpCoefs &c) {
   const int nt1 = c.ntypes + 1;
   for (int t = 2; t <= c.ntypes; t++)

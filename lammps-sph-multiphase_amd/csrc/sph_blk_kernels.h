@@ -468,7 +468,8 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             const Coefs *__restrict__ cf, int ucap, int sstride, int *__restrict__ ulist,
             int *__restrict__ ucnt, int *__restrict__ rcnt, unsigned short *__restrict__ snbr,
             int *__restrict__ icnt, unsigned short *__restrict__ snbi,
-            int *__restrict__ ovf, int *__restrict__ umax, int cq, int *__restrict__ fcnt) {
+            int *__restrict__ ovf, int *__restrict__ umax, int cq, int *__restrict__ fcnt,
+            unsigned char *__restrict__ bperm) {
   constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
   constexpr int RPW = R / NW, UG = U * G, WS = INNER ? 2 : 1;
   static_assert(R <= 64 && R % 32 == 0, "one lane per row, rows in steps of 8 per wave");
@@ -492,6 +493,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   __shared__ double s_bb[6];
   __shared__ double s_cns[NT1 ? 1 : NT2], s_cin[(NT1 || !INNER) ? 1 : NT2];
   __shared__ int s_sc[NW];
+  __shared__ int s_len[R];  // (bperm: the rows' walked lengths)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, 
             wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // (wave-uniform: scalar)
   const int row0 = b * R;
@@ -819,12 +821,34 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     if (live && part == 0) {
       cnt_out[row0 + r] = cnt;
       over |= cnt > sstride;
+      if (sel == WS - 1) s_len[r] = cnt;
     }
   };
   if (N3 && live && part == 0) fcnt[row0 + r] = s_fc[r];
+  if (bperm && tid < R) s_len[tid] = -1;
+  __syncthreads();
   emit(0, snbr, rcnt);
   if (INNER) emit(1, snbi, icnt);
   if (over) atomicMax(ovf, 1 << 21);
+  if (bperm) {
+    // the pair passes' row order inside the block: longest walked row (inner if built) first,
+    // so that a wave's rows -- walked to the longest of them -- have similar lengths
+    __syncthreads();
+    if (tid < R) {
+      const int my = s_len[tid];
+      int rank = 0;
+      for (int k = 0; k < R; k++) {
+        const int o = s_len[k];
+        rank += (o > my || (o == my && k < tid)) ? 1 : 0;
+      }
+      bperm[row0 + rank] = (unsigned char)tid;
+    }
+  }
+}
+
+// the block's lr-th walked row: the build's length order (bperm, k_blk_build) or in place
+__device__ __forceinline__ int blk_row(const unsigned char *bperm, int base, int lr) {
+  return bperm ? (int)bperm[base + lr] : lr;
 }
 
 // A lane's slot words: U = 2 slots in one 4-byte word, U = 4 in one 8-byte pair.
@@ -923,8 +947,8 @@ __device__ __forceinline__ void blk_walk2(BlkSlots<G, U, NCH> &sw, int c, int la
 #ifndef SPH_BLK_WALK
 #define SPH_BLK_WALK 1
 #endif
-#ifndef SPH_BLK_PF
-#define SPH_BLK_PF 2  // (records read ahead)
+#ifndef SPH_BLK_ILP
+#define SPH_BLK_ILP 1  // (pair evaluations per scheduling group; 2: 0.288 vs 0.282 ms, 3: 0.375)
 #endif
 template <class F, int... I>
 __device__ __forceinline__ void blk_steps_(F &&f, std::integer_sequence<int, I...>) {
@@ -943,30 +967,39 @@ __device__ __forceinline__ void blk_walk3(BlkSlots<G, U, NCH> &sw, int cmax, Loa
   constexpr int NS = NCH * U;
   if (cmax <= 0) return;
   typedef decltype(load(0)) Rec;
-  // a ring of PF + 1 records: step s evaluates r[s % (PF + 1)] after reading step s + PF's
-  // (the reads ahead are unconditional: past a row's count its slot words hold the sentinel
-  // slot 0, a valid record)
-  constexpr int PF = SPH_BLK_PF, NR = PF + 1;
-  Rec r[NR];
+  // ILP steps form a group: the group's pair evaluations share one basic block (the scheduler
+  // interleaves their dependency chains); the records of the next group are read before it.
+  // A group runs whole once its first step is inside the wave's longest row (its later
+  // steps may read only padding: exactly-zero terms).  The reads ahead are unconditional:
+  // past a row's count its slot words hold the sentinel slot 0, a valid record.
+  constexpr int IL = SPH_BLK_ILP, NG = (NS + IL - 1) / IL;
+  Rec r[2 * IL];
   blk_steps_([&](auto sc) -> bool {
     constexpr int s = decltype(sc)::value;
-    if constexpr (s < PF && s < NS) r[s] = load(SlotWord<U>::get(sw.w[s / U], s % U));
+    if constexpr (s < NS) r[s] = load(SlotWord<U>::get(sw.w[s / U], s % U));
     return true;
-  }, std::make_integer_sequence<int, PF>{});
-  // steps unrolled at compile time (the slot words stay in registers), left at the first
-  // step past the wave's longest row
-  auto step = [&](auto sc) -> bool {
-    constexpr int s = decltype(sc)::value;
-    if (s * G >= cmax) return false;  // (wave-uniform)
-    if constexpr (s + PF < NS)
-      r[(s + PF) % NR] = load(SlotWord<U>::get(sw.w[(s + PF) / U], (s + PF) % U));
-    // (keeps the reads ahead of the evaluation: the scheduler would sink them to their use,
-    // tuning for an occupancy the LDS image does not allow)
+  }, std::make_integer_sequence<int, IL>{});
+  // groups unrolled at compile time (the slot words stay in registers), left at the first
+  // group past the wave's longest row
+  auto group = [&](auto gc) -> bool {
+    constexpr int g = decltype(gc)::value;
+    if (g * IL * G >= cmax) return false;  // (wave-uniform)
+    blk_steps_([&](auto sc) -> bool {
+      constexpr int s = (g + 1) * IL + decltype(sc)::value;
+      if constexpr (s < NS) r[s % (2 * IL)] = load(SlotWord<U>::get(sw.w[s / U], s % U));
+      return true;
+    }, std::make_integer_sequence<int, IL>{});
+    // (keeps the reads ahead of the evaluations: the scheduler would sink them to their
+    // use, tuning for an occupancy the LDS image does not allow)
     __builtin_amdgcn_sched_barrier(0);
-    body(r[s % NR]);
+    blk_steps_([&](auto sc) -> bool {
+      constexpr int s = g * IL + decltype(sc)::value;
+      if constexpr (s < NS) body(r[s % (2 * IL)]);
+      return true;
+    }, std::make_integer_sequence<int, IL>{});
     return true;
   };
-  blk_steps_(step, std::make_integer_sequence<int, NS>{});
+  blk_steps_(group, std::make_integer_sequence<int, NG>{});
 }
 
 // a neighbour's record in the force pass's image (blk_put layout)
@@ -991,7 +1024,8 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
              const int *__restrict__ rcnt, double4 *__restrict__ xf,
              const int *__restrict__ ty, double4 *__restrict__ vr,
              const Coefs *__restrict__ cf, int um, const unsigned short *__restrict__ snbi,
-             const int *__restrict__ icnt, const int *__restrict__ moved, int n3) {
+             const int *__restrict__ icnt, const int *__restrict__ moved, int n3,
+             const unsigned char *__restrict__ bperm) {
   constexpr int NTH = R * G;
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
@@ -1002,7 +1036,8 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   __shared__ double s_acc[R];  // n3: the later rows' shares (k_blk_build N3)
   const int nt1 = cf->ntypes + 1;
   const int b = (int)xcd_block(), tid = threadIdx.x;
-  const int row = b * R + tid / G, lane = tid & (G - 1);
+  // (bperm: the block's rows in the build's length order, blk_row)
+  const int row = b * R + blk_row(bperm, b * R, tid / G), lane = tid & (G - 1);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
   // n3: slots 1 .. nrow are the block's rows (q <= qn3); a row's entries among them are the
@@ -1204,7 +1239,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
             double gz, int um, const int *__restrict__ blist, int cq,
             const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,
-            const int *__restrict__ moved, int n3) {
+            const int *__restrict__ moved, int n3, const unsigned char *__restrict__ bperm) {
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
     rcnt = icnt;
@@ -1230,7 +1265,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   const int qn3 = n3on ? blk_q(min(R, n - b * R), CQ) : -1;
   if (n3on)
     for (int t = tid; t < R * NA; t += NTH) s_acc[t] = 0.0;
-  const int row = b * R + tid / G, lane = tid & (G - 1);
+  const int row = b * R + blk_row(bperm, b * R, tid / G), lane = tid & (G - 1);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
   // loads first: the row's count, the union's atom ids, then the row's slots and the
@@ -1488,6 +1523,7 @@ struct BlkArgs {
   const unsigned short *snbi = nullptr;
   const int *icnt = nullptr, *moved = nullptr;
   bool n3 = false;      // rows built with Newton-3 inside the blocks (k_blk_build N3)
+  const unsigned char *bperm = nullptr;  // the passes' row order per block (k_blk_build)
   bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
 };
 
@@ -1535,7 +1571,7 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
                         const int *ty, const double4 *xb, const int *tb, const int *qbeg,
                         const Coefs *cf, int ucap, int sstride, int *ulist, int *ucnt,
                         int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
-                        int *ovf, int *umax, int cq, int bexp, int *fcnt) {
+                        int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm) {
 #ifdef SPH_STUDY
   auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, N3, 1>
           : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, N3, 2>
@@ -1548,30 +1584,30 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
 #endif
   hipLaunchKernelGGL(fn, dim3(blk_blocks(n, R)), dim3(256), 0, s, n, q, dim, xf, ty, xb, tb,
                      qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                     fcnt);
+                     fcnt, bperm);
 }
 template <int R, int G, int U, bool N3>
 inline void blk_build_n(bool nt1, bool inner, hipStream_t s, int n, const QBins &q, int dim,
                         const double4 *xf, const int *ty, const double4 *xb, const int *tb,
                         const int *qbeg, const Coefs *cf, int ucap, int sstride, int *ulist,
                         int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
-                        unsigned short *snbi, int *ovf, int *umax, int cq, int bexp, int *fcnt) {
+                        unsigned short *snbi, int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm) {
   if (nt1 && inner)
     blk_build_t<R, G, U, true, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                          ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp,
-                                         fcnt);
+                                         fcnt, bperm);
   else if (nt1)
     blk_build_t<R, G, U, true, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                           ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                                          bexp, fcnt);
+                                          bexp, fcnt, bperm);
   else if (inner)
     blk_build_t<R, G, U, false, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                           ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                                          bexp, fcnt);
+                                          bexp, fcnt, bperm);
   else
     blk_build_t<R, G, U, false, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,
                                            sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf,
-                                           umax, cq, bexp, fcnt);
+                                           umax, cq, bexp, fcnt, bperm);
 }
 // n3: Newton-3 inside the blocks (rows first in the union, the later rows' share; fcnt gets
 // the full counts)
@@ -1580,13 +1616,13 @@ inline void blk_build(int shape, bool nt1, bool inner, bool n3, hipStream_t s, i
                       const double4 *xb, const int *tb, const int *qbeg, const Coefs *cf,
                       int ucap, int sstride, int *ulist, int *ucnt, int *rcnt,
                       unsigned short *snbr, int *icnt, unsigned short *snbi, int *ovf, int *umax,
-                      int cq, int bexp, int *fcnt) {
+                      int cq, int bexp, int *fcnt, unsigned char *bperm) {
 #ifdef SPH_STUDY
 #define SPH_IF_N3(R, G, U)                                                                  \
   if (n3)                                                                                 \
     blk_build_n<R, G, U, true>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,    \
                                sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
-                               bexp, fcnt);                                                \
+                               bexp, fcnt, bperm);                                                \
   else
 #else
 #define SPH_IF_N3(R, G, U) (void)n3;
@@ -1597,7 +1633,7 @@ inline void blk_build(int shape, bool nt1, bool inner, bool n3, hipStream_t s, i
     SPH_IF_N3(R, G, U)                                                                    \
     blk_build_n<R, G, U, false>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,   \
                                 sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
-                                bexp, fcnt);                                               \
+                                bexp, fcnt, bperm);                                               \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE
@@ -1615,7 +1651,7 @@ inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int
                                   (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um, k.snbi, k.icnt,
-                     k.moved, k.n3 ? 1 : 0);
+                     k.moved, k.n3 ? 1 : 0, k.bperm);
 }
 template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
@@ -1652,12 +1688,12 @@ inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
                      a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq, k.snbi,
-                     k.icnt, k.moved, k.n3 ? 1 : 0);
+                     k.icnt, k.moved, k.n3 ? 1 : 0, k.bperm);
   if (k.nbig > 0)
     hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
                        k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
                        a.gx, a.gy, a.gz, k.um, k.blist, k.cq, k.snbi, k.icnt, k.moved,
-                       k.n3 ? 1 : 0);
+                       k.n3 ? 1 : 0, k.bperm);
 }
 
 // the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum

@@ -130,6 +130,15 @@ static bool mp_typed_env() {
 }
 // SPH_N3 (study builds only; default 0): the block build keeps each pair of rows of one
 // block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
+// SPH_ROWSORT (study builds; default 0): the pair passes walk each block's rows longest
+// first (k_blk_build's per-block order), so that a wave's rows have similar lengths
+static bool rowsort() {
+#ifndef SPH_ROWSORT_DEFAULT
+#define SPH_ROWSORT_DEFAULT 0  // (on: force 0.291 vs 0.287 ms, rhosum 0.123 vs 0.111, profiles/r04/rowsort)
+#endif
+  static bool v = study_int("SPH_ROWSORT", SPH_ROWSORT_DEFAULT) != 0;
+  return v;
+}
 static bool n3_env() {
   static bool v = BLK_N3_BUILT && study_int("SPH_N3", 0) != 0;
   return v;
@@ -285,6 +294,13 @@ struct sph_engine {
   // owned positions they were written at and the flag that retires them (sc.x0 / sc.moved)
   DBuf<unsigned short> snbi;
   DBuf<int> icnt, moved;
+  // the pair passes' row order inside each block (longest row first, k_blk_build)
+  DBuf<unsigned char> bperm;
+  bool blk_perm = false;
+  unsigned char *bperm_buf(int nb, int R) {
+    bperm.reserve((size_t)nb * R);
+    return bperm.p;
+  }
   DBuf<double4> x0;
   double inner_margin = 0.0;
   bool inner = false, inner_written = false;  // (written: by k_blk_build, with the full rows)
@@ -1352,12 +1368,13 @@ struct sph_engine {
         blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
                   qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
                   blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
-                  study_int("SPH_BEXP", 0), ccnt.p);
+                  study_int("SPH_BEXP", 0), ccnt.p, rowsort() ? bperm_buf(nb, sh.R) : nullptr);
       else
         blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
                   blk_cq(), study_int("SPH_BEXP", 0));
       inner_written = v2 && want_inner;
+      blk_perm = v2 && !blk_n3 && rowsort();
       // the force pass's image size and its large-union blocks, then ONE read-back
       bl.reserve(nb);
       hipLaunchKernelGGL(k_blk_large_dev, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p,
@@ -1409,6 +1426,7 @@ struct sph_engine {
     k.ucnt = ucnt.p;
     k.rcnt = blk_n3 ? pcnt.p : ccnt.p;
     k.n3 = blk_n3;
+    k.bperm = blk_perm ? bperm.p : nullptr;
     k.snbr = snbr.p;
     if (inner) {
       k.snbi = snbi.p;

@@ -31,6 +31,12 @@ namespace sph {
 #ifndef SPH_MP2_NU
 #define SPH_MP2_NU 2
 #endif
+// ... in the fused gather: one (its three records per entry; 128 VGPRs = 4 waves per SIMD
+// with gamma = 1, against 156 = 3 waves with two: 4.36 vs 4.53 ms per C5 step,
+// profiles/r04/c5)
+#ifndef SPH_MP2_GNU
+#define SPH_MP2_GNU 1
+#endif
 
 // quintic W(s) and dW/ds without the norm (s = 3 r / h)
 __device__ __forceinline__ double q5_w(double s) {
@@ -276,7 +282,7 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   const double4 cFi = a.pF[i], cSi = a.pS[i];
   const double irFi = mp_rcp(cFi.w), irSi = mp_rcp(cSi.w);
   double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
-  constexpr int NU = SPH_MP2_NU;
+  constexpr int NU = SPH_MP2_GNU;
   const MpRow rw(a.off, a.cnt, a.stride, row);
   const long long kend = rw.end;
   // the next round's entries are read while this round computes (the rows stream from HBM:

@@ -128,8 +128,6 @@ static bool mp_typed_env() {
   static bool v = study_int("SPH_MP_TYPED", 1) != 0;
   return v;
 }
-// SPH_N3 (study builds only; default 0): the block build keeps each pair of rows of one
-// block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
 // SPH_ROWSORT (study builds; default 0): the pair passes walk each block's rows longest
 // first (k_blk_build's per-block order), so that a wave's rows have similar lengths
 static bool rowsort() {
@@ -139,6 +137,8 @@ static bool rowsort() {
   static bool v = study_int("SPH_ROWSORT", SPH_ROWSORT_DEFAULT) != 0;
   return v;
 }
+// SPH_N3 (study builds only; default 0): the block build keeps each pair of rows of one
+// block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
 static bool n3_env() {
   static bool v = BLK_N3_BUILT && study_int("SPH_N3", 0) != 0;
   return v;

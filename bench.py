@@ -931,7 +931,7 @@ def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
                                    "with every class timed"},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = c5_cpu_baseline(args.c5_cpu_n)
+        out["cpu_baseline"] = c5_cpu_baseline(args.c5_cpu_n, steps=1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     with stdout_to_stderr():
@@ -1047,9 +1047,10 @@ def main():
                     help="lattice edge (default 100; c5pair 80: C5's ~0.5M particles per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-n", type=int, default=100)
-    ap.add_argument("--c5-cpu-n", type=int, default=40,
+    ap.add_argument("--c5-cpu-n", type=int, default=100,
                     help="c5: edge of the two-phase block the reference's five styles are "
-                         "timed on for cpu_baseline")
+                         "timed on for cpu_baseline (100^3 = 1M: ~35 s for the one timed "
+                         "step on one core, the largest size that fits a minute)")
     ap.add_argument("--workload", choices=["c2", "c3", "c5", "c2pair", "c5pair"], default="c2",
                     help="c2: the headline engine step (default); c3: two-phase Morris + "
                          "heat conduction engine step (config 3); c5: the bubble_growth "

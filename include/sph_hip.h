@@ -323,10 +323,12 @@ typedef struct {
   int blk_nbig;                /* block path: blocks of the last build whose union exceeds the
                                   force pass's LDS image (walked by the second launch) */
   int inner_rows;              /* block path: inner rows were built at the last rebuild */
-  int inner_live;              /* ... and no atom has moved past their margin since (the pair
-                                  passes walk them) */
+  int inner_live;              /* ... and the last step's passes walked them (no atom had moved
+                                  past their margin since they were written) */
   int flags;                   /* bit 0: the last rhosum/multiphase was summed inside the
                                   list fill (C5: its time is in ms_neigh, not ms_rhosum) */
+  int64_t inner_refresh;       /* refresh launches since create (inner rows derived again
+                                  between rebuilds when an atom passed their margin) */
 } sph_engine_stats;
 
 typedef struct sph_engine sph_engine;

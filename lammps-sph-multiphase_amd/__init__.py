@@ -90,7 +90,7 @@ class EngineStats(C.Structure):
         ("ms_integrate", C.c_double), ("ms_comm", C.c_double), ("ms_neigh", C.c_double),
         ("n_rhosum", C.c_int64), ("n_tait", C.c_int64), ("n_heat", C.c_int64),
         ("n_neigh", C.c_int64), ("blk_nbig", C.c_int), ("inner_rows", C.c_int),
-        ("inner_live", C.c_int), ("flags", C.c_int),
+        ("inner_live", C.c_int), ("flags", C.c_int), ("inner_refresh", C.c_int64),
     ]
 
     def as_dict(self):

@@ -1144,65 +1144,81 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
 // weight is exactly zero); once an atom has moved further the passes fall back to the full
 // rows until the next rebuild.  The slots keep their full-row order (rank by ballot within
 // the row's G lanes); tails are padded with the sentinel like the full rows.
+// Refresh (cond != nullptr; one workgroup per several blocks, grid-stride): only if *cond
+// is set -- an atom moved more than half the margin since the rows were written -- the rows
+// are derived again from the full rows at the current positions and x0 (the owned rows'
+// reference positions) takes them; *zero (the next step's flag) is cleared either way.  The
+// pair passes then walk inner rows again instead of the full rows for the rest of the build.
 template <int R, int G, int U, int NCH, bool NT1, int CQ>
 __global__ void __launch_bounds__(R * G)
 k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
             const unsigned short *__restrict__ snbr, int sstride, const int *__restrict__ rcnt,
             const double4 *__restrict__ xf, const int *__restrict__ ty,
             const Coefs *__restrict__ cf, unsigned short *__restrict__ snbi,
-            int *__restrict__ icnt, int um) {
+            int *__restrict__ icnt, int um, const int *__restrict__ cond,
+            int *__restrict__ zero, double4 *__restrict__ x0) {
   constexpr int NTH = R * G;
+  if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
+  if (cond && *cond == 0) return;  // (workgroup-uniform)
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ double s_c[NT1 ? 1 : NT2];
-  const int b = (int)xcd_block(), tid = threadIdx.x;
-  const int row = b * R + tid / G, lane = tid & (G - 1);
-  const bool live = row < n;
-  const int rr = live ? row : n - 1;
-  const int u = ucnt[b];
-  const int c = live ? rcnt[rr] : 0;
-  const int *const ul = ulist + (size_t)b * ucap;
-  BlkSlots<G, U, NCH> sw;
-  sw.load(snbr + (size_t)rr * sstride, c, lane);
-  const double4 xi = xf[rr];
-  const int it = NT1 ? 1 : ty[rr];
+  const int tid = threadIdx.x;
   const int nt1 = cf->ntypes + 1;
-  double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
-  double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)(um + 1) * 16);
-  unsigned char *const s_t = blk_smem + (size_t)(um + 1) * 24;
   if (!NT1)
     for (int t = tid; t < nt1 * nt1; t += NTH) s_c[t] = cf->cutinsq[t];
-  for (int p = tid; p < u; p += NTH) {
-    const int j = ul[p];
-    const double4 x = xf[j];
-    s_xy[p + 1] = make_double2(x.x, x.y);
-    s_z[p + 1] = x.z;
-    if (!NT1) s_t[p + 1] = (unsigned char)ty[j];
+  const int nb = (n + R - 1) / R;
+  for (int b = cond ? (int)blockIdx.x : (int)xcd_block(); b < nb; b += cond ? gridDim.x : nb) {
+    const int row = b * R + tid / G, lane = tid & (G - 1);
+    const bool live = row < n;
+    const int rr = live ? row : n - 1;
+    const int u = ucnt[b];
+    const int c = live ? rcnt[rr] : 0;
+    const int *const ul = ulist + (size_t)b * ucap;
+    BlkSlots<G, U, NCH> sw;
+    sw.load(snbr + (size_t)rr * sstride, c, lane);
+    const double4 xi = xf[rr];
+    const int it = NT1 ? 1 : ty[rr];
+    double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
+    double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)(um + 1) * 16);
+    unsigned char *const s_t = blk_smem + (size_t)(um + 1) * 24;
+    __syncthreads();  // (the previous block's image is no longer read)
+    for (int p = tid; p < u; p += NTH) {
+      const int j = ul[p];
+      const double4 x = xf[j];
+      s_xy[p + 1] = make_double2(x.x, x.y);
+      s_z[p + 1] = x.z;
+      if (!NT1) s_t[p + 1] = (unsigned char)ty[j];
+    }
+    if (tid == 0) {
+      s_xy[0] = make_double2(1e100, 1e100);
+      s_z[0] = 1e100;
+      if (!NT1) s_t[0] = 1;
+    }
+    __syncthreads();
+    const double c1 = NT1 ? cf->cutinsq[3] : 0.0;
+    const int grp = (tid & 63) / G;                   // the row's lane group in the wave
+    unsigned short *const out = snbi + (size_t)rr * sstride;
+    int base = 0;
+    sw.walk(c, lane, [&](int q, bool in) {
+      const int sj = blk_s<CQ>(q);
+      const double2 xy = s_xy[sj];
+      const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
+      const double rsq = dx * dx + dy * dy + dz * dz;
+      const bool hit = in && rsq < (NT1 ? c1 : s_c[it * nt1 + s_t[sj]]);
+      const unsigned long long m = __ballot(hit);
+      const unsigned g = (unsigned)(m >> (grp * G)) & ((1u << G) - 1u);
+      if (hit && live) out[blk_tpos<G, U>(base + __popc(g & ((1u << lane) - 1u)))] = (unsigned short)q;
+      base += __popc(g);
+    });
+    if (live) {
+      if (lane == 0) {
+        icnt[row] = base;
+        if (x0) x0[row] = xi;
+      }
+      const int cend = min((base + U * G - 1) / (U * G) * (U * G), sstride);
+      for (int k = base + lane; k < cend; k += G) out[blk_tpos<G, U>(k)] = 0;  // the sentinel
+    }
   }
-  if (tid == 0) {
-    s_xy[0] = make_double2(1e100, 1e100);
-    s_z[0] = 1e100;
-    if (!NT1) s_t[0] = 1;
-  }
-  __syncthreads();
-  const double c1 = NT1 ? cf->cutinsq[3] : 0.0;
-  const int grp = (tid & 63) / G;                   // the row's lane group in the wave
-  unsigned short *const out = snbi + (size_t)rr * sstride;
-  int base = 0;
-  sw.walk(c, lane, [&](int q, bool in) {
-    const int sj = blk_s<CQ>(q);
-    const double2 xy = s_xy[sj];
-    const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
-    const double rsq = dx * dx + dy * dy + dz * dz;
-    const bool hit = in && rsq < (NT1 ? c1 : s_c[it * nt1 + s_t[sj]]);
-    const unsigned long long m = __ballot(hit);
-    const unsigned g = (unsigned)(m >> (grp * G)) & ((1u << G) - 1u);
-    if (hit && live) out[blk_tpos<G, U>(base + __popc(g & ((1u << lane) - 1u)))] = (unsigned short)q;
-    base += __popc(g);
-  });
-  if (!live) return;
-  if (lane == 0) icnt[row] = base;
-  const int cend = min((base + U * G - 1) / (U * G) * (U * G), sstride);
-  for (int k = base + lane; k < cend; k += G) out[blk_tpos<G, U>(k)] = 0;  // the sentinel
 }
 
 // sph/taitwater[/morris] [+ sph/heatconduction] over the block union (full list, i side
@@ -1697,35 +1713,47 @@ inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
 }
 
 // the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum
+// (refresh: cond != nullptr, see k_blk_inner; a grid of at most 512 workgroups, so that a
+// launch whose flag is clear costs a few microseconds)
+struct BlkInnerRefresh {
+  const int *cond = nullptr;
+  int *zero = nullptr;
+  double4 *x0 = nullptr;
+};
 template <int R, int G, int U, int NCH, bool NT1>
 inline void blk_inner_t(hipStream_t s, const BlkArgs &k, const double4 *xf, const int *ty,
-                        const Coefs *cf, unsigned short *snbi, int *icnt) {
+                        const Coefs *cf, unsigned short *snbi, int *icnt,
+                        const BlkInnerRefresh &rf) {
   const size_t lds = blk_rho_lds(k.um, NT1);
   auto fn = k.cq == BLK_CH / 16 ? k_blk_inner<R, G, U, NCH, NT1, BLK_CH / 16>
                                 : k_blk_inner<R, G, U, NCH, NT1, BLK_CHE / 16>;
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
-  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
-                     k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, cf, snbi, icnt, k.um);
+  const int nb = blk_blocks(k.n, R);
+  hipLaunchKernelGGL(fn, dim3(rf.cond ? std::min(nb, 512) : nb), dim3(R * G), lds, s, k.n,
+                     k.ulist, k.ucnt, k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, cf, snbi, icnt,
+                     k.um, rf.cond, rf.zero, rf.x0);
 }
 template <int R, int G, int U>
 inline void blk_inner_s(bool nt1, hipStream_t s, const BlkArgs &k, const double4 *xf,
-                        const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt) {
+                        const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt,
+                        const BlkInnerRefresh &rf) {
   const bool pre = k.pre(BlkShape{R, G, U});
   if (nt1) {
-    if (pre) blk_inner_t<R, G, U, BLK_NCH, true>(s, k, xf, ty, cf, snbi, icnt);
-    else blk_inner_t<R, G, U, 0, true>(s, k, xf, ty, cf, snbi, icnt);
+    if (pre) blk_inner_t<R, G, U, BLK_NCH, true>(s, k, xf, ty, cf, snbi, icnt, rf);
+    else blk_inner_t<R, G, U, 0, true>(s, k, xf, ty, cf, snbi, icnt, rf);
   } else {
-    if (pre) blk_inner_t<R, G, U, BLK_NCH, false>(s, k, xf, ty, cf, snbi, icnt);
-    else blk_inner_t<R, G, U, 0, false>(s, k, xf, ty, cf, snbi, icnt);
+    if (pre) blk_inner_t<R, G, U, BLK_NCH, false>(s, k, xf, ty, cf, snbi, icnt, rf);
+    else blk_inner_t<R, G, U, 0, false>(s, k, xf, ty, cf, snbi, icnt, rf);
   }
 }
 inline void blk_inner(bool nt1, hipStream_t s, const BlkArgs &k, const double4 *xf,
-                      const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt) {
+                      const int *ty, const Coefs *cf, unsigned short *snbi, int *icnt,
+                      const BlkInnerRefresh &rf = BlkInnerRefresh{}) {
   if (k.n == 0) return;
   switch (k.shape) {
 #define SPH_CASE(q, R, G, U) \
-  case q: blk_inner_s<R, G, U>(nt1, s, k, xf, ty, cf, snbi, icnt); break;
+  case q: blk_inner_s<R, G, U>(nt1, s, k, xf, ty, cf, snbi, icnt, rf); break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE
   }

@@ -139,6 +139,12 @@ static bool rowsort() {
 }
 // SPH_N3 (study builds only; default 0): the block build keeps each pair of rows of one
 // block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
+// SPH_INNER_REFRESH (study builds; default 1): derive the inner rows again between rebuilds
+// once an atom has moved past their margin (refresh_inner)
+static bool refresh_env() {
+  static bool v = study_int("SPH_INNER_REFRESH", 1) != 0;
+  return v;
+}
 static bool n3_env() {
   static bool v = BLK_N3_BUILT && study_int("SPH_N3", 0) != 0;
   return v;
@@ -277,6 +283,7 @@ struct sph_engine {
   DBuf<int> cnt, off, nbr;
   int64_t nbr_total = 0;   // list entries (-1: strided list, counted on demand)
   int nbr_builds = 0, nbr_maxrow = 0;
+  int64_t inner_refreshes = 0;  // refresh_inner launches
   bool strided = false;    // list in fixed-stride rows (row i at i*list_stride, ccnt[i])
   int list_stride = 0;
   int list_perm_g = 0;     // strided rows stored chunk-transposed for G-lane rows (tpos)
@@ -467,12 +474,7 @@ struct sph_engine {
       hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, vel.p, rm.p,
                          cvv.p, cg.p, xbuf.p);
     }
-    xf2.reserve_exact(xf.cap);
-    vr2.reserve_exact(vr.cap);
-    en2.reserve_exact(en.cap);
-    ty2.reserve_exact(ty.cap);
-    vel2.reserve_exact(vel.cap);
-    tag2.reserve_exact(tag.cap);
+    grow_twins();
     hipLaunchKernelGGL(k_permute, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, xf.p, vr.p,
                        en.p, ty.p, vel.p, tag.p, xf2.p, vr2.p, en2.p, ty2.p, vel2.p, tag2.p);
     std::swap(xf, xf2);
@@ -484,6 +486,19 @@ struct sph_engine {
     if (mp)
       hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
                          0, xbuf.p, vel.p, rm.p, cvv.p, cg.p);
+  }
+
+  // the sort's twins at the capacity of the arrays they swap with; called again at the end
+  // of every build, so that the growth borders caused (ghosts) is matched in the same build
+  // -- at setup -- and not by a hipMalloc + synchronising hipFree in the next one (~1 ms of
+  // host time in the first rebuild after setup, profiles/r04/first_rebuild)
+  void grow_twins() {
+    xf2.reserve_exact(xf.cap);
+    vr2.reserve_exact(vr.cap);
+    en2.reserve_exact(en.cap);
+    ty2.reserve_exact(ty.cap);
+    vel2.reserve_exact(vel.cap);
+    tag2.reserve_exact(tag.cap);
   }
 
   // kernel_path 0: block-staged passes (production; the row path takes over for a build
@@ -1431,7 +1446,7 @@ struct sph_engine {
     if (inner) {
       k.snbi = snbi.p;
       k.icnt = icnt.p;
-      k.moved = moved.p;
+      k.moved = moved_flag();
     }
     return k;
   }
@@ -1452,6 +1467,7 @@ struct sph_engine {
       last_sort = step;
     }
     borders();
+    if (cfg.sort) grow_twins();
     bin_q();
     blk = false;
     if (need_csr || !want_blk() || mp) list_q(need_csr);
@@ -1484,7 +1500,7 @@ struct sph_engine {
     const BlkShape sh = blk_shape(blk_sh);
     snbi.reserve((size_t)nlocal * blk_sstride + 2 * sh.U * sh.G);
     icnt.reserve(nlocal);
-    moved.reserve(1);
+    moved.reserve(2);
     const size_t nx0 = (size_t)nlocal + (multi() ? nghost : 0);
     x0.reserve(nx0);
     if (!inner_written) {
@@ -1492,10 +1508,35 @@ struct sph_engine {
       blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
     }
     SPH_HIP_TRY(hipMemcpyAsync(x0.p, xf.p, nx0 * sizeof(double4), hipMemcpyDeviceToDevice, s));
-    SPH_HIP_TRY(hipMemsetAsync(moved.p, 0, sizeof(int), s));
+    SPH_HIP_TRY(hipMemsetAsync(moved.p, 0, 2 * sizeof(int), s));
     sc.x0 = x0.p;
     sc.lim2 = 0.25 * inner_margin * inner_margin;
-    sc.moved = moved.p;
+    sc.moved = moved_flag();
+  }
+  // The moved flag of this step (two slots, by step parity: the integrate and the ghost check
+  // of step k raise slot k & 1 against x0, the passes of step k read it; refresh_inner
+  // clears the other slot for step k + 1).  Validity of the inner rows depends only on the
+  // current displacements from x0, so a flag per step, not a sticky one, is exact.
+  int *moved_flag() const { return moved.p ? moved.p + (step & 1) : nullptr; }
+  // After the passes of a step between rebuilds: if this step's flag is raised, the inner
+  // rows are derived again from the full rows at the current positions (x0 := them), so the
+  // next steps walk ~120 instead of ~155 entries per row until the next rebuild; skipped
+  // when the next step rebuilds anyway.
+  void refresh_inner(bool rebuild_next) {
+    if (!inner || !sc.x0 || !refresh_env()) return;
+    if (rebuild_next) return;  // (the rebuild clears both slots)
+    int *const cur = moved_flag();
+    int *const nxt = moved.p + ((step + 1) & 1);
+    BlkArgs k = blk_args();
+    BlkInnerRefresh rf;
+    rf.cond = cur;
+    rf.zero = nxt;
+    rf.x0 = x0.p;
+    blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p, rf);
+    if (multi() && nghost)
+      hipLaunchKernelGGL(k_x0_cond, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost, cur,
+                         xf.p + nlocal, x0.p + nlocal);
+    inner_refreshes++;
   }
 
   bool overlap_on() const {
@@ -2128,6 +2169,7 @@ struct sph_engine {
     // the last step's final_integrate runs on its own after the loop
     for (int k = 0; k < nsteps; k++) {
       step++;
+      if (sc.x0) sc.moved = moved_flag();
       {
         Scope t(this, T_INT);
         if (k == 0)
@@ -2153,6 +2195,7 @@ struct sph_engine {
         forward();
         pair_compute(rhosum_due());
       }
+      refresh_inner(!pc && (step + 1 - last_build) % every == 0);
       if (timing && pending.size() > 4096) harvest();
     }
     if (nsteps > 0) {
@@ -2833,11 +2876,12 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->inner_live = 0;
   if (e->inner && e->moved.p) {
     int mv = 1;
-    SPH_HIP_TRY(hipMemcpyAsync(&mv, e->moved.p, sizeof(int), hipMemcpyDeviceToHost, e->s));
+    SPH_HIP_TRY(hipMemcpyAsync(&mv, e->moved_flag(), sizeof(int), hipMemcpyDeviceToHost, e->s));
     SPH_HIP_TRY(hipStreamSynchronize(e->s));
     st->inner_live = mv == 0 ? 1 : 0;
   }
   st->flags = (e->rho_fused_step >= 0 && e->rho_fused_step == e->step) ? 1 : 0;
+  st->inner_refresh = e->inner_refreshes;
   SPH_API_END
 }
 

@@ -39,6 +39,15 @@ static __global__ void k_inner_ghosts(int ng, int nlocal, StepConst sc,
   inner_check(sc, nlocal + g, xf[nlocal + g]);
 }
 
+// the ghosts' reference positions of the inner rows, taken again when *cond is raised
+// (sph_engine refresh_inner, bricks)
+static __global__ void k_x0_cond(int ng, const int *__restrict__ cond,
+                                 const double4 *__restrict__ xg, double4 *__restrict__ x0g) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng || *cond == 0) return;
+  x0g[g] = xg[g];
+}
+
 // FixMeso::initial_integrate (fix_meso.cpp:91-140) / FixMesoStationary (:71-90)
 static __global__ void k_initial_integrate(int n, StepConst sc, double4 *__restrict__ xf,
                                            double4 *__restrict__ vr, double *__restrict__ en,

@@ -42,6 +42,9 @@ def at_rest(s):
     return s
 
 
+LAST_STATS = []   # sph_engine_stats of every brick of the last run_bricks
+
+
 def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0, overlap=False):
     nt = s.ntypes
     P = int(np.prod(pg))
@@ -84,8 +87,9 @@ def run_bricks(sph_amd, s, ph, pg, nsteps, every=None, path=0, overlap=False):
     assert not any(t.is_alive() for t in th), "brick threads hung"
     try:
         assert not errors, errors
-        for e in engines:  # the requested pair path really ran (no silent fallback)
-            assert e.stats()["staged"] == (1 if path == 0 else 0)
+        LAST_STATS[:] = [e.stats() for e in engines]
+        for st in LAST_STATS:  # the requested pair path really ran (no silent fallback)
+            assert st["staged"] == (1 if path == 0 else 0)
         return collect(engines, s)
     finally:
         for e in engines:
@@ -172,6 +176,8 @@ def test_bricks_migration(gpu, sph_amd, path):
     assert sum(nloc) == s.n
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
+    if path == 0:  # the inner rows were derived again between rebuilds (ghosts' x0 too)
+        assert sum(st["inner_refresh"] for st in LAST_STATS) > 0
 
 
 @pytest.mark.parametrize("path", PATHS)

@@ -96,6 +96,32 @@ def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     assert eng.stats()["step"] == 25
 
 
+def test_inner_rows_refresh(gpu, sph_amd):
+    """Between rebuilds the inner rows (pairs within cut + skin/16 at the time they were
+    written) are derived again once an atom has moved past half that margin (refresh_inner,
+    a per-step moved flag): with 3x the lattice's velocities and 20 steps per build the
+    refresh runs several times; fields stay at 1e-10 and counts exact at every compared step,
+    and the passes end on inner rows (inner_live)."""
+    s = c2_system(12)
+    s.v *= 3.0
+    ph = po.c2_physics()
+    ph.every = 20
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    eng = engine_for(sph_amd, s, ph)
+    eng.setup()
+    done = 0
+    for k in (6, 13, 19, 27):
+        ref.run(k - done)
+        eng.run(k - done)
+        done = k
+        assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full()), k
+        compare(eng, ref, path=0)
+    st = eng.stats()
+    assert st["inner_refresh"] > 0, "no refresh: the atoms did not move past the margin"
+    assert st["inner_rows"] == 1 and st["inner_live"] == 1
+
+
 @pytest.mark.parametrize("path", PATHS)
 def test_run_c3_morris_heat(gpu, sph_amd, path):
     s = c3_system(10)

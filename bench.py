@@ -1256,7 +1256,7 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args):
     the kernel, config and commit it was taken on.  Attached as `traffic` only when that
     record matches this run (same kernel family, single GPU, same lattice edge and steps);
     otherwise it is omitted (traffic null) rather than reported from another configuration."""
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         if not os.path.exists(tj):
             continue

@@ -263,6 +263,7 @@ struct sph_engine {
   std::vector<int> dr_peer;
   std::vector<size_t> dr_soff, dr_roff;
   DBuf<int> dr_sidx, dr_rslot, dr_self, dr_req;
+  DBuf<int> dr_byq, dr_byg, dr_hist;  // ghosts grouped by origin rank: owned index, slot
   int dr_nself = 0;
   std::vector<const void *> dr_sb;
   std::vector<void *> dr_rb;
@@ -656,29 +657,35 @@ struct sph_engine {
     dr_ok = false;
     if (!direct_env() || mp || !tr) return;
     const int P = tr->size(), me = tr->rank(), ng = nghost;
-    std::vector<int> hr(ng), hi(ng);
+    // the ghosts grouped by origin rank on the device (a stable radix sort of (rank, ghost)
+    // keeps the ghost order within a rank), the per-rank counts the only read-back
+    std::vector<int> beg(P + 2, 0);
+    dr_byq.reserve(ng > 0 ? ng : 1);
+    dr_byg.reserve(ng > 0 ? ng : 1);
+    dr_hist.reserve(P + 2);
     if (ng) {
-      SPH_HIP_TRY(hipMemcpyAsync(hr.data(), gorank.p, ng * sizeof(int), hipMemcpyDeviceToHost, s));
-      SPH_HIP_TRY(hipMemcpyAsync(hi.data(), goidx.p, ng * sizeof(int), hipMemcpyDeviceToHost, s));
+      bkey.reserve(ng);
+      bkey2.reserve(ng);
+      bidx.reserve(ng);
+      bidx2.reserve(ng);
+      hipLaunchKernelGGL(k_dr_keys, dim3(blocks(ng)), dim3(BLK), 0, s, ng, P, gorank.p, bkey.p,
+                         bidx.p);
+      int eb = 1;
+      while ((1 << eb) <= P) eb++;
+      size_t tb = 0;
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, eb, s));
+      tmp_reserve(tb);
+      SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, bkey.p, bkey2.p, bidx.p, bidx2.p, ng, 0, eb, s));
+      hipLaunchKernelGGL(k_dr_group, dim3(blocks(ng)), dim3(BLK), 0, s, ng, bidx2.p, goidx.p,
+                         dr_byq.p, dr_byg.p);
+      // beg[r]: the first ghost of rank r (r = 0 .. P + 1; ranks out of range sort as P)
+      hipLaunchKernelGGL(k_lower_bound, dim3(1), dim3(64 * ((P + 2 + 63) / 64)), 0, s, P + 1,
+                         ng, 0, bkey2.p, dr_hist.p);
+      SPH_HIP_TRY(hipMemcpyAsync(beg.data(), dr_hist.p, (P + 2) * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
     }
-    // counting sort of the ghosts by origin rank (ghost order kept within a rank)
-    std::vector<int> cnt(P + 1, 0);
-    for (int g = 0; g < ng; g++) {
-      SPH_REQUIRE(hr[g] >= 0 && hr[g] < P, SPH_HIP_ERUNTIME, "ghost %d: origin rank %d", g, hr[g]);
-      cnt[hr[g] + 1]++;
-    }
-    std::vector<int> beg(P + 1, 0);
-    for (int r = 0; r < P; r++) beg[r + 1] = beg[r] + cnt[r + 1];
-    std::vector<int> byq(ng), byg(ng);  // owned indices / ghost slots, grouped by origin rank
-    {
-      std::vector<int> pos(beg.begin(), beg.end() - 1);
-      for (int g = 0; g < ng; g++) {
-        const int k = pos[hr[g]]++;
-        byq[k] = hi[g];
-        byg[k] = g;
-      }
-    }
+    SPH_REQUIRE(beg[P + 1] == beg[P], SPH_HIP_ERUNTIME,
+                "%d ghosts with an origin rank outside [0,%d)", beg[P + 1] - beg[P], P);
     std::vector<int> scnt(P, 0), rcnt(P, 0);
     for (int r = 0; r < P; r++)
       if (r != me) scnt[r] = beg[r + 1] - beg[r];
@@ -686,28 +693,34 @@ struct sph_engine {
     dr_peer.clear();
     dr_soff.assign(1, 0);
     dr_roff.assign(1, 0);
-    std::vector<int> hreq, hslot;
-    hreq.reserve(ng);
-    hslot.reserve(ng);
     for (int r = 0; r < P; r++) {
       if (r == me && !loopback) continue;
       const size_t nin = beg[r + 1] - beg[r], nout = (r == me) ? nin : (size_t)rcnt[r];
       if (nin == 0 && nout == 0) continue;
       dr_peer.push_back(r);
-      hreq.insert(hreq.end(), byq.begin() + beg[r], byq.begin() + beg[r + 1]);
-      hslot.insert(hslot.end(), byg.begin() + beg[r], byg.begin() + beg[r + 1]);
       dr_roff.push_back(dr_roff.back() + nin);
       dr_soff.push_back(dr_soff.back() + nout);
     }
     const int np = (int)dr_peer.size();
     const size_t S = dr_soff.back(), R = dr_roff.back();
+    // the peers' groups are the rank-ordered groups without this rank's own (unless the
+    // loopback sends those through the communicator): two device copies
     DBuf<int> &req = dr_req;  // (persistent: no hipMalloc / synchronising hipFree per rebuild)
     req.reserve(R > 0 ? R : 1);
     dr_sidx.reserve(S > 0 ? S : 1);
     dr_rslot.reserve(R > 0 ? R : 1);
-    if (R) {
-      SPH_HIP_TRY(hipMemcpyAsync(req.p, hreq.data(), R * sizeof(int), hipMemcpyHostToDevice, s));
-      SPH_HIP_TRY(hipMemcpyAsync(dr_rslot.p, hslot.data(), R * sizeof(int), hipMemcpyHostToDevice, s));
+    {
+      const size_t a = loopback ? (size_t)ng : (size_t)beg[me];
+      const size_t b0 = loopback ? (size_t)ng : (size_t)beg[me + 1];
+      SPH_REQUIRE(a + (ng - b0) == R, SPH_HIP_ERUNTIME, "direct forward: %zu != %zu", a + (ng - b0), R);
+      if (a) {
+        SPH_HIP_TRY(hipMemcpyAsync(req.p, dr_byq.p, a * sizeof(int), hipMemcpyDeviceToDevice, s));
+        SPH_HIP_TRY(hipMemcpyAsync(dr_rslot.p, dr_byg.p, a * sizeof(int), hipMemcpyDeviceToDevice, s));
+      }
+      if (ng > (int)b0) {
+        SPH_HIP_TRY(hipMemcpyAsync(req.p + a, dr_byq.p + b0, (ng - b0) * sizeof(int), hipMemcpyDeviceToDevice, s));
+        SPH_HIP_TRY(hipMemcpyAsync(dr_rslot.p + a, dr_byg.p + b0, (ng - b0) * sizeof(int), hipMemcpyDeviceToDevice, s));
+      }
     }
     dr_sb.resize(np);
     dr_rb.resize(np);
@@ -724,8 +737,7 @@ struct sph_engine {
     dr_nself = loopback ? 0 : beg[me + 1] - beg[me];
     dr_self.reserve(dr_nself > 0 ? dr_nself : 1);
     if (dr_nself)
-      SPH_HIP_TRY(hipMemcpyAsync(dr_self.p, byg.data() + beg[me], dr_nself * sizeof(int), hipMemcpyHostToDevice, s));
-    SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host vectors go out of scope)
+      SPH_HIP_TRY(hipMemcpyAsync(dr_self.p, dr_byg.p + beg[me], dr_nself * sizeof(int), hipMemcpyDeviceToDevice, s));
     dr_ok = true;
   }
   // one direct forward of rec-byte records: pack the send lists, one exchange, unpack
@@ -2406,7 +2418,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->rhoS, &e->rhoF}) b->release();
   for (auto *b : {&e->cg, &e->cgS, &e->cgF, &e->recA, &e->recK, &e->recF, &e->recS}) b->release();
   if (e->dm) (void)hipFree(e->dm);
-  for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->dr_req, &e->pc_flag,
+  for (auto *b : {&e->nbs, &e->gorank, &e->goidx, &e->dr_sidx, &e->dr_rslot, &e->dr_self, &e->dr_req, &e->dr_byq, &e->dr_byg, &e->dr_hist, &e->pc_flag,
                   &e->pc_cand, &e->pc_otag, &e->pc_idx})
     b->release();
   for (auto *b : {&e->pc_rec, &e->pc_gat, &e->pc_Wd, &e->pc_vals, &e->pc_nrec, &e->pc_v0,

@@ -39,6 +39,27 @@ static __global__ void k_inner_ghosts(int ng, int nlocal, StepConst sc,
   inner_check(sc, nlocal + g, xf[nlocal + g]);
 }
 
+// build_direct: (origin rank, ghost) keys for the stable grouping sort; an origin rank out
+// of range sorts last as rank P (the group bounds come from k_lower_bound on the sorted keys)
+static __global__ void k_dr_keys(int ng, int P, const int *__restrict__ gorank,
+                                 unsigned *__restrict__ key, int *__restrict__ val) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  const int r = gorank[g];
+  key[g] = (r >= 0 && r < P) ? (unsigned)r : (unsigned)P;
+  val[g] = g;
+}
+// ... and the grouped ghosts' owned indices on their origin ranks and their slots
+static __global__ void k_dr_group(int ng, const int *__restrict__ sg,
+                                  const int *__restrict__ goidx, int *__restrict__ byq,
+                                  int *__restrict__ byg) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ng) return;
+  const int g = sg[k];
+  byq[k] = goidx[g];
+  byg[k] = g;
+}
+
 // the ghosts' reference positions of the inner rows, taken again when *cond is raised
 // (sph_engine refresh_inner, bricks)
 static __global__ void k_x0_cond(int ng, const int *__restrict__ cond,

@@ -930,6 +930,8 @@ def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
                                    "build / phase change, integrate, comm: 3 further steps "
                                    "with every class timed"},
     }
+    attach_pmc_traffic(out, "k_mp2_gather", b_half * nloc, world, args,
+                       fname="pmc_traffic_c5.json")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = c5_cpu_baseline(args.c5_cpu_n, steps=1)
     if rank == 0:
@@ -1250,14 +1252,14 @@ def main():
         dist.destroy_process_group()
 
 
-def attach_pmc_traffic(out, kname, alg_bytes, world, args):
+def attach_pmc_traffic(out, kname, alg_bytes, world, args, fname="pmc_traffic.json"):
     """HBM traffic per step of the roofline kernel from PMC counters, measured on THIS
     workload by tools/pmc_traffic.sh and committed as profiles/<round>/pmc_traffic.json with
     the kernel, config and commit it was taken on.  Attached as `traffic` only when that
     record matches this run (same kernel family, single GPU, same lattice edge and steps);
     otherwise it is omitted (traffic null) rather than reported from another configuration."""
     for rnd in ("r04", "r03", "r02"):
-        tj = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        tj = os.path.join(ROOT, "profiles", rnd, fname)
         if not os.path.exists(tj):
             continue
         rec = json.load(open(tj))
@@ -1270,7 +1272,7 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args):
             out["roofline"]["traffic"] = v["traffic_bytes"] / 1e9
             out["roofline"]["traffic_unit"] = (
                 f"GB per step of {kname} (its launches summed; PMC 2*FETCH_SIZE + WRITE_SIZE, "
-                f"tools/pmc_traffic.sh, profiles/{rnd}/pmc_traffic.json, commit "
+                f"tools/pmc_traffic.sh, profiles/{rnd}/{fname}, commit "
                 f"{meta.get('commit', '?')})")
             out["roofline"]["algorithmic_GB_per_step"] = alg_bytes / 1e9
             va = v.get("valu")

@@ -62,8 +62,12 @@ def main(root, meta):
             per[str(g)] = {"fetch_bytes": fa, "write_bytes": wa, "launches": len(f),
                            "traffic_bytes": 2.0 * fa + wa}
             tot += (2.0 * fa + wa) * len(f)
-        # per step: all launches' bytes over the count of the largest-grid (main) launch
+        # per step: all launches' bytes over the count of the largest-grid (main) launch; a
+        # family with one launch per step whose grid drifts (C5: the atom count grows with
+        # the insertions) is averaged over all its launches instead
         nmain = per[str(max(grids))]["launches"] if ok and grids else 0
+        if ok and grids and min(grids) > 0.9 * max(grids):
+            nmain = sum(v["launches"] for v in per.values())
         out[k] = {"grids": per, "traffic_bytes": tot / nmain if ok and nmain else None}
     dur = collections.defaultdict(lambda: collections.defaultdict(list))
     valu = load(f"{root}/valu", "SQ_INSTS_VALU", 1.0, dur)

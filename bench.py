@@ -255,6 +255,67 @@ def cpu_baseline(n_cpu, steps=2):
             "pair_only_particle_steps_per_s": s.n / (t_rho + t_tait)}
 
 
+def _brick_cpu_worker(a):
+    """One brick of cpu_baseline_cores, in its own process: the reference's list build and
+    rhosum + taitwater on the brick's owned + ghost atoms (borders_bricks), per step."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    R = po.ref()
+    x, typ, nlocal, nghost, lo, hi, cmax, cns, rho, vest, mass, cut, visc, rho0, c0, steps = a
+    args = (3, 1, nlocal, nghost, x, typ, lo, hi, lo, hi, cmax, cns)
+    t0 = time.perf_counter()
+    foff = np.zeros(nlocal + 1, dtype=np.int64)
+    tot = R.ref_neigh_full(*args, foff, None, 0)
+    fnb = np.zeros(max(tot, 1), dtype=np.int32)
+    R.ref_neigh_full(*args, foff, fnb.ctypes.data, tot)
+    hoff = np.zeros(nlocal + 1, dtype=np.int64)
+    htot = R.ref_neigh_half_from_full(nlocal, nghost, x, foff, fnb, hoff, None)
+    hnb = np.zeros(max(htot, 1), dtype=np.int32)
+    R.ref_neigh_half_from_full(nlocal, nghost, x, foff, fnb, hoff, hnb.ctypes.data)
+    t_build = (time.perf_counter() - t0) / 2.0
+    nall = nlocal + nghost
+    f, drho, de = np.zeros((nall, 3)), np.zeros(nall), np.zeros(nall)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        R.ref_rhosum(3, 1, nlocal, nghost, x, typ, mass, cut, foff, fnb, rho)
+        R.ref_taitwater(3, 1, nlocal, nghost, 1, x, vest, rho, typ, mass, rho0, c0, visc, cut,
+                        hoff, hnb, f, drho, de)
+    return (time.perf_counter() - t0) / steps + t_build / 10.0
+
+
+def cpu_baseline_cores(n_cpu, nproc=8, steps=2):
+    """The C2 CPU baseline on nproc cores as LAMMPS runs it with MPI: the n_cpu^3 box split
+    into nproc bricks (2x2x2 at 8, CommBrick::borders ghosts, pyoracle.borders_bricks), each
+    brick's reference list build + rhosum + taitwater in its own process at the same time;
+    per step = the slowest brick (halo exchange and reverse comm, ~1 % on one core, not
+    timed).  Processes are spawned (not forked: the parent holds a HIP context)."""
+    import multiprocessing as mpc
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+    if not po.ref_available():
+        return None
+    s = po.cubic_lattice(n_cpu)
+    ph = po.c2_physics()
+    cns, cmax = po.cutneighsq(1, ph.cutmax(1), ph.skin)
+    pg = procgrid_for(nproc)
+    work = []
+    for v in po.borders_bricks(s, cmax, pg):
+        work.append((np.ascontiguousarray(v.x), np.ascontiguousarray(v.type), v.nlocal, v.nghost,
+                     np.asarray(v.lo, float), np.asarray(v.hi, float), cmax,
+                     np.ascontiguousarray(cns), np.ascontiguousarray(s.rho[v.gid]),
+                     np.ascontiguousarray(s.v[v.gid]), s.mass, np.ascontiguousarray(ph.tait_cut),
+                     np.ascontiguousarray(ph.visc), ph.rho0, ph.c0, steps))
+    with mpc.get_context("spawn").Pool(nproc) as pool:
+        per = pool.map(_brick_cpu_worker, work)
+    t = max(per)
+    return {"value": s.n / t, "unit": "particle-steps/s", "cores": nproc, "kind": "reference",
+            "sample": f"reference USER-SPH compute code (oracle/_ref) on {s.n} particles split "
+                      f"into {pg[0]}x{pg[1]}x{pg[2]} bricks, one process per brick running at "
+                      f"the same time (LAMMPS' MPI decomposition): list build / 10 + rhosum + "
+                      f"taitwater per step, slowest brick {t:.3f} s (bricks "
+                      f"{min(per):.3f}-{t:.3f} s); halo exchange not timed"}
+
+
 # ---- C3: two-phase Morris + heat conduction on the engine (SURVEY.md 8(d) C3) ----------
 C3_MASS, C3_RHO0, C3_E = (1.0, 0.5), (1.0, 0.5), (1.0, 2.0)
 
@@ -1244,6 +1305,8 @@ def main():
     attach_pmc_traffic(out, kname, bytes_tait * nloc, world, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n)
+        # beside it, the same reference code on 8 cores (one brick per process)
+        out["cpu_baseline_cores"] = cpu_baseline_cores(args.cpu_n, nproc=8)
     if rank == 0:
         print(json.dumps(out), flush=True)
     with stdout_to_stderr():  # communicator teardown

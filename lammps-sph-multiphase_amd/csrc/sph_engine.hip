@@ -141,6 +141,10 @@ static bool rowsort() {
 // block once (Newton-3 inside the blocks, k_blk_build N3) -- measured slower, DESIGN.md 5.2
 // SPH_INNER_REFRESH (study builds; default 1): derive the inner rows again between rebuilds
 // once an atom has moved past their margin (refresh_inner)
+static bool inner_inline() {
+  static bool v = study_int("SPH_INNER_INLINE", 1) != 0;
+  return v;
+}
 static bool refresh_env() {
   static bool v = study_int("SPH_INNER_REFRESH", 1) != 0;
   return v;
@@ -1382,7 +1386,9 @@ struct sph_engine {
       // k_blk_build (ballots, inner rows in the same pass); the bitmap walk k_blk_neigh for
       // the large candidate image (and in study builds, SPH_BUILD=0)
       const bool v2 = !big && study_int("SPH_BUILD", 1) != 0;
-      const bool want_inner = inner_margin > 0.0;
+      // the inner rows' ballots inside the build (SPH_INNER_INLINE, study; default 1), or a
+      // k_blk_inner pass over the full rows afterwards (build_inner)
+      const bool want_inner = inner_margin > 0.0 && inner_inline();
       if (v2 && want_inner) {
         snbi.reserve((size_t)n * blk_sstride + 2 * chunk);
         icnt.reserve(n);

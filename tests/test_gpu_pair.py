@@ -295,3 +295,39 @@ def test_mapped_host_arrays_and_update(gpu, sph_amd):
     assert rel_err(drho, wd2) < TOL
     ctx.host_arrays(0)
     ctx.close()
+
+
+def test_device_lists_edge_cases(gpu, sph_amd):
+    """sph_hip_build_list on an empty system, on isolated atoms (no neighbour, the self term
+    only), with ghosts only beside one owned atom, and a key reused with another
+    cutneighsq (rebuilt, not reused); a non-finite cutoff fails with EINVAL."""
+    ph = po.c2_physics(3.0)
+    mass = np.array([0.0, 1.0])
+    cns = np.array([[0.0, 0.0], [0.0, 3.3 * 3.3]])
+    ctx = sph_amd.PairContext(3, 1, 1)
+    ctx.rhosum_coeff(ph.rhosum_cut, mass)
+    ctx.atoms(0, 0, np.zeros((0, 3)), np.zeros(0, np.int32))
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns, key=1)
+    ctx.rhosum(np.zeros(1))
+    # isolated atoms
+    x = np.array([[0.0, 0.0, 0.0], [50.0, 0.0, 0.0]])
+    ctx.atoms(2, 0, x, np.ones(2, np.int32), vest=np.zeros((2, 3)), rho=np.ones(2), e=np.zeros(2))
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns, key=2)
+    assert np.array_equal(ctx.numneigh(2), [0, 0])
+    rho = ctx.rhosum(np.zeros(2))
+    assert np.allclose(rho, 2.1541870227086614782 / 27.0, rtol=1e-15)
+    # one owned atom, its neighbours all ghosts (owned rows only; ghosts are never rows)
+    xg = np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [0.0, 2.0, 0.0], [0.0, 0.0, 3.2],
+                   [3.0, 3.0, 0.0]])
+    t = np.ones(5, np.int32)
+    ctx.atoms(1, 4, xg, t, vest=np.zeros((5, 3)), rho=np.ones(5), e=np.zeros(5))
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns, key=3)
+    assert np.array_equal(ctx.numneigh(1), [3])      # 4.24 > 3.3 is out
+    ctx.build_list(sph_amd.SPH_LIST_HALF, cns, key=3)
+    assert np.array_equal(ctx.numneigh(1), [3])      # ghosts above in z / y / x all kept
+    # the same key with another cutneighsq: built again
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns * (1.5 / 3.3) ** 2, key=3)
+    assert np.array_equal(ctx.numneigh(1), [1])
+    with pytest.raises(sph_amd.HipError):
+        ctx.build_list(sph_amd.SPH_LIST_FULL, np.array([[0.0, 0.0], [0.0, np.inf]]), key=4)
+    ctx.close()

@@ -128,6 +128,11 @@ static bool mp_typed_env() {
   static bool v = study_int("SPH_MP_TYPED", 1) != 0;
   return v;
 }
+// one brick's borders: a dimension's two swaps in three launches (k_brd_*), or the
+// per-swap flags + select + append of earlier rounds (SPH_BRD_FUSED=0, builds)
+#ifndef SPH_BRD_FUSED
+#define SPH_BRD_FUSED 1
+#endif
 // SPH_ROWSORT (study builds; default 0): the pair passes walk each block's rows longest
 // first (k_blk_build's per-block order), so that a wave's rows have similar lengths
 static bool rowsort() {
@@ -195,6 +200,7 @@ struct sph_engine {
   std::vector<int> gswap_first;  // one brick: first ghost of each swap (+ nghost at the end)
   int gcap_hint = 0;              // one brick: ghost room of the next borders
   DBuf<int> gnall;                // one brick: nall before each swap (+ the overflow word)
+  DBuf<int> bcnt;                 // one brick: the swaps' per-block counts (k_brd_*)
   DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec, pc_v0, pc_v1;
   DBuf<unsigned long long> pc_k0, pc_k1;  // the donations' (donor, candidate) sort keys
   DBuf<int> pc_cnt;
@@ -1041,6 +1047,26 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemcpyAsync(gnall.p + nsw + 1, h_small + 15, sizeof(int),
                                  hipMemcpyHostToDevice, s));
       int w = 0;
+#if SPH_BRD_FUSED
+      // a dimension's two swaps in three launches (k_brd_count / scan / scatter)
+      for (int d = 0; d < ndim; d++) {
+        if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
+        const double lo0 = -1.0e20, hi0 = sublo[d] + cutghost;
+        const double lo1 = subhi[d] - cutghost, hi1 = 1.0e20;
+        const int nb = (cap + BRD_CH - 1) / BRD_CH;
+        bcnt.reserve(2 * (size_t)nb);
+        hipLaunchKernelGGL(k_brd_count, dim3(nb), dim3(BRD_T), 0, s, gnall.p + w, d, lo0, hi0,
+                           lo1, hi1, xf.p, bcnt.p);
+        hipLaunchKernelGGL(k_brd_scan, dim3(1), dim3(1024), 0, s, nb, bcnt.p, gnall.p + w, cap,
+                           gnall.p + nsw + 1);
+        hipLaunchKernelGGL(k_brd_scatter, dim3(nb), dim3(BRD_T), 0, s, gnall.p + w, bcnt.p, cap,
+                           nlocal, d, lo0, hi0, lo1, hi1, box.prd[d], xf.p, vr.p, en.p, ty.p,
+                           gowner.p, gimg.p, pc ? gsrc.p : (int *)nullptr,
+                           mp ? vel.p : (double4 *)nullptr, mp ? rm.p : (double *)nullptr,
+                           mp ? cvv.p : (double *)nullptr, mp ? cg.p : (double4 *)nullptr);
+        w += 2;
+      }
+#else
       for (int d = 0; d < ndim; d++) {
         if (!cfg.periodic[d]) continue;  // sendneed = 0 across a non-periodic boundary
         const int *const nlast = gnall.p + w;  // both swaps scan the atoms before this dim
@@ -1074,6 +1100,7 @@ struct sph_engine {
                              gnall.p + nsw + 1);
         }
       }
+#endif
       SPH_HIP_TRY(hipMemcpyAsync(h_small, gnall.p, (nsw + 2) * sizeof(int),
                                  hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));

@@ -344,6 +344,179 @@ static __global__ void k_append_ghosts_dev(
   }
 }
 
+// ---- one brick's borders, one dimension in three launches ---------------------------------
+// CommBrick::borders (comm_brick.cpp:733-800) for the two swaps of a periodic dimension:
+// both scan atoms [0, n) (owned + earlier dimensions' ghosts, n = *nalls), the lower swap
+// (x_d in [lo0, hi0], shifted +prd) appends its ghosts first, the upper one (x_d in [lo1,
+// hi1], -prd) after them, each in scan order.  k_brd_count: per block of BRD_CH atoms the
+// two swaps' counts; k_brd_scan (one block): their exclusive prefixes and the new atom
+// counts nalls[1] = n + T0, nalls[2] = n + T0 + T1; k_brd_scatter: the ghosts, in scan
+// order (a block-wide prefix per swap), as k_append_ghosts_dev writes them.
+constexpr int BRD_T = 256, BRD_IT = 4, BRD_CH = BRD_T * BRD_IT;
+__device__ __forceinline__ double brd_coord(const double4 &x, int d) {
+  return d == 0 ? x.x : (d == 1 ? x.y : x.z);
+}
+static __global__ void __launch_bounds__(BRD_T)
+k_brd_count(const int *__restrict__ nalls, int d, double lo0, double hi0, double lo1, double hi1,
+            const double4 *__restrict__ xf, int *__restrict__ bc) {
+  __shared__ int s0[BRD_T / 64], s1[BRD_T / 64];
+  const int n = nalls[0];
+  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
+  int c0 = 0, c1 = 0;
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    const int i = base + k;
+    if (i < n) {
+      const double c = brd_coord(xf[i], d);
+      c0 += (c >= lo0 && c <= hi0) ? 1 : 0;
+      c1 += (c >= lo1 && c <= hi1) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    c0 += __shfl_xor(c0, o, 64);
+    c1 += __shfl_xor(c1, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s0[threadIdx.x >> 6] = c0;
+    s1[threadIdx.x >> 6] = c1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int a = 0, b = 0;
+    for (int w = 0; w < BRD_T / 64; w++) {
+      a += s0[w];
+      b += s1[w];
+    }
+    bc[2 * blockIdx.x] = a;
+    bc[2 * blockIdx.x + 1] = b;
+  }
+}
+// exclusive prefix of nb (count0, count1) pairs, in place; one block of 1024 threads
+static __global__ void __launch_bounds__(1024)
+k_brd_scan(int nb, int *__restrict__ bc, int *__restrict__ nalls, int cap, int *__restrict__ ovf) {
+  __shared__ int s0[1024], s1[1024];
+  __shared__ int run0, run1;
+  if (threadIdx.x == 0) run0 = run1 = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nb; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    const int v0 = b < nb ? bc[2 * b] : 0, v1 = b < nb ? bc[2 * b + 1] : 0;
+    s0[threadIdx.x] = v0;
+    s1[threadIdx.x] = v1;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele
+      const int a0 = threadIdx.x >= o ? s0[threadIdx.x - o] : 0;
+      const int a1 = threadIdx.x >= o ? s1[threadIdx.x - o] : 0;
+      __syncthreads();
+      s0[threadIdx.x] += a0;
+      s1[threadIdx.x] += a1;
+      __syncthreads();
+    }
+    if (b < nb) {
+      bc[2 * b] = run0 + s0[threadIdx.x] - v0;
+      bc[2 * b + 1] = run1 + s1[threadIdx.x] - v1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      run0 += s0[1023];
+      run1 += s1[1023];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const long long n = nalls[0], t0 = n + run0, t1 = t0 + run1;
+    nalls[1] = (int)min(t0, (long long)cap);
+    nalls[2] = (int)min(t1, (long long)cap);
+    if (t1 > cap) *ovf = 1;
+  }
+}
+__device__ __forceinline__ void brd_put(int s, int g, int nlocal, int d, int pbc, double shift,
+                                        double4 *__restrict__ xf, double4 *__restrict__ vr,
+                                        double *__restrict__ en, int *__restrict__ ty,
+                                        int *__restrict__ gowner, int *__restrict__ gimg,
+                                        int *__restrict__ gsrc, double4 *__restrict__ vel,
+                                        double *__restrict__ rm, double *__restrict__ cv,
+                                        double4 *__restrict__ cg) {
+  double4 x = xf[s];
+  if (d == 0) x.x = x.x + shift;
+  else if (d == 1) x.y = x.y + shift;
+  else x.z = x.z + shift;
+  xf[g] = x;
+  vr[g] = vr[s];
+  en[g] = en[s];
+  ty[g] = ty[s];
+  int own, img;
+  if (s < nlocal) {
+    own = s;
+    img = 0;
+  } else {
+    own = gowner[s - nlocal];
+    img = gimg[s - nlocal];
+  }
+  gowner[g - nlocal] = own;
+  gimg[g - nlocal] = img_add(img, d, pbc);
+  if (gsrc) gsrc[g - nlocal] = s;
+  if (vel) {
+    const double4 v = vel[s], c = cg[s];
+    vel[g] = make_double4(v.x, v.y, v.z, vel[g].w);
+    rm[g] = rm[s];
+    cv[g] = cv[s];
+    cg[g] = make_double4(c.x, c.y, c.z, 0.0);
+  }
+}
+static __global__ void __launch_bounds__(BRD_T)
+k_brd_scatter(const int *__restrict__ nalls, const int *__restrict__ bc, int cap, int nlocal,
+              int d, double lo0, double hi0, double lo1, double hi1, double prd,
+              double4 *__restrict__ xf, double4 *__restrict__ vr, double *__restrict__ en,
+              int *__restrict__ ty, int *__restrict__ gowner, int *__restrict__ gimg,
+              int *__restrict__ gsrc, double4 *__restrict__ vel, double *__restrict__ rm,
+              double *__restrict__ cv, double4 *__restrict__ cg) {
+  __shared__ int s0[BRD_T], s1[BRD_T];
+  const int n = nalls[0], t0 = nalls[1];  // (t0 = n + the lower swap's count, capped)
+  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
+  unsigned f0 = 0, f1 = 0;  // the thread's items' flags
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    const int i = base + k;
+    if (i < n) {
+      const double c = brd_coord(xf[i], d);
+      if (c >= lo0 && c <= hi0) f0 |= 1u << k;
+      if (c >= lo1 && c <= hi1) f1 |= 1u << k;
+    }
+  }
+  const int c0 = __popc(f0), c1 = __popc(f1);
+  s0[threadIdx.x] = c0;
+  s1[threadIdx.x] = c1;
+  __syncthreads();
+  for (int o = 1; o < BRD_T; o <<= 1) {
+    const int a0 = threadIdx.x >= o ? s0[threadIdx.x - o] : 0;
+    const int a1 = threadIdx.x >= o ? s1[threadIdx.x - o] : 0;
+    __syncthreads();
+    s0[threadIdx.x] += a0;
+    s1[threadIdx.x] += a1;
+    __syncthreads();
+  }
+  int p0 = n + bc[2 * blockIdx.x] + s0[threadIdx.x] - c0;
+  int p1 = t0 + bc[2 * blockIdx.x + 1] + s1[threadIdx.x] - c1;
+  // (the ghosts are written after every read of this launch's sources: a ghost slot g >= n
+  // is never a source, i < n)
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    const int i = base + k;
+    if ((f0 >> k) & 1u) {
+      if (p0 < cap && p0 < t0)
+        brd_put(i, p0, nlocal, d, 1, prd, xf, vr, en, ty, gowner, gimg, gsrc, vel, rm, cv, cg);
+      p0++;
+    }
+    if ((f1 >> k) & 1u) {
+      if (p1 < cap) brd_put(i, p1, nlocal, d, -1, -prd, xf, vr, en, ty, gowner, gimg, gsrc, vel,
+                            rm, cv, cg);
+      p1++;
+    }
+  }
+}
+
 // forward_comm (atom_vec_meso.cpp:246-288): ghost <- owner (+image*prd on x), vest, rho, e
 // (and p/rho^2, carried in xf.w).  One add per coordinate: each hop adds exactly one
 // periodic shift to its own coordinate.

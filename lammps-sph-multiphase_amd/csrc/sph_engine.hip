@@ -224,6 +224,7 @@ struct sph_engine {
     int dim = 0, dir = 0, sendproc = 0, recvproc = 0, nsend = 0, nrecv = 0, firstrecv = 0;
     int pbc = 0;
     double lo = 0.0, hi = 0.0, shift = 0.0;
+    double lo_sel = 0.0, hi_sel = 0.0;  // (the selection's slab: empty without a send)
     bool remote = false;
     DBuf<int> list;
   };
@@ -578,7 +579,10 @@ struct sph_engine {
         // peers' are read back together below: one host sync per dimension
         nsel.reserve(2);
         sw.list.reserve(nlast > 0 ? nlast : 1);
-        if (sendflag && nlast > 0) {
+        if (SPH_BRD_FUSED) {
+          sw.lo_sel = sendflag ? sw.lo : 1.0;  // (no send: an empty slab)
+          sw.hi_sel = sendflag ? sw.hi : 0.0;
+        } else if (sendflag && nlast > 0) {
           flags.reserve(nlast);
           hipLaunchKernelGGL(k_slab_flags, dim3(blocks(nlast)), dim3(BLK), 0, s, nlast, d,
                              sw.lo, sw.hi, xf.p, flags.p);
@@ -594,6 +598,20 @@ struct sph_engine {
         }
       }
       Swap &a = *pair[0], &b = *pair[1];
+      if (SPH_BRD_FUSED) {  // both swaps' selections in three launches
+        const int nb = (nlast + BRD_CH - 1) / BRD_CH;
+        if (nb == 0) {
+          SPH_HIP_TRY(hipMemsetAsync(nsel.p, 0, 2 * sizeof(int), s));
+        } else {
+          bcnt.reserve(2 * (size_t)nb);
+          hipLaunchKernelGGL(k_brd_count, dim3(nb), dim3(BRD_T), 0, s, (const int *)nullptr, d,
+                             a.lo_sel, a.hi_sel, b.lo_sel, b.hi_sel, xf.p, bcnt.p, nlast);
+          hipLaunchKernelGGL(k_brd_scan, dim3(1), dim3(1024), 0, s, nb, bcnt.p, (int *)nullptr,
+                             0, (int *)nullptr, nsel.p);
+          hipLaunchKernelGGL(k_brd_lists, dim3(nb), dim3(BRD_T), 0, s, nlast, bcnt.p, d,
+                             a.lo_sel, a.hi_sel, b.lo_sel, b.hi_sel, xf.p, a.list.p, b.list.p);
+        }
+      }
       if (a.remote) {
         int h[4];
         tr->exchange_count2_dev(nsel.p, a.sendproc, a.recvproc, b.sendproc, b.recvproc, s, h);

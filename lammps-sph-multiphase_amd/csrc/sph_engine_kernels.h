@@ -358,9 +358,9 @@ __device__ __forceinline__ double brd_coord(const double4 &x, int d) {
 }
 static __global__ void __launch_bounds__(BRD_T)
 k_brd_count(const int *__restrict__ nalls, int d, double lo0, double hi0, double lo1, double hi1,
-            const double4 *__restrict__ xf, int *__restrict__ bc) {
+            const double4 *__restrict__ xf, int *__restrict__ bc, int nh = 0) {
   __shared__ int s0[BRD_T / 64], s1[BRD_T / 64];
-  const int n = nalls[0];
+  const int n = nalls ? nalls[0] : nh;  // (bricks: the host's count)
   const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
   int c0 = 0, c1 = 0;
 #pragma unroll
@@ -394,7 +394,8 @@ k_brd_count(const int *__restrict__ nalls, int d, double lo0, double hi0, double
 }
 // exclusive prefix of nb (count0, count1) pairs, in place; one block of 1024 threads
 static __global__ void __launch_bounds__(1024)
-k_brd_scan(int nb, int *__restrict__ bc, int *__restrict__ nalls, int cap, int *__restrict__ ovf) {
+k_brd_scan(int nb, int *__restrict__ bc, int *__restrict__ nalls, int cap, int *__restrict__ ovf,
+           int *__restrict__ nsel = nullptr) {
   __shared__ int s0[1024], s1[1024];
   __shared__ int run0, run1;
   if (threadIdx.x == 0) run0 = run1 = 0;
@@ -424,7 +425,10 @@ k_brd_scan(int nb, int *__restrict__ bc, int *__restrict__ nalls, int cap, int *
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && nsel) {  // (bricks: the two send counts)
+    nsel[0] = run0;
+    nsel[1] = run1;
+  } else if (threadIdx.x == 0) {
     const long long n = nalls[0], t0 = n + run0, t1 = t0 + run1;
     nalls[1] = (int)min(t0, (long long)cap);
     nalls[2] = (int)min(t1, (long long)cap);
@@ -514,6 +518,45 @@ k_brd_scatter(const int *__restrict__ nalls, const int *__restrict__ bc, int cap
                             rm, cv, cg);
       p1++;
     }
+  }
+}
+
+// bricks (CommBrick::borders' sendlists, comm_brick.cpp:733-800): the two swaps' send lists
+// of a dimension, indices in scan order -- k_brd_count / k_brd_scan (nsel) then this
+static __global__ void __launch_bounds__(BRD_T)
+k_brd_lists(int n, const int *__restrict__ bc, int d, double lo0, double hi0, double lo1,
+            double hi1, const double4 *__restrict__ xf, int *__restrict__ list0,
+            int *__restrict__ list1) {
+  __shared__ int s0[BRD_T], s1[BRD_T];
+  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
+  unsigned f0 = 0, f1 = 0;
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    const int i = base + k;
+    if (i < n) {
+      const double c = brd_coord(xf[i], d);
+      if (c >= lo0 && c <= hi0) f0 |= 1u << k;
+      if (c >= lo1 && c <= hi1) f1 |= 1u << k;
+    }
+  }
+  const int c0 = __popc(f0), c1 = __popc(f1);
+  s0[threadIdx.x] = c0;
+  s1[threadIdx.x] = c1;
+  __syncthreads();
+  for (int o = 1; o < BRD_T; o <<= 1) {
+    const int a0 = threadIdx.x >= o ? s0[threadIdx.x - o] : 0;
+    const int a1 = threadIdx.x >= o ? s1[threadIdx.x - o] : 0;
+    __syncthreads();
+    s0[threadIdx.x] += a0;
+    s1[threadIdx.x] += a1;
+    __syncthreads();
+  }
+  int p0 = bc[2 * blockIdx.x] + s0[threadIdx.x] - c0;
+  int p1 = bc[2 * blockIdx.x + 1] + s1[threadIdx.x] - c1;
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    if ((f0 >> k) & 1u) list0[p0++] = base + k;
+    if ((f1 >> k) & 1u) list1[p1++] = base + k;
   }
 }
 

@@ -144,6 +144,26 @@ def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     compare(out, ref)
 
 
+@pytest.mark.parametrize("pg", [(2, 2, 1), (1, 2, 2)])
+def test_bricks_nonperiodic(gpu, sph_amd, pg):
+    """Bricks with a non-periodic y: the bricks at the y faces send nothing across them
+    (sendneed = 0, comm_brick.cpp:226-274) -- the borders' selection runs with an empty slab
+    for that swap, while the inner y face between bricks still exchanges."""
+    s = at_rest(c2_system(12))
+    s.periodic = (1, 0, 1)
+    s.boxlo[1] -= 2.0
+    s.boxhi[1] += 2.0
+    ph = po.c2_physics()
+    ph.every = 4
+    ref = po.RefRun(s, ph)
+    ref.setup()
+    ref.run(9)
+    out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9)
+    assert sum(nloc) == s.n
+    assert np.array_equal(counts, ref.numneigh_full())
+    compare(out, ref)
+
+
 @pytest.mark.parametrize("path", PATHS)
 def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     s = at_rest(c3_system(12))

@@ -954,10 +954,49 @@ template <class F, int... I>
 __device__ __forceinline__ void blk_steps_(F &&f, std::integer_sequence<int, I...>) {
   (void)(f(std::integral_constant<int, I>{}) && ...);
 }
+// Lane map of the pair passes (SPH_BLK_LMAP, G = 8): a ds_read_b128 serves a wave in four
+// 16-lane groups, {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32; each group holds
+// two whole rows instead of halves of four, so the 16 records it reads are two runs of 8
+// consecutive entries of two rows (consecutive union slots where a row's neighbours run
+// along a bin row: distinct banks) -- rows r = 0..3 of a half at lanes {0-3,12-15},
+// {20-27}, {4-11}, {16-19,28-31}.  A row's lanes are closed under xor 1, 2 and 12, so its
+// sums stay butterflies.
+#ifndef SPH_BLK_LMAP
+#define SPH_BLK_LMAP 0
+#endif
+template <int G>
+__device__ __forceinline__ int blk_lrow(int tid) {  // the workgroup-local row of thread tid
+  if constexpr (G == 8 && SPH_BLK_LMAP) {
+    const int p = tid & 31;
+    const int r = p < 4 ? 0 : p < 12 ? 2 : p < 16 ? 0 : p < 20 ? 3 : p < 28 ? 1 : 3;
+    return ((tid >> 5) << 2) + r;
+  } else {
+    return tid / G;
+  }
+}
+template <int G>
+__device__ __forceinline__ int blk_llane(int tid) {  // its lane in the row (entry order)
+  if constexpr (G == 8 && SPH_BLK_LMAP) {
+    const int p = tid & 31;
+    return p < 4 ? p : p < 12 ? p - 4 : p < 16 ? p - 8 : p < 20 ? p - 16 : p < 28 ? p - 20 : p - 24;
+  } else {
+    return tid & (G - 1);
+  }
+}
+template <int G>
+__device__ __forceinline__ double blk_row_sum(double v) {
+  if constexpr (G == 8 && SPH_BLK_LMAP) {
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    return v + __shfl_xor(v, 12, 64);
+  } else {
+    return group_sum<G>(v);
+  }
+}
 template <int G>
 __device__ __forceinline__ int wave_max_count(int c) {
 #pragma unroll
-  for (int d = G; d < 64; d <<= 1) c = max(c, __shfl_xor(c, d, 64));
+  for (int d = (G == 8 && SPH_BLK_LMAP) ? 1 : G; d < 64; d <<= 1) c = max(c, __shfl_xor(c, d, 64));
   return __builtin_amdgcn_readfirstlane(c);
 }
 template <int G, int U, int NCH, class Load, class Body>
@@ -1037,7 +1076,7 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   const int nt1 = cf->ntypes + 1;
   const int b = (int)xcd_block(), tid = threadIdx.x;
   // (bperm: the block's rows in the build's length order, blk_row)
-  const int row = b * R + blk_row(bperm, b * R, tid / G), lane = tid & (G - 1);
+  const int row = b * R + blk_row(bperm, b * R, blk_lrow<G>(tid)), lane = blk_llane<G>(tid);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
   // n3: slots 1 .. nrow are the block's rows (q <= qn3); a row's entries among them are the
@@ -1123,10 +1162,10 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   } else {
     sw.walk(c, lane, [&](int q, bool) { pair(load(q)); });
   }
-  acc = group_sum<G>(acc);
+  acc = blk_row_sum<G>(acc);
   if (n3on) {  // (workgroup-uniform) the earlier rows' shares of this row
     __syncthreads();
-    acc += s_acc[tid / G];
+    acc += s_acc[blk_lrow<G>(tid)];
   }
   if (lane == 0 && live) {
     const double rho = ((cf->rho_keep >> it) & 1) ? vr[row].w
@@ -1281,7 +1320,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   const int qn3 = n3on ? blk_q(min(R, n - b * R), CQ) : -1;
   if (n3on)
     for (int t = tid; t < R * NA; t += NTH) s_acc[t] = 0.0;
-  const int row = b * R + blk_row(bperm, b * R, tid / G), lane = tid & (G - 1);
+  const int row = b * R + blk_row(bperm, b * R, blk_lrow<G>(tid)), lane = blk_llane<G>(tid);
   const bool live = row < n;
   const int rr = live ? row : n - 1;
   // loads first: the row's count, the union's atom ids, then the row's slots and the
@@ -1438,16 +1477,16 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     blk_walk2(sw, c, lane, load, pair);
   }
   if (TAIT) {
-    fx = group_sum<G>(fx);
-    fy = group_sum<G>(fy);
-    fz = group_sum<G>(fz);
-    D = group_sum<G>(D);
-    E = group_sum<G>(E);
+    fx = blk_row_sum<G>(fx);
+    fy = blk_row_sum<G>(fy);
+    fz = blk_row_sum<G>(fz);
+    D = blk_row_sum<G>(D);
+    E = blk_row_sum<G>(E);
   }
-  if (HEAT) EH = group_sum<G>(EH);
+  if (HEAT) EH = blk_row_sum<G>(EH);
   if (n3on) {  // (workgroup-uniform) the earlier rows' shares of this row
     __syncthreads();
-    const double *const a = s_acc + (tid / G) * NA;
+    const double *const a = s_acc + blk_lrow<G>(tid) * NA;
     if (TAIT) {
       fx += a[0];
       fy += a[1];

@@ -469,9 +469,14 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             int *__restrict__ ucnt, int *__restrict__ rcnt, unsigned short *__restrict__ snbr,
             int *__restrict__ icnt, unsigned short *__restrict__ snbi,
             int *__restrict__ ovf, int *__restrict__ umax, int cq, int *__restrict__ fcnt,
-            unsigned char *__restrict__ bperm) {
+            unsigned char *__restrict__ bperm, int *__restrict__ uilist,
+            int *__restrict__ uicnt, int *__restrict__ kcnt) {
   constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
   constexpr int RPW = R / NW, UG = U * G, WS = INNER ? 2 : 1;
+  // the INNER UNION (uilist != nullptr): the inner rows index a union of their own -- the
+  // atoms some inner row names, ~15 % fewer than the full union at C2 -- so the passes stage
+  // a smaller LDS image while the inner rows are live (more workgroups per CU)
+  const bool iu = INNER && !N3 && uilist != nullptr;
   static_assert(R <= 64 && R % 32 == 0, "one lane per row, rows in steps of 8 per wave");
   static_assert(UG <= 64, "a row's padding in one store");
   // the rows' hit words per chunk (full, inner); before the tests the same storage holds
@@ -480,6 +485,8 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   static_assert(SCH * R * WS * 8 >= BLK_MCAP, "the bin-row table fits the hit words");
   unsigned char *const s_rowof = reinterpret_cast<unsigned char *>(s_w);
   __shared__ unsigned long long s_used[SCH];
+  __shared__ unsigned long long s_usedi[INNER ? SCH : 1];  // iu: the inner union's words
+  __shared__ int s_upi[INNER ? SCH + 1 : 1];
   __shared__ unsigned short s_q[SCH][64];
   __shared__ unsigned long long s_keep[MCH];
   __shared__ int s_cpos[BLK_SCAP];
@@ -698,17 +705,23 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     }
     const unsigned long long full = (((unsigned long long)my_hi << 32) | my_lo) & ~sbit;
     const unsigned long long mine = full & keep;
+    const unsigned long long minei = (((unsigned long long)mi_hi << 32) | mi_lo) & keep;
     if (N3 && lane < R) fc += __popcll(full);
     if (lane < R) {
       if (INNER)
-        reinterpret_cast<ulonglong2 *>(s_w)[c * R + lane] =
-            make_ulonglong2(mine, (((unsigned long long)mi_hi << 32) | mi_lo) & keep);
+        reinterpret_cast<ulonglong2 *>(s_w)[c * R + lane] = make_ulonglong2(mine, minei);
       else
         s_w[c * R + lane] = mine;
     }
     unsigned long long u = mine;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) u |= __shfl_xor(u, d, 64);
+    if (INNER && iu) {
+      unsigned long long ui = minei;
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) ui |= __shfl_xor(ui, d, 64);
+      if (lane == 0) s_usedi[c] = ui;
+    }
     if (N3) {  // the rows have fixed slots: the union proper is the other used candidates
       const unsigned long long rm = __ballot(cid >= row0 && cid < row0 + nrow);
       u &= ~rm;
@@ -729,6 +742,12 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   const int ubase = N3 ? nrow : 0;
   u += ubase;
   if (N3 && tid < nrow) ulist[(size_t)b * ucap + tid] = row0 + tid;
+  int ui_tot = 0;  // iu: the inner union, numbered in candidate order like the full one
+  if (iu) {
+    const int v = tid < nch ? __popcll(s_usedi[tid]) : 0;
+    const int ex = blk_scan<NT>(v, s_sc, &ui_tot);
+    if (tid < nch) s_upi[tid] = ex;
+  }
   __syncthreads();
   // the union list, and each chunk's slot words: candidate l of chunk c, if used, has slot
   // ubase + s_upre[c] + 1 + (used candidates below it); a row (N3) has slot r + 1
@@ -740,15 +759,27 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     s_q[c][lane] = (unsigned short)blk_q(sl, cq);
     if ((used >> lane) & 1ull)
       ulist[(size_t)b * ucap + ubase + s_upre[c] + below] = s_cpos[c * 64 + lane];
+    if (iu) {
+      const unsigned long long usedi = s_usedi[c];
+      if ((usedi >> lane) & 1ull)
+        uilist[(size_t)b * ucap + s_upi[c] + blk_mbcnt(usedi)] = s_cpos[c * 64 + lane];
+    }
   }
-  if (tid == 0) {
+  if (tid == 0) {  // (the statistics words: k_blk_stats over these, not one atomic each --
+                   // 15k workgroups' atomics on one line serialise)
     ucnt[b] = u;
-    atomicMax(umax, u);
-    atomicMax(umax + 1, K);   // (stats: largest candidate set, sums of candidates / unions)
-    atomicAdd(umax + 2, K);
-    atomicAdd(umax + 3, u);
+    kcnt[b] = K;
+    if (iu) uicnt[b] = ui_tot;
   }
   __syncthreads();
+  // iu: the inner slots' words, over the candidates' atom ids (spent: the lists are written)
+  unsigned short(*const s_qi)[64] = reinterpret_cast<unsigned short(*)[64]>(s_cpos);
+  static_assert(sizeof(s_cpos) >= sizeof(unsigned short) * SCH * 64, "s_qi fits s_cpos");
+  if (iu) {
+    for (int c = wv; c < nch; c += NW)
+      s_qi[c][lane] = (unsigned short)blk_q(s_upi[c] + 1 + blk_mbcnt(s_usedi[c]), cq);
+    __syncthreads();
+  }
   if (BEXP == 3) return;
   // 5) the slot rows, full and inner: wave w writes rows w*RPW .. w*RPW + RPW-1 with LPR
   // lanes per row; lane `part` of a row writes the row's chunks part, part + LPR, .. (U*G
@@ -772,8 +803,10 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     const unsigned long long m = s_rowm[c];
     return word0(c, sel) & (v < nch ? m : ~m);
   };
-  auto qof = [&](int v, int bit) -> unsigned short {
-    return s_q[(N3 && v >= nch) ? v - nch : v][bit];
+  // the slot words of candidate `bit` of (virtual) word v in table qt: s_q, or s_qi for
+  // the inner rows over their own union
+  auto qof = [&](const unsigned short (*qt)[64], int v, int bit) -> unsigned short {
+    return qt[(N3 && v >= nch) ? v - nch : v][bit];
   };
   bool over = false;
   auto emit = [&](int sel, unsigned short *__restrict__ rows, int *__restrict__ cnt_out) {
@@ -782,6 +815,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
       for (int c = 0; c < nch; c++) cnt += __popcll(word0(c, sel));
     const int nchunk = min((cnt + UG - 1) / UG, sstride / UG);
     unsigned short *const out = rows + (size_t)(row0 + r) * sstride;
+    const unsigned short(*const qt)[64] = (iu && sel == 1) ? s_qi : s_q;
     int c = 0, acc = 0;  // (virtual) word c holds the entries from acc on
     unsigned long long w = (live && nv > 0) ? word(0, sel) : 0ull;
     for (int ch = part; ch < nchunk; ch += LPR) {
@@ -805,7 +839,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             while (m == 0ull) m = word(++cc, sel);
             const int bit = __ffsll((long long)m) - 1;
             m &= m - 1ull;
-            buf[l] |= (unsigned long long)qof(cc, bit) << (16 * q);
+            buf[l] |= (unsigned long long)qof(qt, cc, bit) << (16 * q);
           }
       if (U == 4) {
         ulonglong2 *const o = reinterpret_cast<ulonglong2 *>(out + e0);
@@ -1064,11 +1098,14 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
              const int *__restrict__ ty, double4 *__restrict__ vr,
              const Coefs *__restrict__ cf, int um, const unsigned short *__restrict__ snbi,
              const int *__restrict__ icnt, const int *__restrict__ moved, int n3,
-             const unsigned char *__restrict__ bperm) {
+             const unsigned char *__restrict__ bperm, const int *__restrict__ uilist,
+             const int *__restrict__ uicnt) {
   constexpr int NTH = R * G;
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
     rcnt = icnt;
+    ulist = uilist;  // (over their own union)
+    ucnt = uicnt;
   }
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
@@ -1175,19 +1212,24 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   }
 }
 
-// INNER rows for the pair passes, written at every rebuild: the slots of each full row
-// (cutneighsq = (cut + skin)^2) whose pair is within cut + m now, m = a quarter of the skin.
-// While no atom has moved m/2 since (k_initial_integrate / k_final_initial raise *moved
-// otherwise) every pair inside a pair style's cut is among them, so the passes walk ~128
-// instead of ~160 entries per row at C2 with identical terms (a dropped entry's kernel
-// weight is exactly zero); once an atom has moved further the passes fall back to the full
-// rows until the next rebuild.  The slots keep their full-row order (rank by ballot within
-// the row's G lanes); tails are padded with the sentinel like the full rows.
-// Refresh (cond != nullptr; one workgroup per several blocks, grid-stride): only if *cond
-// is set -- an atom moved more than half the margin since the rows were written -- the rows
-// are derived again from the full rows at the current positions and x0 (the owned rows'
-// reference positions) takes them; *zero (the next step's flag) is cleared either way.  The
-// pair passes then walk inner rows again instead of the full rows for the rest of the build.
+// INNER rows for the pair passes: the entries of each full row (cutneighsq = (cut + skin)^2)
+// whose pair is within cut + m now, m = a sixteenth of the skin, over the block's INNER UNION
+// (the atoms some inner row names, renumbered in full-union order).  While no atom has moved
+// m/2 since (k_initial_integrate / k_final_initial raise *moved otherwise) every pair inside
+// a pair style's cut is among them, so the passes walk ~115 instead of ~155 entries per row
+// at C2 with identical terms (a dropped entry's kernel weight is exactly zero) and stage
+// ~15 % fewer union records; once an atom has moved further the passes fall back to the full
+// rows and union until the next rebuild.  Each row keeps its full-row order (rank by ballot
+// within the row's G lanes); tails are padded with the sentinel like the full rows.
+// Written by k_blk_build's second ballot at a rebuild; here when the bitmap build took the
+// rebuild (k_blk_neigh, no inner ballot), and for a refresh (cond != nullptr; one workgroup
+// per several blocks, grid-stride): only if *cond is set -- an atom moved more than half the
+// margin since the rows were written -- the rows and inner unions are derived again from the
+// full rows at the current positions and x0 (the owned rows' reference positions) takes
+// them; *zero (the next step's flag) is cleared either way.  The pair passes then walk inner
+// rows again instead of the full rows for the rest of the build.
+// Two walks per block: the hits mark a bitmap over the full union's slots; its prefix
+// numbers the inner union; the second walk writes the rows in that numbering.
 template <int R, int G, int U, int NCH, bool NT1, int CQ>
 __global__ void __launch_bounds__(R * G)
 k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
@@ -1195,12 +1237,18 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             const double4 *__restrict__ xf, const int *__restrict__ ty,
             const Coefs *__restrict__ cf, unsigned short *__restrict__ snbi,
             int *__restrict__ icnt, int um, const int *__restrict__ cond,
-            int *__restrict__ zero, double4 *__restrict__ x0) {
+            int *__restrict__ zero, double4 *__restrict__ x0, int *__restrict__ uilist,
+            int *__restrict__ uicnt, int *__restrict__ umax) {
   constexpr int NTH = R * G;
+  constexpr int NWD = (BLK_UCAP + 1 + 31) / 32;       // bitmap words over slots 0 .. BLK_UCAP
+  constexpr int WPT = (NWD + NTH - 1) / NTH;          // consecutive words per thread (scan)
   if (zero && blockIdx.x == 0 && threadIdx.x == 0) *zero = 0;
   if (cond && *cond == 0) return;  // (workgroup-uniform)
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ double s_c[NT1 ? 1 : NT2];
+  __shared__ unsigned s_bm[NWD];
+  __shared__ int s_pre[NWD];
+  __shared__ int s_w[NTH / 64];
   const int tid = threadIdx.x;
   const int nt1 = cf->ntypes + 1;
   if (!NT1)
@@ -1220,7 +1268,8 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     double2 *const s_xy = reinterpret_cast<double2 *>(blk_smem);
     double *const s_z = reinterpret_cast<double *>(blk_smem + (size_t)(um + 1) * 16);
     unsigned char *const s_t = blk_smem + (size_t)(um + 1) * 24;
-    __syncthreads();  // (the previous block's image is no longer read)
+    const int nw = (u + 1 + 31) >> 5;
+    __syncthreads();  // (the previous block's image and bitmap are no longer read)
     for (int p = tid; p < u; p += NTH) {
       const int j = ul[p];
       const double4 x = xf[j];
@@ -1228,6 +1277,7 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       s_z[p + 1] = x.z;
       if (!NT1) s_t[p + 1] = (unsigned char)ty[j];
     }
+    for (int w = tid; w < nw; w += NTH) s_bm[w] = 0u;
     if (tid == 0) {
       s_xy[0] = make_double2(1e100, 1e100);
       s_z[0] = 1e100;
@@ -1235,18 +1285,68 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     }
     __syncthreads();
     const double c1 = NT1 ? cf->cutinsq[3] : 0.0;
-    const int grp = (tid & 63) / G;                   // the row's lane group in the wave
-    unsigned short *const out = snbi + (size_t)rr * sstride;
-    int base = 0;
-    sw.walk(c, lane, [&](int q, bool in) {
+    auto hit_of = [&](int q, bool in) {
       const int sj = blk_s<CQ>(q);
       const double2 xy = s_xy[sj];
       const double dx = xi.x - xy.x, dy = xi.y - xy.y, dz = xi.z - s_z[sj];
       const double rsq = dx * dx + dy * dy + dz * dz;
-      const bool hit = in && rsq < (NT1 ? c1 : s_c[it * nt1 + s_t[sj]]);
+      return in && live && rsq < (NT1 ? c1 : s_c[it * nt1 + s_t[sj]]);
+    };
+    // 1) the inner union: the full-union slots some inner pair names (uilist == nullptr:
+    // none, the rows keep the full union's numbering)
+    const bool ren = uilist != nullptr;
+    if (ren) sw.walk(c, lane, [&](int q, bool in) {
+      if (hit_of(q, in)) {
+        const int sj = blk_s<CQ>(q);
+        atomicOr(&s_bm[sj >> 5], 1u << (sj & 31));
+      }
+    });
+    __syncthreads();
+    int tot = 0;
+    if (ren) {
+      int v = 0;
+#pragma unroll
+      for (int k = 0; k < WPT; k++) {
+        const int w = tid * WPT + k;
+        v += w < nw ? __popc(s_bm[w]) : 0;
+      }
+      int ex = blk_scan<NTH>(v, s_w, &tot);
+#pragma unroll
+      for (int k = 0; k < WPT; k++) {
+        const int w = tid * WPT + k;
+        if (w < nw) {
+          s_pre[w] = ex;
+          ex += __popc(s_bm[w]);
+        }
+      }
+    }
+    __syncthreads();
+    auto rank = [&](int sj) {  // 0-based position of slot sj in the inner union
+      const unsigned w = s_bm[sj >> 5];
+      return s_pre[sj >> 5] + __popc(w & ((1u << (sj & 31)) - 1u));
+    };
+    if (ren)
+      for (int p = tid; p < u; p += NTH)
+        if ((s_bm[(p + 1) >> 5] >> ((p + 1) & 31)) & 1u)
+          uilist[(size_t)b * ucap + rank(p + 1)] = ul[p];
+    if (ren && tid == 0) {
+      uicnt[b] = tot;
+      if (umax) {
+        atomicMax(umax, tot);
+        atomicAdd(umax + 1, tot);
+      }
+    }
+    // 2) the rows in the inner numbering
+    const int grp = (tid & 63) / G;                   // the row's lane group in the wave
+    unsigned short *const out = snbi + (size_t)rr * sstride;
+    int base = 0;
+    sw.walk(c, lane, [&](int q, bool in) {
+      const bool hit = hit_of(q, in);
       const unsigned long long m = __ballot(hit);
       const unsigned g = (unsigned)(m >> (grp * G)) & ((1u << G) - 1u);
-      if (hit && live) out[blk_tpos<G, U>(base + __popc(g & ((1u << lane) - 1u)))] = (unsigned short)q;
+      if (hit)
+        out[blk_tpos<G, U>(base + __popc(g & ((1u << lane) - 1u)))] =
+            (unsigned short)(ren ? blk_q(rank(blk_s<CQ>(q)) + 1, CQ) : q);
       base += __popc(g);
     });
     if (live) {
@@ -1292,12 +1392,15 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
             const double4 *__restrict__ vr, const int *__restrict__ ty,
             const double *__restrict__ en, const Coefs *__restrict__ cf,
             double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-            double gz, int um, const int *__restrict__ blist, int cq,
-            const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,
-            const int *__restrict__ moved, int n3, const unsigned char *__restrict__ bperm) {
+            double gz, int um, int cq, const unsigned short *__restrict__ snbi,
+            const int *__restrict__ icnt, const int *__restrict__ moved, int n3,
+            const unsigned char *__restrict__ bperm, const int *__restrict__ uilist,
+            const int *__restrict__ uicnt) {
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
     rcnt = icnt;
+    ulist = uilist;  // (over their own union)
+    ucnt = uicnt;
   }
   constexpr bool TAIT = (MODE & M_TAIT) != 0;
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
@@ -1307,12 +1410,17 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ TaitPair s_tp[(TAIT && !NT1) ? NT2 : 1];
   __shared__ HeatPair s_hp[(HEAT && !NT1) ? NT2 : 1];
-  __shared__ double s_acc[R * NA];  // n3: the later rows' shares (k_blk_build N3)
+  __shared__ double s_acc[BLK_N3_BUILT ? R * NA : 1];  // n3: the later rows' shares
   const int nt1 = cf->ntypes + 1;
-  const int b = blist ? blist[blockIdx.x] : (int)xcd_block();
+  const int b = (int)xcd_block();
   const int tid = threadIdx.x;
   const int u = EXP == 3 ? 0 : ucnt[b];
-  if (!blist && u > um) return;  // (workgroup-uniform) left to the large-union launch
+  // the LDS image holds um union records (a multiple of 16); a larger union is walked in
+  // WINDOWS of um records: each window staged in turn, every row walked against it with the
+  // entries outside it read as the sentinel (workgroup-uniform; the host sizes um so that
+  // few blocks need it, and never with n3)
+  const int nwin = u > um ? (u + um - 1) / um : 1;
+  const int u0 = min(u, um);
   // n3: slots 1 .. nrow are the block's rows (q <= qn3); a row's entries among them are the
   // later rows, whose shares go to their accumulators (Newton's third law: F and the heat
   // term change sign, D and E do not)
@@ -1329,7 +1437,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   const int *const ul = ulist + (size_t)b * ucap;
   int jj[BLK_SP];
 #pragma unroll
-  for (int k = 0; k < BLK_SP; k++) jj[k] = tid + k * NTH < u ? ul[tid + k * NTH] : -1;
+  for (int k = 0; k < BLK_SP; k++) jj[k] = tid + k * NTH < u0 ? ul[tid + k * NTH] : -1;
   BlkSlots<G, U, NCH> sw;
   sw.load(snbr + (size_t)rr * sstride, c, lane);
   const double4 xi = xf[rr];
@@ -1352,7 +1460,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       if (TAIT) s_tp[t] = cf->tait[t];
       if (HEAT) s_hp[t] = cf->heat[t];
     }
-  unsigned char *const s_t = blk_smem + (size_t)((u + 16) >> 4) * cq * 16;
+  unsigned char *const s_t = blk_smem + (size_t)((u0 + 16) >> 4) * cq * 16;
 #pragma unroll
   for (int k = 0; k < BLK_SP; k++)
     if (jj[k] >= 0) {
@@ -1360,11 +1468,16 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       blk_put<HEAT>(blk_smem, sl, cq, qx[k], qv[k], HEAT ? ge[k] : 0.0);
       if (!NT1) s_t[blk_q(sl, cq)] = (unsigned char)gt[k];
     }
-  for (int p = tid + BLK_SP * NTH; p < u; p += NTH) {
-    const int j = ul[p];
-    blk_put<HEAT>(blk_smem, p + 1, cq, xf[j], vr[j], HEAT ? en[j] : 0.0);
-    if (!NT1) s_t[blk_q(p + 1, cq)] = (unsigned char)ty[j];
-  }
+  // window w's union records [w um, min(u, (w + 1) um)) from p0 on into slots 1, 2, ..
+  auto stage = [&](int w, int p0) {
+    const int base = w * um, end = min(u, base + um);
+    for (int p = base + p0; p < end; p += NTH) {
+      const int j = ul[p];
+      blk_put<HEAT>(blk_smem, p - base + 1, cq, xf[j], vr[j], HEAT ? en[j] : 0.0);
+      if (!NT1) s_t[blk_q(p - base + 1, cq)] = (unsigned char)ty[j];
+    }
+  };
+  stage(0, tid + BLK_SP * NTH);
   if (tid == 0) {
     blk_put_sentinel<HEAT>(blk_smem);
     if (!NT1) s_t[0] = 1;
@@ -1468,13 +1581,34 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       if (HEAT) atomicAdd(a + 5, -tEH);
     }
   };
-  if constexpr (NCH > 0 && SPH_BLK_WALK == 1) {
-    if (!n3on)
-      blk_walk3(sw, wave_max_count<G>(c), load, pair);
-    else
-      blk_walk2(sw, c, lane, load, pair);
+  auto walk = [&](auto ld) {
+    if constexpr (NCH > 0 && SPH_BLK_WALK == 1) {
+      if (!n3on)
+        blk_walk3(sw, wave_max_count<G>(c), ld, pair);
+      else
+        blk_walk2(sw, c, lane, ld, pair);
+    } else {
+      blk_walk2(sw, c, lane, ld, pair);
+    }
+  };
+  if (nwin == 1) {
+    walk(load);
   } else {
-    blk_walk2(sw, c, lane, load, pair);
+    // window w holds slots (w um, (w + 1) um] at 1 .. um: q (monotone in the slot, um a
+    // multiple of 16) shifts by qo = blk_q(w um); the others read the sentinel
+    const int qmax = blk_q(um, CQ);
+    for (int w = 0; w < nwin; w++) {
+      if (w > 0) {
+        __syncthreads();  // (the previous window is walked)
+        stage(w, tid);
+        __syncthreads();
+      }
+      const int qo = blk_q(w * um, CQ);
+      walk([&](int q) {
+        const int qq = q - qo;
+        return load((unsigned)(qq - 1) < (unsigned)qmax ? qq : 0);
+      });
+    }
   }
   if (TAIT) {
     fx = blk_row_sum<G>(fx);
@@ -1511,25 +1645,50 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   }
 }
 
-// blocks whose union exceeds the force pass's LDS image (um): their list for the second
-// launch
-static __global__ void k_blk_large(int nb, const int *__restrict__ ucnt, int um,
-                                   int *__restrict__ blist, int *__restrict__ nbig) {
+// blocks of a build whose union exceeds the force pass's LDS image (um records): the pass
+// walks them in windows of um union records (statistics only, sph_engine_stats blk_nbig)
+static __global__ void k_blk_count_big(int nb, const int *__restrict__ ucnt, int um,
+                                       int *__restrict__ nbig) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < nb && ucnt[b] > um) blist[atomicAdd(nbig, 1)] = b;
+  if (b < nb && ucnt[b] > um) atomicAdd(nbig, 1);
 }
-// k_blk_large right behind the build, without a host round trip: the force pass's image
-// size umf from the build's statistics words (mx[1] = largest union, mx[4] = sum of the
-// unions: ~1.25x the mean, whole 64-record steps, or `fixed` if > 0) into mx[6], the blocks
-// above it into blist (count mx[5])
-static __global__ void k_blk_large_dev(int nb, const int *__restrict__ ucnt, int fixed,
-                                       int *__restrict__ mx, int *__restrict__ blist) {
-  const int um = max(mx[1], 1);
-  int umf = min(um, ((int)(1.25 * ((double)mx[4] / nb)) + 63) / 64 * 64);
-  if (fixed > 0) umf = min(um, fixed);
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b == 0) mx[6] = umf;
-  if (b < nb && umf < um && ucnt[b] > umf) blist[atomicAdd(mx + 5, 1)] = b;
+
+// k_blk_build's statistics words from its per-block counts (one workgroup of 1024):
+// umax[0] largest union, [1] largest candidate set, [2] sum of candidates, [3] sum of
+// unions, [6] largest inner union, [7] sum of inner unions (uicnt == nullptr: none)
+static __global__ void __launch_bounds__(1024)
+k_blk_stats(int nb, const int *__restrict__ ucnt, const int *__restrict__ kcnt,
+            const int *__restrict__ uicnt, int *__restrict__ umax) {
+  __shared__ int s_r[6][16];
+  int v[6] = {0, 0, 0, 0, 0, 0};  // max u, max K, sum K, sum u, max ui, sum ui
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const int u = ucnt[b], k = kcnt[b], ui = uicnt ? uicnt[b] : 0;
+    v[0] = max(v[0], u);
+    v[1] = max(v[1], k);
+    v[2] += k;
+    v[3] += u;
+    v[4] = max(v[4], ui);
+    v[5] += ui;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1)
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+      const int o = __shfl_xor(v[q], d, 64);
+      v[q] = (q == 0 || q == 1 || q == 4) ? max(v[q], o) : v[q] + o;
+    }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+    for (int q = 0; q < 6; q++) s_r[q][w] = v[q];
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int q = threadIdx.x;
+    int r = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++)
+      r = (q == 0 || q == 1 || q == 4) ? max(r, s_r[q][k]) : r + s_r[q][k];
+    const int slot[6] = {0, 1, 2, 3, 6, 7};
+    umax[slot[q]] = r;
+  }
 }
 
 // ---- host-side launch helpers ----------------------------------------------------------
@@ -1566,13 +1725,17 @@ struct BlkArgs {
   int n = 0;            // owned rows
   int shape = 2;        // index into SPH_BLK_SHAPES
   int ucap = 0;         // union stride of ulist
-  int um = 0;           // largest union of the build
-  int umf = 0;          // force pass's LDS image (records); larger unions: second launch
-  int nbig = 0;         // blocks with a union larger than umf (listed in blist)
+  int um = 0;           // largest union of the build (the rho / inner passes' images)
+  int umf = 0;          // force pass's LDS image (records, a multiple of 16); larger
+                        // unions are walked in windows of umf records
   int sstride = 0;      // slot-row stride (entries)
   int exp = 0;          // study variants (SPH_EXP), 0 in production
   int cq = BLK_CH / 16;  // image chunk bytes / 16 (BLK_CHE / 16 with the heat term)
-  const int *ulist = nullptr, *ucnt = nullptr, *rcnt = nullptr, *blist = nullptr;
+  const int *ulist = nullptr, *ucnt = nullptr, *rcnt = nullptr;
+  // the union the inner rows index: their own (iu: k_blk_build / k_blk_inner renumbered
+  // them) or the full one
+  int *uilist = nullptr, *uicnt = nullptr;
+  bool iu = false;
   const unsigned short *snbr = nullptr;
   // inner rows (k_blk_inner) and the device flag that retires them; snbi == nullptr: none
   const unsigned short *snbi = nullptr;
@@ -1626,7 +1789,8 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
                         const int *ty, const double4 *xb, const int *tb, const int *qbeg,
                         const Coefs *cf, int ucap, int sstride, int *ulist, int *ucnt,
                         int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
-                        int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm) {
+                        int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm,
+                        int *uilist, int *uicnt, int *kcnt) {
 #ifdef SPH_STUDY
   auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, N3, 1>
           : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, N3, 2>
@@ -1639,30 +1803,33 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
 #endif
   hipLaunchKernelGGL(fn, dim3(blk_blocks(n, R)), dim3(256), 0, s, n, q, dim, xf, ty, xb, tb,
                      qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                     fcnt, bperm);
+                     fcnt, bperm, uilist, uicnt, kcnt);
+  hipLaunchKernelGGL(k_blk_stats, dim3(1), dim3(1024), 0, s, blk_blocks(n, R), ucnt, kcnt,
+                     uicnt, umax);
 }
 template <int R, int G, int U, bool N3>
 inline void blk_build_n(bool nt1, bool inner, hipStream_t s, int n, const QBins &q, int dim,
                         const double4 *xf, const int *ty, const double4 *xb, const int *tb,
                         const int *qbeg, const Coefs *cf, int ucap, int sstride, int *ulist,
                         int *ucnt, int *rcnt, unsigned short *snbr, int *icnt,
-                        unsigned short *snbi, int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm) {
+                        unsigned short *snbi, int *ovf, int *umax, int cq, int bexp, int *fcnt,
+                        unsigned char *bperm, int *uilist, int *uicnt, int *kcnt) {
   if (nt1 && inner)
     blk_build_t<R, G, U, true, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                          ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, bexp,
-                                         fcnt, bperm);
+                                         fcnt, bperm, uilist, uicnt, kcnt);
   else if (nt1)
     blk_build_t<R, G, U, true, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                           ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                                          bexp, fcnt, bperm);
+                                          bexp, fcnt, bperm, uilist, uicnt, kcnt);
   else if (inner)
     blk_build_t<R, G, U, false, true, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap, sstride,
                                           ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
-                                          bexp, fcnt, bperm);
+                                          bexp, fcnt, bperm, uilist, uicnt, kcnt);
   else
     blk_build_t<R, G, U, false, false, N3>(s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,
                                            sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf,
-                                           umax, cq, bexp, fcnt, bperm);
+                                           umax, cq, bexp, fcnt, bperm, uilist, uicnt, kcnt);
 }
 // n3: Newton-3 inside the blocks (rows first in the union, the later rows' share; fcnt gets
 // the full counts)
@@ -1671,13 +1838,14 @@ inline void blk_build(int shape, bool nt1, bool inner, bool n3, hipStream_t s, i
                       const double4 *xb, const int *tb, const int *qbeg, const Coefs *cf,
                       int ucap, int sstride, int *ulist, int *ucnt, int *rcnt,
                       unsigned short *snbr, int *icnt, unsigned short *snbi, int *ovf, int *umax,
-                      int cq, int bexp, int *fcnt, unsigned char *bperm) {
+                      int cq, int bexp, int *fcnt, unsigned char *bperm, int *uilist,
+                      int *uicnt, int *kcnt) {
 #ifdef SPH_STUDY
 #define SPH_IF_N3(R, G, U)                                                                  \
   if (n3)                                                                                 \
     blk_build_n<R, G, U, true>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,    \
                                sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
-                               bexp, fcnt, bperm);                                                \
+                               bexp, fcnt, bperm, uilist, uicnt, kcnt);                           \
   else
 #else
 #define SPH_IF_N3(R, G, U) (void)n3;
@@ -1688,7 +1856,7 @@ inline void blk_build(int shape, bool nt1, bool inner, bool n3, hipStream_t s, i
     SPH_IF_N3(R, G, U)                                                                    \
     blk_build_n<R, G, U, false>(nt1, inner, s, n, q, dim, xf, ty, xb, tb, qbeg, cf, ucap,   \
                                 sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq, \
-                                bexp, fcnt, bperm);                                               \
+                                bexp, fcnt, bperm, uilist, uicnt, kcnt);                          \
     break;
     SPH_BLK_SHAPES(SPH_CASE)
 #undef SPH_CASE
@@ -1706,7 +1874,7 @@ inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int
                                   (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um, k.snbi, k.icnt,
-                     k.moved, k.n3 ? 1 : 0, k.bperm);
+                     k.moved, k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt);
 }
 template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
@@ -1735,20 +1903,17 @@ inline void blk_rhosum(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, c
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
 inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
   auto fn = k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;
-  // main launch: every block whose union fits umf atoms; then the large-union blocks
-  const size_t lds = blk_lds(k.umf, k.cq, NT1);
-  const size_t ldsb = blk_lds(k.um, k.cq, NT1);
+  // one launch: every block, its union in windows of umf records where it exceeds the image
+  size_t lds = blk_lds(k.umf, k.cq, NT1);
+#ifdef SPH_STUDY  // (SPH_LDS_PAD: extra LDS per workgroup, an occupancy study)
+  if (const char *e = getenv("SPH_LDS_PAD")) lds += (size_t)atoi(e);
+#endif
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)std::max(lds, ldsb)));
+                                  (int)lds));
   hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
-                     a.de, a.gx, a.gy, a.gz, k.umf, (const int *)nullptr, k.cq, k.snbi,
-                     k.icnt, k.moved, k.n3 ? 1 : 0, k.bperm);
-  if (k.nbig > 0)
-    hipLaunchKernelGGL(fn, dim3(k.nbig), dim3(R * G), ldsb, s, k.n, k.ulist, k.ucnt, k.ucap,
-                       k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo, a.de,
-                       a.gx, a.gy, a.gz, k.um, k.blist, k.cq, k.snbi, k.icnt, k.moved,
-                       k.n3 ? 1 : 0, k.bperm);
+                     a.de, a.gx, a.gy, a.gz, k.umf, k.cq, k.snbi, k.icnt, k.moved,
+                     k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt);
 }
 
 // the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum
@@ -1758,6 +1923,7 @@ struct BlkInnerRefresh {
   const int *cond = nullptr;
   int *zero = nullptr;
   double4 *x0 = nullptr;
+  int *umax = nullptr;  // (the inner unions' largest and sum, as k_blk_build's umax + 6, 7)
 };
 template <int R, int G, int U, int NCH, bool NT1>
 inline void blk_inner_t(hipStream_t s, const BlkArgs &k, const double4 *xf, const int *ty,
@@ -1771,7 +1937,8 @@ inline void blk_inner_t(hipStream_t s, const BlkArgs &k, const double4 *xf, cons
   const int nb = blk_blocks(k.n, R);
   hipLaunchKernelGGL(fn, dim3(rf.cond ? std::min(nb, 512) : nb), dim3(R * G), lds, s, k.n,
                      k.ulist, k.ucnt, k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, cf, snbi, icnt,
-                     k.um, rf.cond, rf.zero, rf.x0);
+                     k.um, rf.cond, rf.zero, rf.x0, k.iu ? k.uilist : nullptr,
+                     k.iu ? k.uicnt : nullptr, rf.umax);
 }
 template <int R, int G, int U>
 inline void blk_inner_s(bool nt1, hipStream_t s, const BlkArgs &k, const double4 *xf,

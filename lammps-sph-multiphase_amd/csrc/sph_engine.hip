@@ -306,9 +306,12 @@ struct sph_engine {
   // block-staged path (production, sph_blk_kernels.h): per block of consecutive rows its
   // union of neighbour atoms (ulist, ucnt) and the rows' 16-bit slot rows (snbr)
   bool blk = false;
-  int blk_sh = 0, blk_um = 0, blk_umf = 0, blk_nbig = 0, blk_sstride = 0, blk_rowcap = 0;
-  DBuf<int> ulist, ucnt, bl;
+  int blk_sh = 0, blk_um = 0, blk_umf = 0, blk_sstride = 0, blk_rowcap = 0;
+  DBuf<int> ulist, ucnt, kcnt;  // (kcnt: the build's candidates per block, statistics)
   DBuf<unsigned short> snbr;
+  // the inner rows' own union (k_blk_build / k_blk_inner): a smaller LDS image for the passes
+  DBuf<int> uilist, uicnt;
+  bool blk_iu = false;  // (the inner rows index uilist; else the full union)
   // ... and the inner rows of the build (k_blk_inner: pairs within cut + inner_margin), the
   // owned positions they were written at and the flag that retires them (sc.x0 / sc.moved)
   DBuf<unsigned short> snbi;
@@ -1401,7 +1404,7 @@ struct sph_engine {
   bool build_blk() {
     const int n = nlocal;
     if (n == 0) return false;
-    mx.reserve(8);
+    mx.reserve(10);
     ccnt.reserve(n + 1);
     if (blk_rowcap == 0) blk_rowcap = std::max(list_stride, nbr_maxrow + nbr_maxrow / 4 + 16);
     // the SPH_BLK shape, then 32-row blocks (smaller unions), then 32-row blocks with the
@@ -1427,38 +1430,46 @@ struct sph_engine {
       const int nb = blk_blocks(n, sh.R);
       ulist.reserve((size_t)nb * BLK_UCAP);
       ucnt.reserve(nb);
-      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 7 * sizeof(int), s));
+      kcnt.reserve(nb);
+      SPH_HIP_TRY(hipMemsetAsync(mx.p, 0, 10 * sizeof(int), s));
       // k_blk_build (ballots, inner rows in the same pass); the bitmap walk k_blk_neigh for
       // the large candidate image (and in study builds, SPH_BUILD=0)
       const bool v2 = !big && study_int("SPH_BUILD", 1) != 0;
       // the inner rows' ballots inside the build (SPH_INNER_INLINE, study; default 1), or a
       // k_blk_inner pass over the full rows afterwards (build_inner)
       const bool want_inner = inner_margin > 0.0 && inner_inline();
-      if (v2 && want_inner) {
+      if (want_inner) {
         snbi.reserve((size_t)n * blk_sstride + 2 * chunk);
         icnt.reserve(n);
+        uilist.reserve((size_t)nb * BLK_UCAP);
+        uicnt.reserve(nb);
       }
       // Newton-3 inside the blocks (k_blk_build N3): the passes walk the stored rows (pcnt),
       // ccnt keeps the full counts
       blk_n3 = v2 && n3_env();
       if (blk_n3) pcnt.reserve(n + 1);
+      // the inner rows over their own union (not with N3: its rows-first union)
+#ifdef SPH_NO_IU  // (A/B builds: inner rows over the full union)
+      const bool iu = false;
+#else
+      const bool iu = v2 && want_inner && !blk_n3;
+#endif
       if (v2)
         blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
                   qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
                   blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
-                  study_int("SPH_BEXP", 0), ccnt.p, rowsort() ? bperm_buf(nb, sh.R) : nullptr);
+                  study_int("SPH_BEXP", 0), ccnt.p, rowsort() ? bperm_buf(nb, sh.R) : nullptr,
+                  iu ? uilist.p : nullptr, iu ? uicnt.p : nullptr, kcnt.p);
       else
         blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, mx.p, mx.p + 1,
                   blk_cq(), study_int("SPH_BEXP", 0));
       inner_written = v2 && want_inner;
+      blk_iu = iu;
       blk_perm = v2 && !blk_n3 && rowsort();
-      // the force pass's image size and its large-union blocks, then ONE read-back
-      bl.reserve(nb);
-      hipLaunchKernelGGL(k_blk_large_dev, dim3(blocks(nb)), dim3(BLK), 0, s, nb, ucnt.p,
-                         blkumf, mx.p, bl.p);
+      // the build's statistics: ONE read-back
       int *const hm = h_small;
-      SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 7 * sizeof(int), hipMemcpyDeviceToHost, s));
+      SPH_HIP_TRY(hipMemcpyAsync(hm, mx.p, 9 * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
       if (env_int("SPH_DEBUG", 0))
         fprintf(stderr,
@@ -1473,21 +1484,50 @@ struct sph_engine {
       if (hm[0] != 0) return 2;
       // the largest union's force-pass LDS image (+ the static coefficient tables) must fit
       // the CU's 160 KiB
-      const size_t lds_big = blk_lds(std::max(hm[1], 1), blk_cq(), nt1()) +
-                             (nt1() ? 0 : (sizeof(TaitPair) + sizeof(HeatPair)) * NT2);
-      if (lds_big > 160 * 1024 - 1024) return 2;
       blk_sh = shape;
       blk_um = std::max(hm[1], 1);
-      // the force pass's LDS image: ~1.25x the mean union (64-record steps), the blocks
-      // above it in a second launch (k_blk_large_dev)
-      blk_umf = hm[6];
-      blk_nbig = hm[5];
+      // the force pass's LDS image: sized to the union the passes stage (the inner one when
+      // the build wrote it), for as many workgroups per CU as fit; larger unions are walked
+      // in windows (k_blk_force)
+      if (iu)
+        blk_umf = choose_umf(hm[7], (double)hm[8] / nb);
+      else
+        blk_umf = choose_umf(blk_um, (double)hm[4] / nb);
+      hipLaunchKernelGGL(k_blk_count_big, dim3(blocks(nb)), dim3(BLK), 0, s, nb,
+                         iu ? uicnt.p : ucnt.p, blk_umf, mx.p + 9);
+      if (env_int("SPH_DEBUG", 0))
+        fprintf(stderr, "[sph] inner union max %d mean %.1f; force image %d records\n", hm[7],
+                (double)hm[8] / nb, blk_umf);
       return 1;
     }
     return 0;
   }
   // the union image's chunk size / 16 (sph_blk_kernels.h): with the heat term's e array
   int blk_cq() const { return ((force_mode & M_HEAT) ? BLK_CHE : BLK_CH) / 16; }
+  // The force pass's LDS image in union records (a multiple of 16) for unions of at most
+  // maxu records, meanu on average: the whole largest union if it fits three workgroups per
+  // CU (6 waves per SIMD); else three workgroups' image when the mean union fits it with
+  // 10 % to spare (the few larger unions walked in windows); else up to two workgroups'
+  // image.  SPH_TUNE_BLKUMF caps it (tests force the windowed walk that way).
+  int choose_umf(int maxu, double meanu) const {
+    const bool one = nt1();
+    const int cq = blk_cq();
+    const size_t stat = (one ? 0 : (sizeof(TaitPair) + sizeof(HeatPair)) * NT2) + 1024;
+    auto fits = [&](int w, int wgs) { return blk_lds(w, cq, one) + stat <= 163840 / wgs; };
+    auto cap = [&](int wgs) {
+      int w = 16;
+      while (w < BLK_UCAP && fits(w + 16, wgs)) w += 16;
+      return w;
+    };
+    const int m16 = std::max(16, (maxu + 15) / 16 * 16);
+    int umf;
+    if (fits(m16, 3)) umf = m16;
+    else if (blk_n3) umf = std::min(m16, cap(1));  // (study N3: no windows)
+    else if (meanu * 1.10 <= cap(3)) umf = cap(3);
+    else umf = std::min(m16, cap(2));
+    if (blkumf > 0 && !blk_n3) umf = std::min(umf, std::max(16, blkumf / 16 * 16));
+    return umf;
+  }
   BlkArgs blk_args() const {
     BlkArgs k;
     k.cq = blk_cq();
@@ -1497,8 +1537,6 @@ struct sph_engine {
     k.ucap = BLK_UCAP;
     k.um = blk_um;
     k.umf = blk_umf;
-    k.nbig = blk_nbig;
-    k.blist = bl.p;
     k.sstride = blk_sstride;
     k.ulist = ulist.p;
     k.ucnt = ucnt.p;
@@ -1510,6 +1548,9 @@ struct sph_engine {
       k.snbi = snbi.p;
       k.icnt = icnt.p;
       k.moved = moved_flag();
+      k.iu = blk_iu;
+      k.uilist = blk_iu ? uilist.p : ulist.p;
+      k.uicnt = blk_iu ? uicnt.p : ucnt.p;
     }
     return k;
   }
@@ -1563,10 +1604,13 @@ struct sph_engine {
     const BlkShape sh = blk_shape(blk_sh);
     snbi.reserve((size_t)nlocal * blk_sstride + 2 * sh.U * sh.G);
     icnt.reserve(nlocal);
+    uilist.reserve((size_t)blk_blocks(nlocal, sh.R) * BLK_UCAP);
+    uicnt.reserve(blk_blocks(nlocal, sh.R));
     moved.reserve(2);
     const size_t nx0 = (size_t)nlocal + (multi() ? nghost : 0);
     x0.reserve(nx0);
-    if (!inner_written) {
+    if (!inner_written) {  // (k_blk_inner writes the inner unions too)
+      blk_iu = true;
       BlkArgs k = blk_args();
       blk_inner(nt1(), s, k, xf.p, ty.p, dc, snbi.p, icnt.p);
     }
@@ -2481,7 +2525,7 @@ int sph_engine_destroy(sph_engine *e) {
   for (auto *b : {&e->ty, &e->ty2, &e->tag, &e->tag2, &e->gowner, &e->gimg, &e->sel, &e->nsel,
                   &e->bidx, &e->bidx2, &e->cnt, &e->off, &e->nbr, &e->mx,
                   &e->ccnt, &e->pcnt, &e->qbeg, &e->tb, &e->xpos, &e->sel2, &e->rows_in, &e->rows_bd, &e->tnbr,
-                  &e->tcnt, &e->ulist, &e->ucnt, &e->bl})
+                  &e->tcnt, &e->ulist, &e->ucnt, &e->kcnt, &e->uilist, &e->uicnt})
     b->release();
   for (auto *b : {&e->bkey, &e->bkey2}) b->release();
   for (auto *b : {&e->flags, &e->tmp, &e->cbs, &e->cbr, &e->flag2, &e->fl_in, &e->fl_bd}) b->release();
@@ -2934,7 +2978,12 @@ int sph_engine_stats_get(sph_engine *e, sph_engine_stats *st) {
   st->n_tait = e->nlaunch[T_TAIT];
   st->n_heat = e->nlaunch[T_HEAT];
   st->n_neigh = e->nlaunch[T_NEIGH];
-  st->blk_nbig = e->blk ? e->blk_nbig : 0;
+  st->blk_nbig = 0;
+  if (e->blk && e->mx.p) {  // (k_blk_count_big of the last block build)
+    SPH_HIP_TRY(hipMemcpyAsync(&st->blk_nbig, e->mx.p + 9, sizeof(int), hipMemcpyDeviceToHost,
+                               e->s));
+    SPH_HIP_TRY(hipStreamSynchronize(e->s));
+  }
   st->inner_rows = e->inner ? 1 : 0;
   st->inner_live = 0;
   if (e->inner && e->moved.p) {

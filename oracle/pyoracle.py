@@ -162,6 +162,8 @@ def lib():
                   "orc_dw_quintic3d"):
             getattr(L, n).argtypes = [_d]
             getattr(L, n).restype = _d
+        L.orc_set_quintic_factored.argtypes = [_i]
+        L.orc_set_quintic_factored.restype = None
         L.orc_rhosum_multiphase.argtypes = [_i, _i, _dp, _ip, _i, _dp, _dp, _dp, _lp, _ip,
                                             _dp]
         L.orc_taitwater_multiphase.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp,
@@ -452,10 +454,32 @@ def half_from_full(g: Ghosted, foff: np.ndarray, fneigh: np.ndarray):
 
 
 def _reverse_rows(off, nb):
-    out = nb.copy()
-    for i in range(len(off) - 1):
-        out[off[i]:off[i + 1]] = nb[off[i]:off[i + 1]][::-1]
-    return out
+    """every CSR row reversed"""
+    off = np.asarray(off, dtype=np.int64)
+    if nb.size == 0:
+        return nb.copy()
+    row = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    k = np.arange(nb.size, dtype=np.int64)
+    return nb[off[row] + off[row + 1] - 1 - k]
+
+
+def _rotate_rows(off, nb):
+    """every CSR row rotated by half its length"""
+    off = np.asarray(off, dtype=np.int64)
+    if nb.size == 0:
+        return nb.copy()
+    ln = np.diff(off)
+    row = np.repeat(np.arange(len(off) - 1), ln)
+    k = np.arange(nb.size, dtype=np.int64) - off[row]
+    L = ln[row]
+    return nb[off[row] + (k + L // 2) % np.maximum(L, 1)]
+
+
+def _reorder_rows(off, nb, how):
+    """how: True / "reverse" = each row reversed; "rotate" = each row rotated by half"""
+    if how is True or how == "reverse":
+        return _reverse_rows(off, nb)
+    return _rotate_rows(off, nb)
 
 
 def _nz(a):
@@ -589,10 +613,81 @@ def c3_physics(h=3.0) -> Physics:
                    alpha=a, heat_cut=t.copy())
 
 
-class RefRun:
+SPREAD_ORDERS = (True, "rotate")  # rows reversed; rows rotated by half their length
+SPREAD_ULP_SEED = 4242
+
+
+def ulp_perturbed(sysm: "System", seed=SPREAD_ULP_SEED) -> "System":
+    """a copy of the system with x, v, rho, e each moved by one ulp, random sign"""
+    s = sysm.copy()
+    rng = np.random.default_rng(seed)
+    x0 = s.x.copy()
+    for name in ("x", "v", "rho", "e"):
+        a = getattr(s, name)
+        a += np.spacing(a) * rng.choice((-1.0, 1.0), size=a.shape)
+    for d in range(s.dim):  # (an atom moved out of the box keeps its coordinate)
+        out = (s.x[:, d] < s.boxlo[d]) | (s.x[:, d] >= s.boxhi[d])
+        s.x[out, d] = x0[out, d]
+    return s
+
+
+class _Spread:
+    """spread=True: the run keeps three shadow runs of the same physics, stepped with it --
+    every list row reversed, every row rotated (SPREAD_ORDERS), and the inputs moved by one
+    ulp (ulp_perturbed); spread(k) is, per element of field k, the largest distance of their
+    results from this run's: how far the reference's own result moves under a reordered
+    summation or last-bit changes of its terms (the tests' elementwise bar).
+    Reordering alone misses elements whose reference sum happens to be order-insensitive
+    while its terms cancel (a C5 colour-gradient tail, a C3 atom between two phases: spread
+    < 1e-18 absolute, where the engine's terms -- v_rsq/v_rcp seeds with a Newton step, the
+    factored quintic -- differ from the reference's in their last bits)."""
+
+    def _init_spread(self, spread, make, make_ulp, kernel_form=False):
+        self.alts = []
+        self.qfact = False
+        if spread:
+            # spread="lean" (the 1M tests): one reordering + the ulp shadow
+            for how in (SPREAD_ORDERS[:1] if spread == "lean" else SPREAD_ORDERS):
+                a = make()
+                a.rev = how
+                self.alts.append(a)
+            self.alts.append(make_ulp())
+            if kernel_form:  # (C5: the quintic dW evaluated factored, orc_set_quintic_factored)
+                a = make()
+                a.qfact = True
+                self.alts.append(a)
+
+    def _qf(self, on):
+        if self.qfact:
+            lib().orc_set_quintic_factored(1 if on else 0)
+
+    def field(self, k):
+        s = self.s
+        if k in ("rho", "x", "v", "e", "rmass", "cv"):
+            return getattr(s, k)
+        return getattr(self, k)
+
+    def spread(self, k):
+        """per-element spread of field k (None without shadow runs)"""
+        if not self.alts:
+            return None
+        want = np.asarray(self.field(k), dtype=np.float64)
+        out = np.zeros_like(want)
+        used = 0
+        for a in self.alts:
+            # (a shadow whose fix phase_change took another decision -- a candidate's
+            # temperature within its last bits of the threshold -- is left out)
+            if a.s.n != self.s.n or not np.array_equal(a.s.type, self.s.type):
+                continue
+            out = np.maximum(out, np.abs(np.asarray(a.field(k), dtype=np.float64) - want))
+            used += 1
+        return out if used else None
+
+
+class RefRun(_Spread):
     """Owned state + the reference's per-step sequence, computed by the C restatement."""
 
-    def __init__(self, sysm: System, ph: Physics):
+    def __init__(self, sysm: System, ph: Physics, spread=False):
         self.s = sysm.copy()
         self.ph = ph
         nt = sysm.ntypes
@@ -606,6 +701,13 @@ class RefRun:
         self.last_build = 0
         self.dtf = 0.5 * ph.dt
         self.B = None if ph.rho0 is None else ph.c0 * ph.c0 * ph.rho0 / 7.0
+        # rev: the same run with every full-list row (and so every half row) reversed (True)
+        # or shuffled (an int seed) -- the reference's own result under a reordered summation
+        # (the tests' elementwise bar)
+        self.rev = False
+        self.rev_builds = 0
+        self._init_spread(spread, lambda: RefRun(sysm, ph),
+                          lambda: RefRun(ulp_perturbed(sysm), ph))
 
     # -- helpers -------------------------------------------------------------------------
     def _build(self):
@@ -615,6 +717,9 @@ class RefRun:
         self.image = getattr(self, "image", np.zeros((s.n, 3), np.int64)) + pbc_images(s, x0)
         self.g = borders(s, self.cutneighmax)
         self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
+        if self.rev:  # (list rows reordered: the reference's own reordering spread)
+            self.fnb = _reorder_rows(self.foff, self.fnb, self.rev)
+            self.rev_builds += 1
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
         # ghost copies of the border-packed per-atom fields
         self.vest_all = self.g.gather(self.vest)
@@ -671,6 +776,8 @@ class RefRun:
         self.vest_all[:self.s.n] = self.vest
         self._force()
         self.last_build = 0
+        for a in self.alts:
+            a.setup()
 
     def _meso_mask(self):
         """fix meso's group: every type not under meso/stationary (0 = all)"""
@@ -702,6 +809,8 @@ class RefRun:
             if sm:
                 L.orc_meso_stationary(s.n, self.dtf, s.type, sm, s.rho, self.drho, s.e,
                                       self.de)
+        for a in self.alts:
+            a.run(nsteps)
 
     def numneigh_full(self):
         return np.diff(self.foff).astype(np.int32)
@@ -923,7 +1032,7 @@ def borders_bricks(sysm: System, cutghost: float, pg, x: np.ndarray | None = Non
     return out
 
 
-class MpRefRun:
+class MpRefRun(_Spread):
     """C5 Verlet (verlet.cpp:222-308) over the C restatement: initial_integrate (fix meso,
     rmass) -> [pre_exchange: fix phase_change] -> pbc/borders/lists or forward comm (comm
     vel yes: x, v, rho, cg, rmass, e, vest) -> rhosum/multiphase, colorgradient (owned rows;
@@ -932,7 +1041,7 @@ class MpRefRun:
     half list with Newton-3 -> reverse comm (f, de) -> final_integrate.  Atom order = tag
     order (new atoms appended, no sort)."""
 
-    def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None):
+    def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None, spread=False):
         self.s = sysm.copy()
         assert self.s.rmass is not None
         # procgrid: fix phase_change as it runs on a grid of ranks (each rank scans its owned
@@ -944,6 +1053,9 @@ class MpRefRun:
         # order, so a test can size its tolerance to how far the reference's own result moves
         # under reordering where a sum nearly cancels (ill-conditioned atoms)
         self.rev = False
+        self._init_spread(spread, lambda: MpRefRun(sysm, ph, cg=cg, procgrid=procgrid),
+                          lambda: MpRefRun(ulp_perturbed(sysm), ph, cg=cg, procgrid=procgrid),
+                          kernel_form=True)
         self.ph = ph
         nt = sysm.ntypes
         self.cns, self.cutneighmax = cutneighsq(nt, ph.cutmax(nt), ph.skin)
@@ -997,7 +1109,7 @@ class MpRefRun:
         self.g = borders(s, self.cutneighmax)
         self.foff, self.fnb = neigh_full(s.dim, self.g, s.ntypes, self.cns)
         if self.rev:
-            self.fnb = _reverse_rows(self.foff, self.fnb)
+            self.fnb = _reorder_rows(self.foff, self.fnb, self.rev)
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
         self._ghost_fields()
         if self.pg:
@@ -1007,7 +1119,7 @@ class MpRefRun:
                              np.zeros(bv.nghost, np.int32), np.zeros((bv.nghost, 3), np.int32))
                 bv.off, bv.nb = neigh_full(s.dim, gh, s.ntypes, self.cns)
                 if self.rev:
-                    bv.nb = _reverse_rows(bv.off, bv.nb)
+                    bv.nb = _reorder_rows(bv.off, bv.nb, self.rev)
                 bv.hoff, bv.hnb = half_from_full(gh, bv.off, bv.nb)
 
     def _forward(self):
@@ -1305,12 +1417,25 @@ class MpRefRun:
 
     def setup(self):
         self.step = 0
+        self._qf(True)
         self._build()
         lib().orc_meso_setup(self.s.n, self.s.v, self.vest)   # FixMeso::setup_pre_force
         self._force()
+        self._qf(False)
         self.last_build = 0
+        for a in self.alts:
+            a.setup()
 
     def run(self, nsteps):
+        self._qf(True)
+        try:
+            self._run(nsteps)
+        finally:
+            self._qf(False)
+        for a in self.alts:
+            a.run(nsteps)
+
+    def _run(self, nsteps):
         s, L, ph = self.s, lib(), self.ph
         for _ in range(nsteps):
             self.step += 1

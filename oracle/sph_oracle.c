@@ -552,7 +552,21 @@ double orc_kernel_quintic2d(double r) {
   return 0.0;
 }
 
+/* Test aid (never the reference's arithmetic): orc_set_quintic_factored(1) evaluates dW/ds
+   in the factored form -5 (3-s)^4 + 30 (2-s)^4 - 75 (1-s)^4, which is the same polynomial
+   without the expanded form's cancellation near the pieces' ends (s -> 3: terms ~400 summing
+   to ~1e-4).  The reference's own colour gradients and multiphase forces carry that
+   cancellation's rounding (up to ~1e-10 relative on small elements); the tests' elementwise
+   bar takes its size from a shadow run in this mode (pyoracle _Spread). */
+static int g_quintic_factored = 0;
+void orc_set_quintic_factored(int on) { g_quintic_factored = on; }
+
 static double dw_quintic_poly(double s) {
+  if (g_quintic_factored) {
+    const double a = s < 3.0 ? 3.0 - s : 0.0, b = s < 2.0 ? 2.0 - s : 0.0,
+                 c = s < 1.0 ? 1.0 - s : 0.0;
+    return -5 * (a * a) * (a * a) + 30 * (b * b) * (b * b) - 75 * (c * c) * (c * c);
+  }
   if (s < 1) return -50 * pow(s, 4) + 120 * pow(s, 3) - 120 * s;
   if (s < 2) return 25 * pow(s, 4) - 180 * pow(s, 3) + 450 * pow(s, 2) - 420 * s + 75;
   if (s < 3.0) return -5 * pow(s, 4) + 60 * pow(s, 3) - 270 * pow(s, 2) + 540 * s - 405;

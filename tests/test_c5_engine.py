@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from conftest import rel_err
+from conftest import check_fields, rel_err
 from scenarios import bubble_physics, bubble_system
 
 TOL = 1e-10
@@ -61,9 +61,7 @@ def _compare(eng, ref, counts=True):
     assert np.array_equal(g["type"], s.type)
     if counts:
         assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
-    for k, want in (("x", s.x), ("v", s.v), ("rho", s.rho), ("e", s.e), ("rmass", s.rmass),
-                    ("cv", s.cv), ("cg", ref.cg), ("f", ref.f), ("de", ref.de)):
-        assert rel_err(g[k], want) < TOL, k
+    check_fields(g, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), TOL)
     return g
 
 
@@ -74,7 +72,7 @@ def test_engine_c5_vs_oracle(gpu, sph_amd, nx, dim, slab):
     from c5_util import mp_engine
     s = bubble_system(nx, dim=dim, slab=slab)
     ph = bubble_physics(nx, dim=dim, prob=0.3 if slab else 0.5, Tt=-1.0)
-    ref = po.MpRefRun(s, ph)
+    ref = po.MpRefRun(s, ph, spread=True)
     ref.setup()
     eng = mp_engine(sph_amd, s, ph)
     eng.setup()
@@ -94,7 +92,7 @@ def test_engine_c5_no_phase_change_every2(gpu, sph_amd):
     s = bubble_system(10)
     ph = bubble_physics(10, pc=False)
     ph.every = 2
-    ref = po.MpRefRun(s, ph)
+    ref = po.MpRefRun(s, ph, spread=True)
     ref.setup()
     eng = mp_engine(sph_amd, s, ph)
     eng.setup()

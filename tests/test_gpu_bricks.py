@@ -17,7 +17,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from conftest import rel_err
+from conftest import check_fields, rel_err
 from scenarios import c2_system, c3_system
 
 pytestmark = pytest.mark.gpu
@@ -117,13 +117,9 @@ def collect(engines, s):
 
 
 def compare(out, ref, tol=TOL):
-    s = ref.s
-    assert rel_err(out["rho"], s.rho) < tol
-    assert rel_err(out["f"], ref.f) < tol
-    assert rel_err(out["drho"], ref.drho) < tol
-    assert rel_err(out["de"], ref.de) < tol
-    assert rel_err(out["x"], s.x) < tol
-    assert rel_err(out["v"], s.v) < tol
+    """normwise 1e-10 and the elementwise bar (conftest.check_fields, the RefRun's reordering
+    spread)"""
+    check_fields(out, ref, ("rho", "f", "drho", "de", "x", "v"), tol)
 
 
 PATHS = [0, 1]   # 0 = block-staged LDS unions (production), 1 = row path (global gathers)
@@ -135,7 +131,7 @@ def test_bricks_c2_setup_and_run(gpu, sph_amd, pg, path):
     s = at_rest(c2_system(12))
     ph = po.c2_physics()
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)                       # rebuilds (and migrations) at steps 4 and 8
     out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9, path=path)
@@ -155,7 +151,7 @@ def test_bricks_nonperiodic(gpu, sph_amd, pg):
     s.boxhi[1] += 2.0
     ph = po.c2_physics()
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     out, counts, nloc = run_bricks(sph_amd, s, ph, pg, 9)
@@ -169,7 +165,7 @@ def test_bricks_c3_morris_heat(gpu, sph_amd, path):
     s = at_rest(c3_system(12))
     ph = po.c3_physics()
     ph.every = 3
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(7)
     out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 7, path=path)
@@ -186,7 +182,7 @@ def test_bricks_migration(gpu, sph_amd, path):
     ph = po.c2_physics()
     ph.dt = 5e-3
     ph.every = 5
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(40)
     side0 = s.x[:, 0] < 6.0
@@ -205,7 +201,7 @@ def test_bricks_2d(gpu, sph_amd, path):
     s = at_rest(c2_system(30, dim=2))
     ph = po.c2_physics(2.5)
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     out, counts, _ = run_bricks(sph_amd, s, ph, (2, 2, 1), 9, path=path)
@@ -246,7 +242,7 @@ def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving, path):
         s = at_rest(s)
     ph = po.c2_physics()
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     cfg = sph_amd.make_config(3, 1, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,
@@ -277,7 +273,7 @@ def test_bricks_halo_overlap(gpu, sph_amd, pg):
     s = at_rest(c2_system(14))
     ph = po.c2_physics()
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=1, overlap=True)  # (row path)
@@ -290,7 +286,7 @@ def test_rccl_loopback_overlap(gpu, sph_amd):
     s = c2_system(12)
     ph = po.c2_physics()
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     cfg = sph_amd.make_config(3, 1, s.boxlo, s.boxhi, s.periodic, s.mass, ph.skin, ph.dt,

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from conftest import elem_rel_err, rel_err
+from conftest import check_fields, elem_rel_err, rel_err
 from scenarios import c2_system, c3_system
 
 pytestmark = pytest.mark.gpu
@@ -34,19 +34,17 @@ def engine_for(sph_amd, s, ph: po.Physics, sort=1, every=None, kernel_path=0):
     return eng
 
 
+FIELDS = ("rho", "f", "drho", "de", "x", "v", "e")
+
+
 def compare(eng, ref, tol=TOL, path=None):
+    """normwise 1e-10 and SURVEY 8(d)'s elementwise bar (conftest.elem_ratio: 1e-10 per
+    element, or k x the oracle's own reordering spread where an element's sum cancels --
+    the RefRuns here carry their shadow runs, spread=True)"""
     if path is not None:  # the requested pair path really ran (no silent fallback)
         assert eng.stats()["staged"] == (1 if path == 0 else 0)
     got = eng.get_atoms()
-    s = ref.s
-    assert rel_err(got["rho"], s.rho) < tol
-    assert rel_err(got["f"], ref.f) < tol
-    assert rel_err(got["drho"], ref.drho) < tol
-    assert rel_err(got["de"], ref.de) < tol
-    assert rel_err(got["x"], s.x) < tol
-    assert rel_err(got["v"], s.v) < tol
-    if np.abs(s.e).max() > 0:
-        assert rel_err(got["e"], s.e) < tol
+    check_fields(got, ref, FIELDS, tol)
     return got
 
 
@@ -63,7 +61,7 @@ def test_setup_c2(gpu, sph_amd, sort, path, umf):
     large-image variant."""
     s = c2_system(12)
     ph = po.c2_physics()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     eng = engine_for(sph_amd, s, ph, sort=sort, kernel_path=path)
     if umf:
@@ -85,7 +83,7 @@ def test_setup_c2(gpu, sph_amd, sort, path, umf):
 def test_run_c2_with_rebuilds(gpu, sph_amd, path):
     s = c2_system(12)
     ph = po.c2_physics()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(25)                                # rebuilds at steps 10 and 20
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
@@ -106,7 +104,7 @@ def test_inner_rows_refresh(gpu, sph_amd):
     s.v *= 3.0
     ph = po.c2_physics()
     ph.every = 20
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     eng = engine_for(sph_amd, s, ph)
     eng.setup()
@@ -127,7 +125,7 @@ def test_run_c3_morris_heat(gpu, sph_amd, path):
     s = c3_system(10)
     ph = po.c3_physics()
     ph.every = 5
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(12)
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
@@ -142,7 +140,7 @@ def test_run_2d(gpu, sph_amd, path):
     s = c2_system(30, dim=2)
     ph = po.c2_physics(2.5)
     ph.every = 4
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
@@ -158,7 +156,7 @@ def test_every_step_rebuild_and_nstep(gpu, sph_amd, path):
     ph = po.c2_physics()
     ph.every = 1
     ph.rhosum_nstep = 3          # rhosum gated on ntimestep % nstep (pair_sph_rhosum.cpp:112)
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(7)
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
@@ -175,7 +173,7 @@ def test_nonperiodic_box(gpu, sph_amd, path):
     s.boxlo[1] -= 2.0
     s.boxhi[1] += 2.0
     ph = po.c2_physics()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(3)
     eng = engine_for(sph_amd, s, ph, kernel_path=path)
@@ -215,7 +213,7 @@ def test_timing_classes(gpu, sph_amd):
     are timed, the results do not depend on it, and "all" times every class."""
     s = c2_system(12)
     ph = po.c2_physics()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(12)
     eng = engine_for(sph_amd, s, ph)

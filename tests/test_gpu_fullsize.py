@@ -15,7 +15,7 @@ import pytest
 
 import pyoracle as po
 from c5_util import mp_engine, mp_state
-from conftest import rel_err
+from conftest import check_fields
 from scenarios import bubble_physics, bubble_system, c2_system, c3_system
 from test_gpu_engine import compare, engine_for
 
@@ -47,7 +47,7 @@ def test_full_size_fields(gpu, sph_amd, system, physics, umf):
     if umf:
         eng.tune(eng.TUNE_BLKUMF, umf)
     eng.setup()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread="lean")
     ref.setup()
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     assert eng.stats()["nghost"] == ref.g.nghost
@@ -68,7 +68,7 @@ def test_full_size_c5_phase_change(gpu, sph_amd):
     ph = bubble_physics(nx, prob=0.3, Tt=-1.0)
     eng = mp_engine(sph_amd, s, ph)
     eng.setup()
-    ref = po.MpRefRun(s, ph)
+    ref = po.MpRefRun(s, ph, spread=True)
     ref.setup()
     for k in range(6):
         if k:
@@ -79,8 +79,6 @@ def test_full_size_c5_phase_change(gpu, sph_amd):
         assert int(g["ninserted"]) == ref.ninserted, k
         assert np.array_equal(g["type"], rs.type), k
         assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full()), k
-        for f, want in (("x", rs.x), ("v", rs.v), ("rho", rs.rho), ("e", rs.e),
-                        ("rmass", rs.rmass), ("cv", rs.cv), ("cg", ref.cg), ("f", ref.f),
-                        ("de", ref.de)):
-            assert rel_err(g[f], want) < TOL, (k, f)
+        check_fields(g, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), TOL,
+                     where=k)
     assert ref.ninserted > 1000

@@ -23,7 +23,7 @@ import numpy as np
 import pytest
 
 import pyoracle as po
-from conftest import rel_err
+from conftest import check_fields, rel_err
 from ipc_rank import c2_scenario, c5_scenario
 
 pytestmark = pytest.mark.gpu
@@ -90,7 +90,7 @@ def test_processes_c2_rebuilds_migration(gpu, tmp_path, mode, pg):
     P = int(np.prod(pg))
     snaps = run_ranks(tmp_path, dict(scenario="c2", mode=mode, pg=list(pg), snap_steps=nsteps), P)
     s, ph = c2_scenario({})
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     side0 = s.x[:, 0] < 6.0
     done = 0
@@ -100,10 +100,7 @@ def test_processes_c2_rebuilds_migration(gpu, tmp_path, mode, pg):
         got = merge(snaps, k, s.n)
         assert sum(got["nlocal"]) == s.n
         assert np.array_equal(got["counts"], ref.numneigh_full()), k
-        rs = ref.s
-        for f, want in (("rho", rs.rho), ("f", ref.f), ("drho", ref.drho), ("de", ref.de),
-                        ("x", rs.x), ("v", rs.v)):
-            assert rel_err(got[f], want) < TOL, (k, f)
+        check_fields(got, ref, ("rho", "f", "drho", "de", "x", "v"), TOL, where=k)
     assert ((ref.s.x[:, 0] < 6.0) != side0).any(), "no atom migrated: migration not exercised"
     assert all(int(sn["staged"]) == 1 for sn in snaps)   # the block path ran on every rank
     assert all(int(sn["nghost"]) > 0 for sn in snaps)
@@ -120,7 +117,7 @@ def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx):
     spec = dict(scenario="c5", mode=mode, pg=list(pg), nx=nx, dim=dim, snap_steps=nsteps)
     snaps = run_ranks(tmp_path, spec, P)
     s, ph = c5_scenario(spec)
-    ref = po.MpRefRun(s, ph, procgrid=pg)
+    ref = po.MpRefRun(s, ph, procgrid=pg, spread=True)
     ref.setup()
     for k in [0] + nsteps:
         if k:
@@ -130,9 +127,6 @@ def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx):
         assert got["ninserted"] == ref.ninserted, k
         assert np.array_equal(got["type"], ref.s.type), k
         assert np.array_equal(got["counts"], ref.numneigh_full()), k
-        rs = ref.s
-        for f, want in (("x", rs.x), ("v", rs.v), ("rho", rs.rho), ("e", rs.e),
-                        ("rmass", rs.rmass), ("cv", rs.cv), ("cg", ref.cg), ("f", ref.f),
-                        ("de", ref.de)):
-            assert rel_err(got[f], want) < TOL, (k, f)
+        check_fields(got, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), TOL,
+                     where=k)
     assert ref.ninserted >= 2, "phase change did not insert across the run"

@@ -91,7 +91,7 @@ def test_engine_water_collapse_20_steps(gpu, sph_amd, path):
     from test_gpu_engine import compare, engine_for
     s = water_collapse_system()
     ph = water_collapse_physics()
-    ref = po.RefRun(s, ph)
+    ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(20)
     eng = engine_for(sph_amd, s, ph, kernel_path=path)

@@ -283,6 +283,17 @@ def _brick_cpu_worker(a):
     return (time.perf_counter() - t0) / steps + t_build / 10.0
 
 
+def host_cores():
+    """The cores this process may run on: its CPU affinity set, capped by OMP_NUM_THREADS
+    where that is set (the GPU pool's boxes give a GPU's job 16 cores of a larger machine,
+    whose os.cpu_count() shows them all)"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
 def cpu_baseline_cores(n_cpu, nproc=8, steps=2):
     """The C2 CPU baseline on nproc cores as LAMMPS runs it with MPI: the n_cpu^3 box split
     into nproc bricks (2x2x2 at 8, CommBrick::borders ghosts, pyoracle.borders_bricks), each
@@ -309,6 +320,7 @@ def cpu_baseline_cores(n_cpu, nproc=8, steps=2):
         per = pool.map(_brick_cpu_worker, work)
     t = max(per)
     return {"value": s.n / t, "unit": "particle-steps/s", "cores": nproc, "kind": "reference",
+            "host_cpus_visible": os.cpu_count(),
             "sample": f"reference USER-SPH compute code (oracle/_ref) on {s.n} particles split "
                       f"into {pg[0]}x{pg[1]}x{pg[2]} bricks, one process per brick running at "
                       f"the same time (LAMMPS' MPI decomposition): list build / 10 + rhosum + "
@@ -1305,8 +1317,9 @@ def main():
     attach_pmc_traffic(out, kname, bytes_tait * nloc, world, args)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n)
-        # beside it, the same reference code on 8 cores (one brick per process)
-        out["cpu_baseline_cores"] = cpu_baseline_cores(args.cpu_n, nproc=8)
+        # beside it, the same reference code on all the cores this process may use (one
+        # brick per process)
+        out["cpu_baseline_cores"] = cpu_baseline_cores(args.cpu_n, nproc=host_cores())
     if rank == 0:
         print(json.dumps(out), flush=True)
     with stdout_to_stderr():  # communicator teardown

@@ -9,6 +9,7 @@
 // (comm->reverse_comm, verlet.cpp:290-293) has nothing to carry and is skipped.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstring>
@@ -19,6 +20,7 @@
 #include "sph_comm.h"
 #include "sph_dispatch.h"
 #include "sph_blk_kernels.h"
+#include "sph_blk_build2.h"
 #include "sph_engine_kernels.h"
 #include "sph_engine_mp.h"
 #include "sph_ipc.h"
@@ -359,11 +361,18 @@ struct sph_engine {
     SPH_HIP_TRY(hipEventCreate(&e));
     return e;
   }
+  // A timed class of the step: a roctx range named after LAMMPS' Timer bucket it stands
+  // for (timer.h:19-20: Pair, Neigh, Comm, Modify; seen by rocprofv3 --marker-trace; a few
+  // tens of ns without a tool), and where timing asks for it a hipEvent pair
   struct Scope {
     sph_engine *e;
     EvPair p;
     bool on;
     Scope(sph_engine *eng, int cls) : e(eng), on(((eng->timing_mask >> cls) & 1) != 0) {
+      static const char *const bucket[T_NCLASS] = {"Pair:rhosum", "Pair:taitwater",
+                                                   "Pair:heatconduction", "Modify:integrate",
+                                                   "Comm", "Neigh"};
+      roctxRangePushA(bucket[cls]);
       if (!on) return;
       p.a = e->get_ev();
       p.b = e->get_ev();
@@ -371,6 +380,7 @@ struct sph_engine {
       SPH_HIP_TRY(hipEventRecord(p.a, e->s));
     }
     ~Scope() {
+      roctxRangePop();
       if (!on) return;
       (void)hipEventRecord(p.b, e->s);
       e->pending.push_back(p);
@@ -1424,7 +1434,10 @@ struct sph_engine {
     const int n = nlocal;
     const BlkShape sh = blk_shape(shape);
     const int chunk = sh.G * sh.U;
-    for (int attempt = 0; attempt < 2; attempt++) {
+    // k_blk_build2 (group candidate lists, sph_blk_build2.h): measured slower than
+    // k_blk_build (1.37 vs 1.11 ms at C2 1M, profiles/r05/README.md) -> study builds only
+    bool try2 = study_int("SPH_BUILD2", 0) != 0;
+    for (int attempt = 0; attempt < 3; attempt++) {
       blk_sstride = (std::max(blk_rowcap, 1) + chunk - 1) / chunk * chunk;
       snbr.reserve((size_t)n * blk_sstride + 2 * chunk);  // + the pair passes' prefetch pad
       const int nb = blk_blocks(n, sh.R);
@@ -1454,7 +1467,14 @@ struct sph_engine {
 #else
       const bool iu = v2 && want_inner && !blk_n3;
 #endif
-      if (v2)
+      // the group-list build (sph_blk_build2.h) unless a study variant needs k_blk_build
+      const bool v3 = v2 && try2 && !blk_n3 && !rowsort();
+      if (v3)
+        blk_build2(shape, nt1(), want_inner, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p,
+                   dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, icnt.p, snbi.p,
+                   mx.p, mx.p + 1, blk_cq(), iu ? uilist.p : nullptr, iu ? uicnt.p : nullptr,
+                   kcnt.p);
+      else if (v2)
         blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
                   qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
                   blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
@@ -1477,6 +1497,10 @@ struct sph_engine {
                 "candidates max %d mean %.1f\n",
                 shape, big ? " (large image)" : "", n, blk_rowcap, hm[0], hm[1], (double)hm[4] / nb, hm[2],
                 (double)hm[3] / nb);
+      if (hm[0] == (1 << 23)) {  // a group list outgrew k_blk_build2's: k_blk_build
+        try2 = false;
+        continue;
+      }
       if (hm[0] == (1 << 21)) {  // a row outgrew the slot-row stride
         blk_rowcap *= 2;
         continue;

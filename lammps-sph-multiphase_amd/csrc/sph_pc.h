@@ -186,7 +186,7 @@ k_pc_dmass_emit(int nins, const int *__restrict__ rows, const double *__restrict
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
     const double rsq = dx * dx + dy * dy + dz * dz;
     const int slot = atomicAdd(cnt, 1);
-    if (slot >= cap) continue;  // (cap is an upper bound: never taken)
+    if (slot >= cap) continue;  // (the host checks the count against cap after the launch)
     key[slot] = ((unsigned long long)(unsigned)j << 32) | (unsigned)k;
     val[slot] = p.to_mass * pc_w(p.dim, sqrt(rsq) * p.cutoff) / W;
   }
@@ -271,6 +271,13 @@ inline void pc_dmass_ordered(hipStream_t s, int nins, const int *rows, const dou
   hipLaunchKernelGGL(k_pc_dmass_emit<G>, dim3((unsigned)(((long long)nins * G + 255) / 256)),
                      dim3(256), 0, s, nins, rows, Wtot, ilist, off, nbr, xf, ty, rm, p, lstride,
                      lcnt, rk, k0.p, v0.p, cnt.p, cap);
+  // cap is an upper bound by construction; a stale bound must fail loudly, not drop a
+  // donor's share (dmass is the reference's to the bit)
+  int emitted = 0;
+  SPH_HIP_TRY(hipMemcpyAsync(&emitted, cnt.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  SPH_HIP_TRY(hipStreamSynchronize(s));
+  SPH_REQUIRE(emitted >= 0 && emitted <= cap, SPH_HIP_EOVERFLOW,
+              "fix phase_change: %d donations exceed the bound %lld", emitted, cap);
   size_t tb = 0;
   SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k0.p, k1.p, v0.p, v1.p, (int)cap,
                                                  0, 64, s));

@@ -142,8 +142,14 @@ void LAMMPS_NS::sph_hip_stage(LAMMPS *lmp, sph_hip_ctx *ctx, NeighList *list, in
   // theirs.  Device-list path (default): the list is built on the device from
   // the staged atoms with Neighbor::init's cutneighsq, (sqrt(pair->cutsq) + skin)^2
   // (neighbor.cpp:251-268), full_bin membership and half_from_full_newton's half.
+  // Only where the device list IS the list LAMMPS would hand this caller: not for a
+  // hybrid/overlay sub-style's skip list (pair_hybrid.cpp:428-485: types or type pairs the
+  // sub-style has no coefficients for are left out, and its coefficient tables are
+  // uninitialised there) and not with neigh_modify exclude (neighbor.cpp's exclusion tests) --
+  // those take the NeighList upload below.
   Pair *pair = lmp->force->pair;
-  if (g_device_lists && pair && pair->cutsq) {
+  const bool skip_list = list && (list->iskip || list->ijskip);
+  if (g_device_lists && pair && pair->cutsq && !skip_list && !lmp->neighbor->exclude_setting()) {
     const int nt = atom->ntypes;
     g_cns.assign((size_t)(nt + 1) * (nt + 1), 0.0);
     for (int i = 1; i <= nt; i++)

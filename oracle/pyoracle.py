@@ -239,6 +239,8 @@ def _bind_harness(path, pre):
     g("pack_restart").restype = _i
     g("set_device_lists").argtypes = [_i, _d]
     g("set_device_lists").restype = None
+    g("rhosum_skip").argtypes = [_i, _i, _i, _i, _dp, _ip, _dp, _dp, _i, _ip, _lp, _ip, _ip,
+                                 _ip, _dp]
     for n in ("kernel_quintic2d", "kernel_quintic3d", "dw_quintic2d", "dw_quintic3d"):
         g(n).argtypes = [_d]
         g(n).restype = _d
@@ -251,7 +253,7 @@ def _bind_harness(path, pre):
               "taitwater_morris", "heatconduction", "rhosum_multiphase", "taitwater_multiphase",
               "heatconduction_phasechange", "colorgradient", "surfacetension", "pc_new",
               "pc_pre_exchange", "pack_restart", "kernel_quintic2d", "kernel_quintic3d",
-              "dw_quintic2d", "dw_quintic3d", "set_device_lists"):
+              "dw_quintic2d", "dw_quintic3d", "set_device_lists", "rhosum_skip"):
         setattr(out, "ref_" + n, g(n))
     return out
 

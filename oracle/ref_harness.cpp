@@ -24,6 +24,7 @@
 #include <new>
 #include <string>
 #include <typeinfo>
+#include <vector>
 
 #include "mpi.h"
 #include "lammps.h"
@@ -457,6 +458,71 @@ int REFNAME(rhosum)(int dim, int ntypes, int nlocal, int nghost, const double *x
   p->list = l;
   SPH_INIT(p);
   {
+    DevListScope dl(w, p);
+    p->compute(0, 0);
+  }
+  for (int i = 0; i < nlocal; i++) rho[i] = w.lmp->atom->rho[i];
+  free_list(l);
+  return 0;
+}
+
+// PairSPHRhoSum as a hybrid/overlay sub-style with a SKIP list (pair_hybrid.cpp:428-485):
+// coefficients only where ijskip[i][j] == 0 (the others left as allocate() leaves them --
+// poisoned with NaN here, so a path that reads them shows), the caller's list holds the rows
+// of types with iskip == 0 (ilist) and only pairs with ijskip == 0, and carries the skip info
+// as NeighList::copy_skip_info sets it (neigh_list.cpp:204-215).
+int REFNAME(rhosum_skip)(int dim, int ntypes, int nlocal, int nghost, const double *x,
+                    const int *type, const double *mass, const double *cut, int inum,
+                    const int *ilist, const long *off, const int *neigh, const int *iskip,
+                    const int *ijskip, double *rho) {
+  World w(dim, ntypes, nlocal, nghost, 1, 0);
+  fill_atoms(w, x, NULL, rho, NULL, NULL, type, NULL);
+  for (int t = 0; t <= ntypes; t++) w.lmp->atom->mass[t] = mass[t];
+  HRhoSum *p = new HRhoSum(w.lmp);
+  p->nstep = 1;
+  p->allocate();
+  const double nan = std::nan("");
+  for (int i = 1; i <= ntypes; i++)
+    for (int j = i; j <= ntypes; j++) {
+      const bool on = ijskip[i * (ntypes + 1) + j] == 0;
+      p->cut[i][j] = on ? cut[i * (ntypes + 1) + j] : nan;
+      p->setflag[i][j] = on ? 1 : 0;
+    }
+  for (int i = 1; i <= ntypes; i++)  // (init_one of the assigned pairs only, as hybrid's)
+    for (int j = i; j <= ntypes; j++)
+      if (p->setflag[i][j]) {
+        const double c = p->init_one(i, j);
+        p->cutsq[i][j] = p->cutsq[j][i] = c * c;
+      } else {
+        p->cutsq[i][j] = p->cutsq[j][i] = nan;
+      }
+  NeighList *l = new NeighList(w.lmp);
+  l->inum = inum;
+  l->gnum = 0;
+  l->ilist = (int *)malloc(sizeof(int) * (inum > 0 ? inum : 1));
+  // (numneigh / firstneigh are indexed by the atom, not the list position)
+  l->numneigh = (int *)calloc(nlocal > 0 ? nlocal : 1, sizeof(int));
+  l->firstneigh = (int **)calloc(nlocal > 0 ? nlocal : 1, sizeof(int *));
+  for (int k = 0; k < inum; k++) {
+    const int i = ilist[k];
+    l->ilist[k] = i;
+    l->numneigh[i] = (int)(off[k + 1] - off[k]);
+    l->firstneigh[i] = const_cast<int *>(neigh) + off[k];
+  }
+  {
+    std::vector<int> is(iskip, iskip + ntypes + 1);
+    int **ij;
+    w.lmp->memory->create(ij, ntypes + 1, ntypes + 1, "harness:ijskip");
+    for (int i = 0; i <= ntypes; i++)
+      for (int j = 0; j <= ntypes; j++) ij[i][j] = ijskip[i * (ntypes + 1) + j];
+    l->copy_skip_info(is.data(), ij);
+    w.lmp->memory->destroy(ij);
+  }
+  p->list = l;
+  SPH_INIT(p);
+  {
+    // (device lists on: the style is force->pair, whose cutsq the shim would size the
+    // device list from -- a hybrid's covers every pair, here the assigned ones are NaN)
     DevListScope dl(w, p);
     p->compute(0, 0);
   }

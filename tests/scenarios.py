@@ -154,3 +154,50 @@ def bubble_physics(nx=10, dim=3, dt=None, prob=0.01, Tt=0.1, pc=True, nevery=1, 
                         rbg=np.zeros(3), visc=visc, tait_cut=hh.copy(), st_cut=hh.copy(),
                         heat_alpha=hal, heat_cut=hh.copy(), heat_fixflag=ff, heat_tc=tc,
                         pc=pcd)
+
+
+def skip_list_case(n=7, h=3.0, skin=0.3):
+    """water_collapse.lmp's rhosum under hybrid/overlay (`pair_coeff 1 1 sph/rhosum`) on a
+    two-type jittered box: the sub-style's SKIP list (pair_hybrid.cpp:428-485) holds the
+    type-1 rows and their type-1 neighbours only.  Returns the inputs of ref_rhosum_skip and
+    the oracle's result (type-1 rows summed over that list, type-2 rho untouched)."""
+    s = po.cubic_lattice(n, ntypes=2, type2_frac=0.4, rho=(1.0, 0.7))
+    nt = 2
+    cut = np.zeros((nt + 1, nt + 1))
+    cut[1, 1] = h
+    cns, cmax = po.cutneighsq(nt, cut, skin)
+    g = po.borders(s, cmax)
+    off, nb = po.neigh_full(s.dim, g, nt, cns)
+    rows = np.nonzero(s.type == 1)[0].astype(np.int32)
+    soff = [0]
+    snb = []
+    moff = np.zeros(s.n + 1, dtype=np.int64)  # (the oracle's CSR: type-2 rows empty)
+    for i in range(s.n):
+        js = nb[off[i]:off[i + 1]]
+        keep = js[g.type[js] == 1] if s.type[i] == 1 else js[:0]
+        if s.type[i] == 1:
+            snb.append(keep)
+            soff.append(soff[-1] + len(keep))
+        moff[i + 1] = moff[i] + len(keep)
+    snb = np.concatenate(snb).astype(np.int32) if snb else np.zeros(0, np.int32)
+    iskip = np.array([0, 0, 1], dtype=np.int32)
+    ijskip = np.ones((nt + 1, nt + 1), dtype=np.int32)
+    ijskip[1, 1] = 0
+    rho0 = g.gather(s.rho)
+    want = s.rho.copy()
+    got = po.rhosum(s.dim, g, nt, s.mass, cut, moff, snb)
+    want[rows] = got[rows]
+    return dict(dim=s.dim, nt=nt, nlocal=s.n, nghost=g.nghost, x=np.ascontiguousarray(g.x),
+                type=np.ascontiguousarray(g.type, dtype=np.int32), mass=s.mass, cut=cut,
+                rows=rows, off=np.asarray(soff, dtype=np.int64), nb=snb, iskip=iskip,
+                ijskip=np.ascontiguousarray(ijskip.ravel()), rho0=rho0, want=want)
+
+
+def run_rhosum_skip(R, c):
+    """R.ref_rhosum_skip on a case of skip_list_case; returns the owned rho"""
+    rho = c["rho0"].copy()
+    R.ref_rhosum_skip(c["dim"], c["nt"], c["nlocal"], c["nghost"], c["x"], c["type"],
+                      c["mass"], np.ascontiguousarray(c["cut"].ravel()), len(c["rows"]),
+                      c["rows"], c["off"], c["nb"] if c["nb"].size else np.zeros(1, np.int32),
+                      c["iskip"], c["ijskip"], rho)
+    return rho[:c["nlocal"]]

@@ -158,3 +158,25 @@ def test_single_phase_styles_device_lists(S, name):
         test_single_phase_styles(S, name)
     finally:
         S.ref_set_device_lists(0, 0.0)
+
+
+@pytest.mark.parametrize("devlists", [0, 1])
+def test_hybrid_substyle_skip_list(S, devlists):
+    """sph/rhosum/hip as a hybrid/overlay sub-style with a skip list (water_collapse.lmp:
+    `pair_coeff 1 1 sph/rhosum`, scenarios.skip_list_case), on both list paths: the
+    device-list path must not be taken for a skip list (its rows and pairs would cover every
+    type, and the sub-style's coefficients for the unassigned pairs are uninitialised --
+    NaN in the harness), so either way the result is the reference's on its skip list
+    (test_lammps_shim.test_reference_rhosum_on_a_skip_list): type-1 rows summed over type-1
+    neighbours, type-2 rho untouched."""
+    from scenarios import run_rhosum_skip, skip_list_case
+    c = skip_list_case()
+    S.ref_set_device_lists(devlists, 0.3)
+    try:
+        got = run_rhosum_skip(S, c)
+    finally:
+        S.ref_set_device_lists(0, 0.0)
+    assert np.isfinite(got).all()
+    assert rel_err(got, c["want"]) < 1e-13
+    t2 = c["type"][:c["nlocal"]] == 2
+    assert (got[t2] == c["rho0"][:c["nlocal"]][t2]).all()

@@ -134,3 +134,18 @@ def test_fix_arguments_match_reference_errors(tail, msg):
         line = [l for l in out.splitlines() if l.startswith("ERROR")][0]
         outs.append(line.split(" (")[0])
     assert outs[0] == outs[1] == "ERROR: " + msg
+
+
+@pytest.mark.ref
+def test_reference_rhosum_on_a_skip_list(ref):
+    """The reference's own PairSPHRhoSum as a hybrid/overlay sub-style with a skip list
+    (scenarios.skip_list_case, water_collapse's `pair_coeff 1 1 sph/rhosum`) against the
+    oracle on the same list: type-1 rows summed over type-1 neighbours, type-2 rho left as it
+    was -- the fixture test_gpu_shim's skip-list test holds the /hip class to."""
+    from conftest import rel_err
+    from scenarios import run_rhosum_skip, skip_list_case
+    c = skip_list_case()
+    got = run_rhosum_skip(ref, c)
+    assert rel_err(got, c["want"]) < 1e-13
+    t2 = c["type"][:c["nlocal"]] == 2
+    assert t2.any() and (got[t2] == c["rho0"][:c["nlocal"]][t2]).all()

@@ -383,11 +383,19 @@ int sph_engine_set_atoms_multiphase(sph_engine *e, const double *rmass, const do
 /* fix phase_change on a one-brick multiphase engine (FixPhaseChange::pre_exchange at steps
    1, 1+nevery, ...; the rebuild follows): p's sublo/subhi/boxhi/top are filled by the
    engine, p->dt must be the engine's dt.  Candidates meet the Park-Miller stream (seed) in
-   ascending tag order -- the reference's atom order on one process (new atoms are
-   appended and LAMMPS sorts atoms only every 1000 steps by default).  New atoms get tags
-   n, n+1, ... in creation order (atom->tag_extend), type to_type.  Before setup. */
+   the reference's local atom order, which the engine tracks beside its own row order while
+   the fix is armed: read order (ascending tag within the brick), CommBrick::exchange's hole
+   fill (comm_brick.cpp:620-632; received atoms appended), Atom::sort at setup and every
+   sortfreq steps (sph_engine_atom_sort), created atoms appended.  New atoms get tags n,
+   n+1, ... in creation order (atom->tag_extend), type to_type.  Before setup. */
 int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int nevery,
                             int seed);
+/* atom_modify sort sortfreq binsize (atom.cpp:540-551; replaces Atom::sortfreq/userbinsize):
+   the spatial sort whose order fix phase_change meets its candidates in -- bins of binsize
+   (0 = half the neighbor cutoff, Atom::setup_sort_bins) over the brick, at setup and every
+   sortfreq steps (0 = never).  Default 1000 / 0, LAMMPS' own.  The engine's rows keep their
+   own order; only the tracked LAMMPS order changes. */
+int sph_engine_atom_sort(sph_engine *e, int sortfreq, double binsize);
 /* Multiphase fields of the owned atoms in get_atoms order (any pointer may be NULL):
    rmass, cv, colorgradient (n*3), vest (n*3), type; *ninserted = atoms created so far. */
 int sph_engine_get_atoms_multiphase(sph_engine *e, double *rmass, double *cv, double *cg,

@@ -159,6 +159,7 @@ EXPORTS = {
     "sph_engine_rebuild_passes": (_i, [_vp, _i]),
     "sph_engine_set_atoms_multiphase": (_i, [_vp, _dp, _vp, _vp]),
     "sph_engine_phase_change": (_i, [_vp, _vp, _i, _i]),
+    "sph_engine_atom_sort": (_i, [_vp, _i, C.c_double]),
     "sph_engine_get_atoms_multiphase": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sph_engine_write_restart": (_i, [_vp, _vp, C.c_int64, C.POINTER(_i)]),
     "sph_engine_read_restart": (_i, [_vp, _i, _dp]),
@@ -578,6 +579,11 @@ class Engine:
         p.energy_chance, p.change_chance, p.rate = energy_chance, prob, rate
         p.maxattempt = maxattempt
         _chk(self.L.sph_engine_phase_change(self.h, C.byref(p), nevery, seed))
+
+    def atom_sort(self, sortfreq=1000, binsize=0.0):
+        """atom_modify sort sortfreq binsize: the LAMMPS local order fix phase_change meets its
+        candidates in (Atom::sort at setup and every sortfreq steps; 0 = never)."""
+        _chk(self.L.sph_engine_atom_sort(self.h, int(sortfreq), float(binsize)))
 
     def get_atoms_multiphase(self):
         n = self.nlocal

@@ -206,8 +206,19 @@ struct sph_engine {
   DBuf<double> pc_rec, pc_gat, pc_Wd, pc_vals, pc_nrec, pc_v0, pc_v1;
   DBuf<unsigned long long> pc_k0, pc_k1;  // the donations' (donor, candidate) sort keys
   DBuf<int> pc_cnt;
-  bool pc_order_warned = false;
   int64_t migrations = 0;  // atoms that left this brick at exchanges so far
+  // LAMMPS' local order of the owned atoms, tracked while fix phase_change is armed (its
+  // candidates meet the random stream in that order): lidx[row] = the atom's index in the
+  // reference's arrays -- read order, CommBrick::exchange's hole fill, Atom::sort at setup and
+  // every sortfreq steps (atom_modify sort, default 1000 at half the neighbour cutoff)
+  DBuf<int> lidx, lidx2, lidx_tab;
+  DBuf<unsigned long long> skey, skey2;
+  DBuf<int> srow, srow2;
+  std::vector<char> h_leave;
+  bool lidx_valid = false;
+  int sortfreq = 1000;
+  double sort_binsize = 0.0;
+  int64_t nextsort = 0;
   // fix phase_change (one brick): parameters, stream state, next call, atoms created
   bool pc = false;
   sph_phasechange_params pcp{};
@@ -508,6 +519,12 @@ struct sph_engine {
     std::swap(ty, ty2);
     std::swap(vel, vel2);
     std::swap(tag, tag2);
+    if (pc) {  // (the LAMMPS index rides along)
+      lidx2.reserve_exact(lidx.cap);
+      hipLaunchKernelGGL(k_lidx_take, dim3(blocks(n)), dim3(BLK), 0, s, n, bidx2.p, lidx.p, 0,
+                         (const int *)nullptr, lidx2.p);
+      std::swap(lidx, lidx2);
+    }
     if (mp)
       hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(n)), dim3(BLK), 0, s, n, (const int *)nullptr,
                          0, xbuf.p, vel.p, rm.p, cvv.p, cg.p);
@@ -980,26 +997,29 @@ struct sph_engine {
       const int nl = select_flagged(flags.p, n, sel);
       migrations += nl;
       const int nst = select_flagged(flag2.p, n, sel2);
+      if (pc && nl) hole_fill(n, nl, nst);  // (leavers put in send order, lidx renumbered)
       cbs.reserve((size_t)(nl > 0 ? nl : 1) * sizeof(MigRec));
       if (nl)
         hipLaunchKernelGGL(k_pack_mig, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, xf.p,
                            vr.p, vel.p, en.p, ty.p, tag.p, (MigRec *)cbs.p);
-      if (mp && nl) {  // the leavers' extra fields, then the stayers' compacted
+      if (mp && nl) {  // the leavers' extra fields
         xbuf.reserve((size_t)MPX * nl, false, s);
         hipLaunchKernelGGL(k_mpx_pack, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, vel.p,
                            rm.p, cvv.p, cg.p, xbuf.p);
-        mpx_copy(nst, sel2.p, 0, xbuf2);
       }
       if (nl) {  // compact the staying atoms to the front (order kept)
         DBuf<unsigned char> keep;
         keep.reserve((size_t)(nst > 0 ? nst : 1) * sizeof(MigRec));
-        if (nst) {
+        // (every record is packed from the old rows before any row is rewritten: the extra
+        // fields' copy rewrites vel, which the records carry whole)
+        if (nst)
           hipLaunchKernelGGL(k_pack_mig, dim3(blocks(nst)), dim3(BLK), 0, s, nst, sel2.p, xf.p,
                              vr.p, vel.p, en.p, ty.p, tag.p, (MigRec *)keep.p);
+        mpx_copy(nst, sel2.p, 0, xbuf2);
+        if (nst)
           hipLaunchKernelGGL(k_gather_mig, dim3(blocks(nst)), dim3(BLK), 0, s, nst,
                              (const int *)nullptr, (const MigRec *)keep.p, 0, xf.p, vr.p,
                              vel.p, en.p, ty.p, tag.p);
-        }
         SPH_HIP_TRY(hipStreamSynchronize(s));
         keep.release();
       }
@@ -1029,6 +1049,11 @@ struct sph_engine {
         tag.reserve((size_t)nlocal + nm, true, s);
         hipLaunchKernelGGL(k_gather_mig, dim3(blocks(nm)), dim3(BLK), 0, s, nm, sel2.p,
                            (const MigRec *)cbr.p, nlocal, xf.p, vr.p, vel.p, en.p, ty.p, tag.p);
+        if (pc) {  // unpack_exchange appends in buffer order
+          lidx.reserve((size_t)nlocal + nm, true, s);
+          hipLaunchKernelGGL(k_lidx_iota, dim3(blocks(nm)), dim3(BLK), 0, s, nm, nlocal,
+                             lidx.p + nlocal);
+        }
         if (mp)
           hipLaunchKernelGGL(k_mpx_unpack, dim3(blocks(nm)), dim3(BLK), 0, s, nm, sel2.p,
                              nlocal, (const double *)xbuf2.p, vel.p, rm.p, cvv.p, cg.p);
@@ -1037,6 +1062,124 @@ struct sph_engine {
     }
     fo.reserve(nlocal > 0 ? nlocal : 1, true, s);
     de.reserve(nlocal > 0 ? nlocal : 1, true, s);
+  }
+
+  // CommBrick::exchange's scan of one dimension (comm_brick.cpp:620-632) on the LAMMPS
+  // indices: a departing atom's slot takes the last atom, which is examined next.  The n - nst
+  // leavers (sel) go into the buffer in that order -- the receivers append them as LAMMPS
+  // does -- and the stayers' indices are compacted along sel2, the tail atoms that moved
+  // into holes renumbered.  Host work over the leavers only (the tail atom at LAMMPS index
+  // m is always the one that started there: moves only go from the tail into lower holes).
+  void hole_fill(int n, int nl, int nst) {
+    std::vector<int> hl(nl), hr(nl);
+    lidx_tab.reserve(nl);
+    hipLaunchKernelGGL(k_lidx_take, dim3(blocks(nl)), dim3(BLK), 0, s, nl, sel.p, lidx.p, 0,
+                       (const int *)nullptr, lidx_tab.p);
+    SPH_HIP_TRY(hipMemcpyAsync(hl.data(), lidx_tab.p, nl * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipMemcpyAsync(hr.data(), sel.p, nl * sizeof(int), hipMemcpyDeviceToHost, s));
+    SPH_HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int> ord(nl);
+    for (int k = 0; k < nl; k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) { return hl[a] < hl[b]; });
+    if ((int)h_leave.size() < n) h_leave.resize(n, 0);
+    for (int k = 0; k < nl; k++) h_leave[hl[k]] = 1;
+    std::vector<int> sent, tab(nl, -1);
+    sent.reserve(nl);
+    int m = n;
+    for (int q = 0; q < nl; q++) {
+      const int p = hl[ord[q]];  // the leavers in ascending LAMMPS index
+      if (p >= m) break;         // (already sent from the tail)
+      sent.push_back(p);
+      for (;;) {
+        m--;
+        if (m == p) break;  // the hole was the last slot
+        if (h_leave[m]) {   // the tail atom leaves too: examined in the hole, sent
+          sent.push_back(m);
+          continue;
+        }
+        tab[m - nst] = p;
+        break;
+      }
+    }
+    for (int k = 0; k < nl; k++) h_leave[hl[k]] = 0;
+    SPH_REQUIRE((int)sent.size() == nl && m == nst, SPH_HIP_ERUNTIME,
+                "exchange: hole fill sent %zu of %d atoms", sent.size(), nl);
+    std::vector<int> rows(nl);  // sel in send order
+    for (int k = 0; k < nl; k++) {
+      const int v = sent[k];
+      const auto it = std::lower_bound(ord.begin(), ord.end(), v,
+                                       [&](int a, int val) { return hl[a] < val; });
+      rows[k] = hr[*it];
+    }
+    SPH_HIP_TRY(hipMemcpyAsync(sel.p, rows.data(), nl * sizeof(int), hipMemcpyHostToDevice, s));
+    SPH_HIP_TRY(hipMemcpyAsync(lidx_tab.p, tab.data(), nl * sizeof(int), hipMemcpyHostToDevice, s));
+    if (nst) {
+      lidx2.reserve_exact(lidx.cap);
+      hipLaunchKernelGGL(k_lidx_take, dim3(blocks(nst)), dim3(BLK), 0, s, nst, sel2.p, lidx.p,
+                         nst, lidx_tab.p, lidx2.p);
+      SPH_HIP_TRY(hipMemcpyAsync(lidx.p, lidx2.p, nst * sizeof(int), hipMemcpyDeviceToDevice, s));
+    }
+    SPH_HIP_TRY(hipStreamSynchronize(s));  // (host vectors)
+  }
+
+  // Atom::sort (atom.cpp:1555-1654) on the LAMMPS indices: the bins of setup_sort_bins
+  // (:1660-1726) over this brick's sub-box, atoms listed bin by bin and in their current order
+  // within a bin; one bin = no sort.  nextsort as atom.cpp:1561.
+  void atom_sort() {
+    nextsort = (step / sortfreq) * sortfreq + sortfreq;
+    const double bs = sort_binsize > 0.0 ? sort_binsize : 0.5 * cutneighmax;
+    const double bininv = 1.0 / bs;
+    SortBins b{};
+    double nbins = 1.0;
+    for (int d = 0; d < 3; d++) {
+      const double ext = subhi[d] - sublo[d];
+      int m = (int)(ext * bininv);
+      if (d == 2 && cfg.dim == 2) m = 1;
+      if (m == 0) m = 1;
+      b.lo[d] = sublo[d];
+      b.nb[d] = m;
+      b.inv[d] = m / ext;
+      nbins *= m;
+    }
+    SPH_REQUIRE(nbins <= 2147483647.0, SPH_HIP_EINVAL, "Too many atom sorting bins");
+    const int n = nlocal;
+    if (nbins == 1.0 || n == 0) return;
+    skey.reserve(n);
+    skey2.reserve(n);
+    srow.reserve(n);
+    srow2.reserve(n);
+    hipLaunchKernelGGL(k_lidx_sortkeys, dim3(blocks(n)), dim3(BLK), 0, s, n, b, xf.p, lidx.p,
+                       skey.p, srow.p);
+    int hb = 32;
+    while ((double)(1ll << (hb - 32)) < nbins) hb++;
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, skey.p, skey2.p, srow.p, srow2.p,
+                                                   n, 0, hb, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, skey.p, skey2.p, srow.p, srow2.p,
+                                                   n, 0, hb, s));
+    hipLaunchKernelGGL(k_lidx_rank, dim3(blocks(n)), dim3(BLK), 0, s, n, srow2.p, lidx.p);
+  }
+
+  // the LAMMPS indices from the tags: read order (tag order) -- set_atoms, read_restart
+  void lidx_from_tags() {
+    const int n = nlocal;
+    lidx.reserve(n > 0 ? n : 1);
+    lidx_valid = true;
+    if (n == 0) return;
+    skey.reserve(n);
+    skey2.reserve(n);
+    srow.reserve(n);
+    srow2.reserve(n);
+    hipLaunchKernelGGL(k_lidx_tagkeys, dim3(blocks(n)), dim3(BLK), 0, s, n, tag.p, skey.p,
+                       srow.p);
+    size_t tb = 0;
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, skey.p, skey2.p, srow.p, srow2.p,
+                                                   n, 0, 32, s));
+    tmp_reserve(tb);
+    SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, skey.p, skey2.p, srow.p, srow2.p,
+                                                   n, 0, 32, s));
+    hipLaunchKernelGGL(k_lidx_rank, dim3(blocks(n)), dim3(BLK), 0, s, n, srow2.p, lidx.p);
   }
 
   // One brick: CommBrick::borders' self swaps (comm_brick.cpp:696-864) with every count kept
@@ -1160,7 +1303,7 @@ struct sph_engine {
       pc_key.reserve(2 * (size_t)ns);
       pc_val.reserve(2 * (size_t)ns);
       hipLaunchKernelGGL(k_pc_swapkeys, dim3(blocks(ns)), dim3(BLK), 0, s, ns, first, gsrc.p,
-                         nlocal, tag.p, pc_grank.p, pc_key.p, pc_val.p);
+                         nlocal, lidx.p, pc_grank.p, pc_key.p, pc_val.p);
       size_t tb = 0;
       SPH_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, pc_key.p, pc_key.p + ns,
                                                      pc_val.p, pc_val.p + ns, ns, 0, 32, s));
@@ -1187,10 +1330,10 @@ struct sph_engine {
       cbr.reserve(std::max<size_t>(ro + rb, 1), true, s);
       if (a.nsend)
         hipLaunchKernelGGL(k_pc_sendkeys, dim3(blocks(a.nsend)), dim3(BLK), 0, s, a.nsend,
-                           a.list.p, nlocal, tag.p, pc_grank.p, (int *)cbs.p);
+                           a.list.p, nlocal, lidx.p, pc_grank.p, (int *)cbs.p);
       if (b.nsend)
         hipLaunchKernelGGL(k_pc_sendkeys, dim3(blocks(b.nsend)), dim3(BLK), 0, s, b.nsend,
-                           b.list.p, nlocal, tag.p, pc_grank.p, (int *)(cbs.p + so));
+                           b.list.p, nlocal, lidx.p, pc_grank.p, (int *)(cbs.p + so));
       if (a.remote) {
         tr->exchange2(cbs.p, sa, a.sendproc, cbr.p, ra, a.recvproc, cbs.p + so, sb, b.sendproc,
                       cbr.p + ro, rb, b.recvproc, s);
@@ -1588,6 +1731,9 @@ struct sph_engine {
     // orientation, k_neigh3: CSR at setup, fixed-stride rows once the setup sized them)
     hipLaunchKernelGGL(k_pbc, dim3(blocks(nlocal)), dim3(BLK), 0, s, nlocal, box, xf.p, vel.p);
     if (multi()) exchange_multi();
+    // Atom::sort between the exchange and borders (verlet.cpp:106, 251): only the LAMMPS
+    // indices move -- the rows keep the engine's own order
+    if (pc && sortfreq > 0 && step >= nextsort) atom_sort();
     // (at most every sort_every() steps, as atom_modify sort Nevery: the C5 stack rebuilds
     // every step, and its rows keep their locality over a few steps of motion)
     if (cfg.sort && (!setup_done || step == 0 || step - last_sort >= sort_every())) {
@@ -2096,6 +2242,7 @@ struct sph_engine {
   // in the collectives (slot keys, reverse comm, counts) and in the finish loop.
   void phase_change() {
     Scope t(this, T_NEIGH);
+    if (!lidx_valid) lidx_from_tags();  // (armed after setup: the local order from here on)
     const bool mul = multi();
     const int n = nlocal, nall = nlocal + nghost;
     if (n == 0 && !mul) return;
@@ -2149,7 +2296,7 @@ struct sph_engine {
         }
       }
       hipLaunchKernelGGL(k_pc_gather, dim3(blocks(ncand)), dim3(BLK), 0, s, ncand, cand.p, xf.p,
-                         vr.p, en.p, cvv.p, cg.p, tag.p, gat.p, otag.p);
+                         vr.p, en.p, cvv.p, cg.p, lidx.p, gat.p, otag.p);
       SPH_HIP_TRY(hipMemcpyAsync(hm.data(), pc_minr.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipMemcpyAsync(hc.data(), cand.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipMemcpyAsync(ht.data(), otag.p, ncand * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -2157,21 +2304,8 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemcpyAsync(hg.data(), gat.p, hg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
     }
-    // the reference meets the candidates in its atom order: tag order (one process, or one
-    // rank's owned atoms while none has migrated).  LAMMPS' local order leaves tag order once
-    // CommBrick::exchange has filled a departed atom's hole with the last atom
-    // (comm_brick.cpp:600-625) or Atom::sort has run (every 1000 steps by default,
-    // atom.cpp:63): from then on the draws can meet the candidates in another order than the
-    // reference's -- same statistics, other particles.  Said once.
-    if (!pc_order_warned && (migrations > 0 || step >= 1000)) {
-      pc_order_warned = true;
-      fprintf(stderr,
-              "[sph] fix phase_change: candidates meet the random stream in tag order; the "
-              "reference's local atom order differs after %s (step %lld), so the inserted "
-              "atoms can differ from the reference's from here on\n",
-              migrations > 0 ? "an atom migrated between bricks" : "Atom::sort (sortfreq 1000)",
-              (long long)step);
-    }
+    // the reference meets the candidates in its local order (lidx: read order, exchange hole
+    // fill, Atom::sort)
     std::vector<int> ord(ncand);
     for (int k = 0; k < ncand; k++) ord[k] = k;
     std::sort(ord.begin(), ord.end(), [&](int a, int b) { return ht[a] < ht[b]; });
@@ -2263,6 +2397,8 @@ struct sph_engine {
       hipLaunchKernelGGL(k_pc_append, dim3(blocks(nins)), dim3(BLK), 0, s, nins, nrec.p, n,
                          p.to_type, tag0, xf.p, vr.p, vel.p, en.p, rm.p, cvv.p, cg.p, ty.p,
                          tag.p, fo.p, de.p);
+      lidx.reserve((size_t)n + nins, true, s);  // (create_atom: at the end, in creation order)
+      hipLaunchKernelGGL(k_lidx_iota, dim3(blocks(nins)), dim3(BLK), 0, s, nins, n, lidx.p + n);
     }
     SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host staging vectors go out of scope)
     if (ninsall == 0) return;  // (natoms unchanged: the ghosts stay, the rebuild follows)
@@ -2280,6 +2416,10 @@ struct sph_engine {
   void setup() {
     step = 0;
     Scope t(this, T_NEIGH);
+    if (pc) {  // (every setup sorts: verlet.cpp:106)
+      if (!lidx_valid) lidx_from_tags();
+      nextsort = 0;
+    }
     // borders() runs before setup_pre_force: ghosts carry vest as it was (reference order);
     // the setup force pass needs the global-index list for its half-list walk
     build_all(true);
@@ -2592,6 +2732,7 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   e->tag_next = n;
   e->pc_tags_agreed = false;
   e->pc_inserted = 0;
+  e->lidx_valid = false;
   e->cv_by_tag.assign(n, 1.0);
   if (cv)
     for (int i = 0; i < n; i++) e->cv_by_tag[i] = cv[i];
@@ -3146,6 +3287,16 @@ int sph_engine_set_tags(sph_engine *e, const int *tags) {
   e->global_tags = true;
   e->tag_next = mx + 1;  // (bricks: the ranks agree on the largest at the first phase change)
   e->pc_tags_agreed = false;
+  e->lidx_valid = false;  // (read order = tag order, taken at setup)
+  SPH_API_END
+}
+
+int sph_engine_atom_sort(sph_engine *e, int sortfreq, double binsize) {
+  SPH_API_BEGIN
+  SPH_REQUIRE(e, SPH_HIP_EINVAL, "sph_engine_atom_sort: NULL engine");
+  SPH_REQUIRE(sortfreq >= 0 && binsize >= 0.0, SPH_HIP_EINVAL, "Illegal atom_modify command");
+  e->sortfreq = sortfreq;
+  e->sort_binsize = binsize;
   SPH_API_END
 }
 

@@ -145,13 +145,13 @@ static __global__ void k_unpack_rev1(int n, const int *__restrict__ list,
 
 // ---- fix phase_change bookkeeping -------------------------------------------------------
 // what the stream replay needs of candidate atom cand[k]: x[3], cg[3], e, cv, rho (9
-// doubles) and its tag
+// doubles) and its order key (the LAMMPS local index)
 static __global__ void k_pc_gather(int n, const int *__restrict__ cand,
                                    const double4 *__restrict__ xf,
                                    const double4 *__restrict__ vr, const double *__restrict__ en,
                                    const double *__restrict__ cv, const double4 *__restrict__ cg,
-                                   const int *__restrict__ tag, double *__restrict__ out,
-                                   int *__restrict__ otag) {
+                                   const int *__restrict__ key, double *__restrict__ out,
+                                   int *__restrict__ okey) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const int i = cand[k];
@@ -166,7 +166,7 @@ static __global__ void k_pc_gather(int n, const int *__restrict__ cand,
   o[6] = en[i];
   o[7] = cv[i];
   o[8] = vr[i].w;
-  otag[k] = tag[i];
+  okey[k] = key[i];
 }
 // e of the atoms that changed phase (:317-320)
 static __global__ void k_pc_set_e(int n, const int *__restrict__ idx,

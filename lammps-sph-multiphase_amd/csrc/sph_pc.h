@@ -208,15 +208,15 @@ static __global__ void k_pc_dmass_sum(long long cap, const unsigned long long *_
 }
 
 // one swap of a brick's ghosts: key = LAMMPS index of the atom each ghost was copied from
-// (owned: tag - 1; ghost of an earlier swap: nlocal + its slot), val = position in the swap
+// (owned: lidx; ghost of an earlier swap: nlocal + its slot), val = position in the swap
 static __global__ void k_pc_swapkeys(int ns, int first, const int *__restrict__ gsrc,
-                                     int nlocal, const int *__restrict__ tag,
+                                     int nlocal, const int *__restrict__ lidx,
                                      const int *__restrict__ grank, int *__restrict__ key,
                                      int *__restrict__ val) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= ns) return;
   const int src = gsrc[first + k];
-  key[k] = src < nlocal ? tag[src] - 1 : nlocal + grank[src - nlocal];
+  key[k] = src < nlocal ? lidx[src] : nlocal + grank[src - nlocal];
   val[k] = k;
 }
 
@@ -229,16 +229,69 @@ static __global__ void k_pc_swaprank(int ns, int first, const int *__restrict__ 
 }
 
 // bricks: the key each sent atom carries to the receiving rank -- its place in the order
-// CommBrick::borders scanned this rank's atoms (owned in tag order, then ghosts in LAMMPS
-// slot order); tags stay below 2^30
+// CommBrick::borders scanned this rank's atoms (owned in local order, then ghosts in
+// LAMMPS slot order); local indices stay below 2^30
 static __global__ void k_pc_sendkeys(int n, const int *__restrict__ list, int nlocal,
-                                     const int *__restrict__ tag,
+                                     const int *__restrict__ lidx,
                                      const int *__restrict__ grank, int *__restrict__ key) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const int i = list[k];
-  key[k] = i < nlocal ? tag[i] : (1 << 30) + grank[i - nlocal];
+  key[k] = i < nlocal ? lidx[i] : (1 << 30) + grank[i - nlocal];
 }
+// ---- LAMMPS' local atom order (lidx: each owned row's index in the reference's arrays) -----
+static __global__ void k_lidx_iota(int n, int base, int *__restrict__ lidx) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) lidx[k] = base + k;
+}
+// out[k] = lidx[list[k]], a value >= nfin renumbered through tab (CommBrick::exchange's hole
+// fill: the tail atoms that moved into departed atoms' slots)
+static __global__ void k_lidx_take(int n, const int *__restrict__ list,
+                                   const int *__restrict__ lidx, int nfin,
+                                   const int *__restrict__ tab, int *__restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int v = lidx[list ? list[k] : k];
+  out[k] = (tab && v >= nfin) ? tab[v - nfin] : v;
+}
+// Atom::sort's bins (atom.cpp:1590-1600): key = bin << 32 | current index, so the sort is
+// stable within a bin as the reference's linked lists are
+struct SortBins {
+  double lo[3], inv[3];
+  int nb[3];
+};
+static __global__ void k_lidx_sortkeys(int n, SortBins b, const double4 *__restrict__ xf,
+                                       const int *__restrict__ lidx,
+                                       unsigned long long *__restrict__ key,
+                                       int *__restrict__ row) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double4 x = xf[i];
+  const double c[3] = {x.x, x.y, x.z};
+  int ib[3];
+  for (int d = 0; d < 3; d++) {
+    const double t = (c[d] - b.lo[d]) * b.inv[d];  // static_cast<int>, then MAX 0 / MIN nb-1
+    ib[d] = t < 1.0 ? 0 : (t >= (double)b.nb[d] ? b.nb[d] - 1 : (int)t);
+  }
+  const unsigned long long bin =
+      ((unsigned long long)ib[2] * b.nb[1] + ib[1]) * b.nb[0] + ib[0];
+  key[i] = (bin << 32) | (unsigned)lidx[i];
+  row[i] = i;
+}
+static __global__ void k_lidx_tagkeys(int n, const int *__restrict__ tag,
+                                      unsigned long long *__restrict__ key,
+                                      int *__restrict__ row) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  key[i] = (unsigned)tag[i];
+  row[i] = i;
+}
+static __global__ void k_lidx_rank(int n, const int *__restrict__ row_sorted,
+                                   int *__restrict__ lidx) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) lidx[row_sorted[p]] = p;
+}
+
 // received keys of one swap -> (key, position) pairs for the sort
 static __global__ void k_pc_keys_in(int n, const int *__restrict__ in, int *__restrict__ key,
                                     int *__restrict__ val) {

@@ -852,6 +852,10 @@ class MpPhysics:
     heat_fixflag: np.ndarray | None = None
     heat_tc: np.ndarray | None = None
     pc: dict | None = None
+    # atom_modify sort N binsize (atom.cpp:63, 540-551): Atom::sort every N steps (0 = never);
+    # binsize 0 = half the neighbor cutoff (setup_sort_bins, atom.cpp:1660-1726)
+    sortfreq: int = 1000
+    sort_binsize: float = 0.0
 
     def tables(self):
         return [(self.rhosum_nstep > 0, self.rhosum_cut), (self.cg_nstep > 0, self.cg_cut),
@@ -937,9 +941,9 @@ def brick_owner(sysm: System, x: np.ndarray, pg) -> np.ndarray:
 
 @dataclass
 class BrickView:
-    """One rank's atoms after CommBrick::borders over a processor grid: owned atoms in tag
-    order (their LAMMPS order while nothing has migrated), then each swap's ghosts in the
-    order the sending rank scanned its atoms (comm_brick.cpp:733-800)."""
+    """One rank's atoms after CommBrick::borders over a processor grid: owned atoms in the
+    rank's local order (borders_bricks' `local`), then each swap's ghosts in the order the
+    sending rank scanned its atoms (comm_brick.cpp:733-800)."""
 
     rank: int
     nlocal: int
@@ -963,17 +967,96 @@ class BrickView:
         return int(self.gid.shape[0]) - self.nlocal
 
 
-def borders_bricks(sysm: System, cutghost: float, pg, x: np.ndarray | None = None):
+def hole_fill(local: np.ndarray, leave: np.ndarray):
+    """CommBrick::exchange's scan of one dimension (comm_brick.cpp:620-632): a departing
+    atom's slot takes the last atom (avec->copy(nlocal-1, i)), which is examined next.
+    local: atom ids in local order, leave: their flags -> (the kept ids in their new local
+    order, the departed ids in send-buffer order)."""
+    a = np.array(local, dtype=np.int64)
+    lv = np.array(leave, dtype=bool)
+    n, i, sent = a.size, 0, []
+    while True:
+        nz = np.flatnonzero(lv[i:n])
+        if nz.size == 0:
+            break
+        i += int(nz[0])
+        sent.append(int(a[i]))
+        n -= 1
+        a[i], lv[i] = a[n], lv[n]
+    return a[:n].copy(), np.array(sent, dtype=np.int64)
+
+
+def exchange_bricks(sysm: System, pg, local: list, x: np.ndarray | None = None) -> list:
+    """CommBrick::exchange (comm_brick.cpp:573-680) over the grid: per dimension every rank
+    sends the atoms outside its slab (hole fill, above) to its lower neighbour (and, with more
+    than 2 ranks along the dimension, the same buffer to its upper one); a rank appends the
+    received atoms inside its slab, the upper neighbour's buffer first.  local[r] = rank r's
+    atom ids in local order; returns the new lists."""
+    xo = sysm.x if x is None else x
+    grid = brick_grid(sysm, pg)
+    local = [np.asarray(l, dtype=np.int64) for l in local]
+    for d in range(sysm.dim):
+        if pg[d] == 1:
+            continue   # (nothing leaves a periodic dimension after Domain::pbc)
+        sent = []
+        for r, b in enumerate(grid):
+            xd = xo[local[r], d]
+            local[r], snd = hole_fill(local[r], (xd < b["lo"][d]) | (xd >= b["hi"][d]))
+            sent.append(snd)
+        for r, b in enumerate(grid):
+            srcs = [int(b["neigh"][d, 1])] + ([int(b["neigh"][d, 0])] if pg[d] > 2 else [])
+            add = [local[r]]
+            for src in srcs:
+                g = sent[src]
+                xd = xo[g, d]
+                add.append(g[(xd >= b["lo"][d]) & (xd < b["hi"][d])])
+            local[r] = np.concatenate(add)
+    return local
+
+
+def sort_bricks(sysm: System, pg, local: list, binsize: float, x: np.ndarray | None = None):
+    """Atom::sort (atom.cpp:1555-1654) on every rank: bins of setup_sort_bins (:1660-1726)
+    over the rank's sub-box, atoms listed bin by bin, in their current order within a bin;
+    one bin = no sort."""
+    xo = sysm.x if x is None else x
+    out = []
+    for r, b in enumerate(brick_grid(sysm, pg)):
+        ids = np.asarray(local[r], dtype=np.int64)
+        bininv = 1.0 / binsize
+        nb, inv = [], []
+        for k in range(3):
+            ext = float(b["hi"][k] - b["lo"][k])
+            m = int(ext * bininv)
+            if k == 2 and sysm.dim == 2:
+                m = 1
+            m = max(m, 1)
+            nb.append(m)
+            inv.append(m / ext)
+        if nb[0] * nb[1] * nb[2] == 1:
+            out.append(ids)
+            continue
+        c = []
+        for k in range(3):
+            t = np.trunc((xo[ids, k] - b["lo"][k]) * inv[k])
+            c.append(np.clip(t, 0, nb[k] - 1).astype(np.int64))
+        ibin = c[2] * nb[1] * nb[0] + c[1] * nb[0] + c[0]
+        out.append(ids[np.argsort(ibin, kind="stable")])
+    return out
+
+
+def borders_bricks(sysm: System, cutghost: float, pg, x: np.ndarray | None = None,
+                   local: list | None = None):
     """CommBrick::borders (comm_brick.cpp:696-864, maxneed 1) on every rank of the grid at
     once: per dimension both swaps scan owned + earlier dimensions' ghosts, the lower swap's
     ghosts are appended before the upper one's; a brick at the periodic edge shifts the
-    copies by the box length (one add per coordinate)."""
+    copies by the box length (one add per coordinate).  local[r]: rank r's owned atoms in
+    their local order (default: the atoms inside its sub-box in tag order)."""
     xo = sysm.x if x is None else x
     grid = brick_grid(sysm, pg)
-    own = brick_owner(sysm, xo, pg)
+    own = brick_owner(sysm, xo, pg) if local is None else None
     V = []
     for r, b in enumerate(grid):
-        idx = np.nonzero(own == r)[0]
+        idx = np.nonzero(own == r)[0] if local is None else np.asarray(local[r], np.int64)
         V.append(dict(gid=[idx], x=[xo[idx].copy()], type=[sysm.type[idx].copy()],
                       image=[np.zeros((idx.size, 3), dtype=np.int64)], sf=[], srank=[],
                       sidx=[], nlocal=int(idx.size)))
@@ -1040,17 +1123,26 @@ class MpRefRun(_Spread):
     vel yes: x, v, rho, cg, rmass, e, vest) -> rhosum/multiphase, colorgradient (owned rows;
     the styles' misnamed pack_comm moves nothing, so ghosts keep their comm-time rho and cg,
     SURVEY A.6-1) -> taitwater/multiphase, surfacetension, heatconduction/phasechange on the
-    half list with Newton-3 -> reverse comm (f, de) -> final_integrate.  Atom order = tag
-    order (new atoms appended, no sort)."""
+    half list with Newton-3 -> reverse comm (f, de) -> final_integrate.  The arrays are kept
+    in tag order (new atoms appended); with fix phase_change each rank's LAMMPS local order is
+    tracked beside them (self.local): read order, CommBrick::exchange's hole fill, Atom::sort
+    at setup and every ph.sortfreq steps (verlet.cpp:106, 251), created atoms appended."""
 
     def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None, spread=False):
         self.s = sysm.copy()
         assert self.s.rmass is not None
         # procgrid: fix phase_change as it runs on a grid of ranks (each rank scans its owned
-        # atoms in tag order with its own RanPark of the same seed, fix_phase_change.cpp:116,
-        # creates atoms only in its sub-box, and the ghosts' dmass goes back over the ranks'
-        # swaps); the pair styles, integrators and lists do not depend on the decomposition
+        # atoms in its local order with its own RanPark of the same seed,
+        # fix_phase_change.cpp:116, creates atoms only in its sub-box, and the ghosts' dmass
+        # goes back over the ranks' swaps); the pair styles, integrators and lists do not
+        # depend on the decomposition
         self.pg = None if procgrid is None or int(np.prod(procgrid)) == 1 else tuple(procgrid)
+        # the candidates' order is LAMMPS' local order: one process that sorts atoms runs the
+        # per-rank path on a 1x1x1 grid, whose views list the owned atoms in that order
+        if ph.pc is not None and ph.sortfreq > 0 and self.pg is None:
+            self.pg = (1, 1, 1)
+        self.local = None                    # per rank: atom ids in local order (pc only)
+        self.nextsort = 0
         # rev: every list row walked backwards -- the same physics in another summation
         # order, so a test can size its tolerance to how far the reference's own result moves
         # under reordering where a sum nearly cancels (ill-conditioned atoms)
@@ -1115,7 +1207,9 @@ class MpRefRun(_Spread):
         self.hoff, self.hnb = half_from_full(self.g, self.foff, self.fnb)
         self._ghost_fields()
         if self.pg:
-            self.bviews = borders_bricks(s, self.cutneighmax, self.pg)
+            if self.ph.pc is not None:
+                self._local_order()
+            self.bviews = borders_bricks(s, self.cutneighmax, self.pg, local=self.local)
             for bv in self.bviews:
                 gh = Ghosted(bv.nlocal, bv.nghost, np.ascontiguousarray(bv.x), bv.type,
                              np.zeros(bv.nghost, np.int32), np.zeros((bv.nghost, 3), np.int32))
@@ -1123,6 +1217,23 @@ class MpRefRun(_Spread):
                 if self.rev:
                     bv.nb = _reorder_rows(bv.off, bv.nb, self.rev)
                 bv.hoff, bv.hnb = half_from_full(gh, bv.off, bv.nb)
+
+    def _local_order(self):
+        """Between Domain::pbc and CommBrick::borders (verlet.cpp:100-107, 245-253): the
+        exchange, then Atom::sort at setup and once step >= nextsort (nextsort =
+        (step/sortfreq)*sortfreq + sortfreq, atom.cpp:1561).  The first call lists every
+        rank's atoms in read order (tag order within the rank)."""
+        s, ph = self.s, self.ph
+        if self.local is None:
+            own = brick_owner(s, s.x, self.pg)
+            self.local = [np.nonzero(own == r)[0] for r in range(int(np.prod(self.pg)))]
+        else:
+            self.local = exchange_bricks(s, self.pg, self.local)
+        if ph.sortfreq > 0 and (self.step == 0 or self.step >= self.nextsort):
+            self.nextsort = (self.step // ph.sortfreq) * ph.sortfreq + ph.sortfreq
+            bs = ph.sort_binsize if ph.sort_binsize > 0 else 0.5 * self.cutneighmax
+            self.local = sort_bricks(s, self.pg, self.local, bs)
+        assert sum(l.size for l in self.local) == s.n
 
     def _forward(self):
         g, s = self.g, self.s
@@ -1390,6 +1501,7 @@ class MpRefRun(_Spread):
             res.append((a, dm, ncur))
         self._reverse_bricks([r[1] for r in res])   # reverse_comm_fix of dmass
         new = []
+        nxt = s.n
         for bv, (a, dm, ncur) in zip(self.bviews, res):
             nl = bv.nlocal
             own = bv.gid[:nl]
@@ -1399,6 +1511,10 @@ class MpRefRun(_Spread):
             s.e[own] = e
             if ncur > nl:
                 new.append({k: v[nl:ncur].copy() for k, v in a.items()})
+                if self.local is not None:   # created at the end of the rank's local list
+                    self.local[bv.rank] = np.concatenate(
+                        [self.local[bv.rank], np.arange(nxt, nxt + ncur - nl)])
+                nxt += ncur - nl
         nins = sum(d["x"].shape[0] for d in new)
         if nins:
             cat = lambda k: np.concatenate([d[k] for d in new])

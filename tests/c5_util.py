@@ -34,6 +34,7 @@ def mp_engine(sph, s, ph, path=0, procgrid=(1, 1, 1), rank=0, sel=None):
         eng.phase_change(p["Tc"], p["Tt"], p["Hwv"], p["dr"], p["to_mass"], p["cutoff"],
                          p["from_type"], p["to_type"], nevery=p.get("nevery", 1),
                          seed=p["seed"], prob=p.get("prob", 0.0))
+        eng.atom_sort(getattr(ph, "sortfreq", 1000), getattr(ph, "sort_binsize", 0.0))
     return eng
 
 

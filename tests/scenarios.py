@@ -201,3 +201,24 @@ def run_rhosum_skip(R, c):
                       c["rows"], c["off"], c["nb"] if c["nb"].size else np.zeros(1, np.int32),
                       c["iskip"], c["ijskip"], rho)
     return rho[:c["nlocal"]]
+
+
+def shuffled(s, seed):
+    """The same atoms read in another order (a data file's line order = the tags)."""
+    p = np.random.default_rng(seed).permutation(s.n)
+    s = s.copy()
+    for k in ("x", "v", "type", "rho", "e", "cv", "rmass"):
+        if getattr(s, k) is not None:
+            setattr(s, k, np.ascontiguousarray(getattr(s, k)[p]))
+    return s
+
+
+def drifting(s, vx, dx0):
+    """s moving as a whole along x at vx, shifted by dx0 (wrapped into the box): atoms cross
+    brick faces every few steps (CommBrick::exchange), the flow itself unchanged."""
+    s = s.copy()
+    lo, hi = s.boxlo[0], s.boxhi[0]
+    x = s.x[:, 0] + dx0
+    s.x[:, 0] = np.where(x >= hi, x - (hi - lo), x)
+    s.v[:, 0] += vx
+    return s

@@ -7,8 +7,8 @@ scans its own atoms with its own RanPark(seed) (:116) and creates atoms only ins
 sub-box (insert_one_atom, :441-452); the donors' dmass on ghosts goes back to their owners
 through CommBrick's swaps (reverse_comm_fix, :324; comm_brick.cpp:999-1030); the created atoms
 take the next tags rank by rank (MPI_Allreduce + tag_extend, :338-351, atom.cpp:598-630).
-Candidate order on a rank = its LAMMPS atom order, i.e. tag order while nothing has migrated
-(the convention both sides use).  Created atoms over ghost slots (the reference's memory
+Candidate order on a rank = its LAMMPS local order: read order, CommBrick::exchange's hole
+fill and appended arrivals (comm_brick.cpp:620-680), Atom::sort (atom.cpp:1555-1654).  Created atoms over ghost slots (the reference's memory
 behaviour) follow each rank's own slot order, which the engine derives from keys the sending
 ranks attach to their swaps.
 
@@ -24,7 +24,9 @@ import pytest
 import pyoracle as po
 from c5_util import bricks_step, mp_bricks, mp_collect
 from conftest import check_fields, rel_err
-from scenarios import bubble_physics, bubble_system
+import dataclasses
+
+from scenarios import bubble_physics, bubble_system, drifting, shuffled
 
 TOL = 1e-10
 
@@ -96,6 +98,38 @@ def test_c5_bricks_stack_every2(gpu, sph_amd):
         ref.run(5)
         bricks_step(engines, lambda e: e.run(5))
         _compare(mp_collect(engines, ref.s.n), ref)
+    finally:
+        for e in engines:
+            e.close()
+        world.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,pg,sortfreq", [(3, (2, 1, 1), 4), (3, (2, 2, 1), 0),
+                                             (2, (2, 2, 1), 3)])
+def test_c5_bricks_migration_local_order(gpu, sph_amd, dim, pg, sortfreq):
+    """Atoms crossing brick faces while fix phase_change runs: each rank's local order goes
+    through CommBrick::exchange's hole fill (a departed atom's slot takes the last atom; the
+    arrivals are appended, the upper neighbour's first) and Atom::sort; the candidates and
+    the ghost slots follow it on both sides."""
+    nx = 10 if dim == 3 else 16
+    s = drifting(shuffled(bubble_system(nx, dim=dim), 3), 200.0, 0.49 / nx)
+    ph = dataclasses.replace(bubble_physics(nx, dim=dim, prob=0.5, Tt=-1.0),
+                             sortfreq=sortfreq)
+    ref = po.MpRefRun(s, ph, procgrid=pg, spread=True)
+    ref.setup()
+    own0 = po.brick_owner(s, s.x, pg)
+    world, engines = mp_bricks(sph_amd, s, ph, pg, own0)
+    try:
+        bricks_step(engines, lambda e: e.setup())
+        _compare(mp_collect(engines, ref.s.n), ref)
+        for _ in range(8):
+            ref.run(1)
+            bricks_step(engines, lambda e: e.run(1))
+            _compare(mp_collect(engines, ref.s.n), ref)
+        assert ref.ninserted >= 2
+        moved = po.brick_owner(s, ref.s.x[:s.n], pg) != own0
+        assert moved.sum() >= 10   # (the drift carried atoms across the faces)
     finally:
         for e in engines:
             e.close()

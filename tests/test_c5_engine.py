@@ -10,12 +10,14 @@ per atom exactly at the cutoff, which the reference's own Neighbor::full_bin kee
 oracle's builder to it there).  The oracle's fix phase_change is the reference's own behaviour
 (pinned by test_phasechange_golden.py), created atoms overwriting ghost slots included; the
 slab cases are geometries where that matters."""
+import dataclasses
+
 import numpy as np
 import pytest
 
 import pyoracle as po
 from conftest import check_fields, rel_err
-from scenarios import bubble_physics, bubble_system
+from scenarios import bubble_physics, bubble_system, shuffled
 
 TOL = 1e-10
 
@@ -42,7 +44,8 @@ def test_slab_geometry_exercises_the_aliasing():
     res = {}
     for exact in (True, False):
         s = bubble_system(8, slab=True)
-        ph = bubble_physics(8, prob=0.3, Tt=-1.0)
+        # (no sort: the global path, where pc_exact selects the port semantics)
+        ph = dataclasses.replace(bubble_physics(8, prob=0.3, Tt=-1.0), sortfreq=0)
         ref = po.MpRefRun(s, ph)
         ref.pc_exact = exact
         ref.setup()
@@ -101,3 +104,26 @@ def test_engine_c5_no_phase_change_every2(gpu, sph_amd):
     eng.run(5)
     _compare(eng, ref)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sortfreq,binsize", [(1000, 0.0), (3, 0.0), (2, 0.06), (0, 0.0)])
+def test_engine_c5_local_order(gpu, sph_amd, sortfreq, binsize):
+    """fix phase_change meets its candidates in LAMMPS' local order: the atoms read in a
+    shuffled order, then Atom::sort at setup and every sortfreq steps (atom_modify sort;
+    binsize 0 = half the neighbour cutoff), created atoms appended.  The engine tracks that
+    order beside its own rows; the draws must meet the same candidates as the oracle's."""
+    from c5_util import mp_engine
+    s = shuffled(bubble_system(10), 7)
+    ph = dataclasses.replace(bubble_physics(10, prob=0.5, Tt=-1.0), sortfreq=sortfreq,
+                             sort_binsize=binsize)
+    ref = po.MpRefRun(s, ph, spread=True)
+    ref.setup()
+    eng = mp_engine(sph_amd, s, ph)
+    eng.setup()
+    _compare(eng, ref)
+    for _ in range(7):
+        ref.run(1)
+        eng.run(1)
+        _compare(eng, ref)
+    assert ref.ninserted >= 3

@@ -21,7 +21,7 @@ sys.path.insert(0, HERE)
 import pyoracle as po  # noqa: E402  (the System/Physics constructors only)
 from c5_util import mp_engine, mp_state  # noqa: E402
 from conftest import load_sph_amd  # noqa: E402
-from scenarios import bubble_physics, bubble_system, c2_system  # noqa: E402
+from scenarios import bubble_physics, bubble_system, c2_system, drifting, shuffled  # noqa: E402
 
 
 def c2_scenario(spec):
@@ -36,9 +36,17 @@ def c2_scenario(spec):
 
 
 def c5_scenario(spec):
-    """tests/test_c5_bricks.py's jittered slab: bubble_growth stack + fix phase_change."""
-    s = bubble_system(spec["nx"], dim=spec.get("dim", 3), slab=True)
-    ph = bubble_physics(spec["nx"], dim=spec.get("dim", 3), prob=0.3, Tt=-1.0)
+    """tests/test_c5_bricks.py's jittered slab: bubble_growth stack + fix phase_change.
+    drift: the bubble instead, read in a shuffled order and moving along x at that speed, so
+    atoms cross the brick faces (exchange hole fill) while Atom::sort runs every `sortfreq`."""
+    nx, dim = spec["nx"], spec.get("dim", 3)
+    if spec.get("drift"):
+        s = drifting(shuffled(bubble_system(nx, dim=dim), 3), spec["drift"], 0.49 / nx)
+        ph = bubble_physics(nx, dim=dim, prob=0.5, Tt=-1.0)
+    else:
+        s = bubble_system(nx, dim=dim, slab=True)
+        ph = bubble_physics(nx, dim=dim, prob=0.3, Tt=-1.0)
+    ph.sortfreq = spec.get("sortfreq", ph.sortfreq)
     return s, ph
 
 

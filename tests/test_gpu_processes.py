@@ -106,15 +106,21 @@ def test_processes_c2_rebuilds_migration(gpu, tmp_path, mode, pg):
     assert all(int(sn["nghost"]) > 0 for sn in snaps)
 
 
-@pytest.mark.parametrize("mode,pg,dim,nx", [(0, (2, 1, 1), 3, 8), (1, (2, 1, 1), 3, 8),
-                                            (0, (2, 2, 1), 2, 12)])
-def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx):
+@pytest.mark.parametrize("mode,pg,dim,nx,drift", [(0, (2, 1, 1), 3, 8, 0), (1, (2, 1, 1), 3, 8, 0),
+                                                  (0, (2, 2, 1), 2, 12, 0),
+                                                  (0, (2, 1, 1), 3, 10, 200.0),
+                                                  (1, (2, 2, 1), 2, 16, 200.0)])
+def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx, drift):
     """C5 (bubble_growth stack + fix phase_change, rebuild every step) on 2 or 4 processes for
     5 steps against pyoracle.MpRefRun(procgrid): per-rank RanPark streams, dmass reverse comm,
-    the nins allgather and rank-by-rank tag_extend all cross process boundaries."""
+    the nins allgather and rank-by-rank tag_extend all cross process boundaries.  drift: atoms
+    migrate every step and Atom::sort runs every 2 steps, so every rank's candidates meet the
+    stream in a local order that went through exchange hole fills and sorts."""
     nsteps = [1, 2, 3, 4, 5]
     P = int(np.prod(pg))
     spec = dict(scenario="c5", mode=mode, pg=list(pg), nx=nx, dim=dim, snap_steps=nsteps)
+    if drift:
+        spec.update(drift=drift, sortfreq=2)
     snaps = run_ranks(tmp_path, spec, P)
     s, ph = c5_scenario(spec)
     ref = po.MpRefRun(s, ph, procgrid=pg, spread=True)
@@ -130,3 +136,6 @@ def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx):
         check_fields(got, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), TOL,
                      where=k)
     assert ref.ninserted >= 2, "phase change did not insert across the run"
+    if drift:
+        moved = po.brick_owner(s, ref.s.x[:s.n], pg) != po.brick_owner(s, s.x, pg)
+        assert moved.sum() >= 10, "no atom migrated: the hole fill not exercised"

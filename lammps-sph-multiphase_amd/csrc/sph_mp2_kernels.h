@@ -37,6 +37,16 @@ namespace sph {
 #ifndef SPH_MP2_GNU
 #define SPH_MP2_GNU 1
 #endif
+// ... or software-pipelined (records of the next entry loaded while this one is evaluated)
+#ifndef SPH_MP2_PIPE
+#define SPH_MP2_PIPE 0
+#endif
+// study builds: -DSPH_MP2_WPE=n asks the compiler for n waves per SIMD in the gather
+#if defined(SPH_MP2_WPE) && SPH_MP2_WPE > 0
+#define SPH_MP2_OCC __attribute__((amdgpu_waves_per_eu(SPH_MP2_WPE, SPH_MP2_WPE)))
+#else
+#define SPH_MP2_OCC
+#endif
 
 // quintic W(s) and dW/ds without the norm (s = 3 r / h)
 __device__ __forceinline__ double q5_w(double s) {
@@ -265,7 +275,7 @@ __device__ __forceinline__ double3 mp2_svec(int dim, const double4 &w, double3 e
 // POW = false: every gamma is 1 (bubble.lmp), the pressures are linear in rho and the pow()
 // code (and its registers) is not instantiated.
 template <int G, bool TAIT, bool SURF, bool HEAT, bool POW = true>
-__global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
+__global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
   mp2_tables(a.mc, s_p, s_t);
@@ -282,9 +292,93 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
   const double4 cFi = a.pF[i], cSi = a.pS[i];
   const double irFi = mp_rcp(cFi.w), irSi = mp_rcp(cSi.w);
   double fx = 0.0, fy = 0.0, fz = 0.0, dE = 0.0;
-  constexpr int NU = SPH_MP2_GNU;
   const MpRow rw(a.off, a.cnt, a.stride, row);
   const long long kend = rw.end;
+  // one pair (i = row, jr = its entry) on the records x_j, v_j (k), c_j (fresh or stale)
+  auto pair = [&](int jr, int tj, const double4 &xj, const double4 &v4j, const double4 &cj) {
+    const int j = jr & MP_NMASK;
+    const bool fi = !(j >= a.nlocal && jr >= 0);
+    const double4 ci = fi ? cFi : cSi;
+    const Mp2Pair &q = pi[tj];
+    const double rhoi = ci.w, rhoj = cj.w, mj = xj.w;
+    const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
+    const double rsq = dx * dx + dy * dy + dz * dz;
+    const bool ct = TAIT && rsq < q.tcsq, cs = SURF && rsq < q.scsq, ch = HEAT && rsq < q.hcsq;
+    if (!(ct || cs || ch)) return;
+    double r, ir;
+    mp2_r_ir(rsq, r, ir);
+    const double qt = ct ? q5_dw(3.0 * (r * q.tih)) * mp2_dwnorm(dim, q.tih) : 0.0;
+    const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt
+                                  : q5_dw(3.0 * (r * q.sih)) * mp2_dwnorm(dim, q.sih);
+    const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt
+                                 : q5_dw(3.0 * (r * q.hih)) * mp2_dwnorm(dim, q.hih);
+    const double iri = fi ? irFi : irSi, irj = mp_rcp(rhoj);
+    const double Vi = mi * iri, Vj = mj * irj;
+    const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
+    if (ct) {  // pair_sph_taitwater_multiphase.cpp:128-170
+      const Mp2Type tyj = s_t[tj];
+      const double pI = tyi.B * ((!POW || tyi.gamma == 1.0 ? rhoi * tyi.rho0i
+                                                            : pow(rhoi * tyi.rho0i, tyi.gamma)) -
+                                 tyi.rbg);
+      const double pJ = tyj.B * ((!POW || tyi.gamma == 1.0 ? rhoj * tyj.rho0i
+                                                            : pow(rhoj * tyj.rho0i, tyi.gamma)) -
+                                 tyj.rbg);
+      const double pij = (rhoj * pI + rhoi * pJ) * mp_rcp(rhoi + rhoj);
+      const double wfd = qt * ir, V2 = Vi2 + Vj2;
+      const double fvisc = V2 * q.tvisc * wfd, fpair = -V2 * pij * wfd;
+      fx += dx * fpair + (v4i.x - v4j.x) * fvisc;
+      fy += dy * fpair + (v4i.y - v4j.y) * fvisc;
+      fz += dz * fpair + (v4i.z - v4j.z) * fvisc;
+    }
+    if (SURF && cs) {  // pair_sph_surfacetension.cpp:100-190
+      const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
+      const double3 Si = mp2_svec(dim, ci, e, Vi2), Sj = mp2_svec(dim, cj, e, Vj2);
+      fx += (Si.x + Sj.x) * qs;
+      fy += (Si.y + Sj.y) * qs;
+      if (dim == 3) fz += (Si.z + Sj.z) * qs;
+    }
+    if (HEAT && ch) {  // pair_sph_heatconduction_phasechange.cpp:101-136
+      double Tp = Ti, Tq = v4j.w;
+      if (q.hfix == ti && Tp < Tq) Tp = q.htc;
+      if (q.hfix == tj && Tq < Tp) Tq = q.htc;
+      dE += q.halpha2 * (Tp - Tq) * (qh * ir) * (iri * irj) * mj;
+    }
+  };
+  // the records of entry jr: x (with the mass), v (with T), and j's colour-gradient record,
+  // fresh if j is owned or the pair is not i's (else as communicated)
+  auto fetch = [&](int jr, double4 &xj, double4 &v4j, double4 &cj, int &tj) {
+    const int j = jr & MP_NMASK;
+    const bool fj = j < a.nlocal || jr >= 0;
+    xj = a.pA[j];
+    v4j = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
+    cj = (fj ? a.pF : a.pS)[j];
+    tj = a.typed ? mp_etype(jr) : a.ty[j];
+  };
+#if SPH_MP2_PIPE
+  // software-pipelined walk: entry values two rounds ahead, records one round ahead -- the
+  // records of the next entry are in flight while this one is evaluated (the rows stream
+  // from L2: one round's latency is covered by the previous round's pair)
+  long long k = rw.beg + lane;
+  int jc = k < kend ? a.nbr[k] : 0;
+  int jn = k + G < kend ? a.nbr[k + G] : 0;
+  double4 xc, vc, cc;
+  int tc;
+  fetch(jc, xc, vc, cc, tc);
+  for (; k < kend; k += G) {
+    const int jn2 = k + 2 * G < kend ? a.nbr[k + 2 * G] : 0;
+    double4 xn, vn, cn;
+    int tn;
+    fetch(jn, xn, vn, cn, tn);
+    pair(jc, tc, xc, vc, cc);
+    jc = jn;
+    jn = jn2;
+    xc = xn;
+    vc = vn;
+    cc = cn;
+    tc = tn;
+  }
+#else
+  constexpr int NU = SPH_MP2_GNU;
   // the next round's entries are read while this round computes (the rows stream from HBM:
   // one dependent miss per round instead of two)
   int jn[NU];
@@ -304,67 +398,14 @@ __global__ void __launch_bounds__(256) k_mp2_gather(MpArgs a) {
       jn[u] = k < kend ? a.nbr[k] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < NU; u++) {
-      const int j = jrs[u] & MP_NMASK;
-      const bool fj = j < a.nlocal || jrs[u] >= 0;
-      xjs[u] = a.pA[j];
-      v4js[u] = (TAIT || HEAT) ? a.pK[j] : make_double4(0, 0, 0, 0);
-      cjs[u] = (fj ? a.pF : a.pS)[j];
-      tjs[u] = a.typed ? mp_etype(jrs[u]) : a.ty[j];
-    }
+    for (int u = 0; u < NU; u++) fetch(jrs[u], xjs[u], v4js[u], cjs[u], tjs[u]);
 #pragma unroll
     for (int u = 0; u < NU; u++) {
       if (k0 + u * G >= kend) break;
-      const int jr = jrs[u], j = jr & MP_NMASK;
-      const bool fi = !(j >= a.nlocal && jr >= 0);
-      const double4 xj = xjs[u], v4j = v4js[u], cj = cjs[u];
-      const double4 ci = fi ? cFi : cSi;
-      const Mp2Pair &q = pi[tjs[u]];
-      const double rhoi = ci.w, rhoj = cj.w, mj = xj.w;
-      const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-      const double rsq = dx * dx + dy * dy + dz * dz;
-      const bool ct = TAIT && rsq < q.tcsq, cs = SURF && rsq < q.scsq, ch = HEAT && rsq < q.hcsq;
-      if (!(ct || cs || ch)) continue;
-      double r, ir;
-      mp2_r_ir(rsq, r, ir);
-      const double qt = ct ? q5_dw(3.0 * (r * q.tih)) * mp2_dwnorm(dim, q.tih) : 0.0;
-      const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt
-                                    : q5_dw(3.0 * (r * q.sih)) * mp2_dwnorm(dim, q.sih);
-      const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt
-                                   : q5_dw(3.0 * (r * q.hih)) * mp2_dwnorm(dim, q.hih);
-      const double iri = fi ? irFi : irSi, irj = mp_rcp(rhoj);
-      const double Vi = mi * iri, Vj = mj * irj;
-      const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
-      if (ct) {  // pair_sph_taitwater_multiphase.cpp:128-170
-        const Mp2Type tyj = s_t[tjs[u]];
-        const double pI = tyi.B * ((!POW || tyi.gamma == 1.0 ? rhoi * tyi.rho0i
-                                                              : pow(rhoi * tyi.rho0i, tyi.gamma)) -
-                                   tyi.rbg);
-        const double pJ = tyj.B * ((!POW || tyi.gamma == 1.0 ? rhoj * tyj.rho0i
-                                                              : pow(rhoj * tyj.rho0i, tyi.gamma)) -
-                                   tyj.rbg);
-        const double pij = (rhoj * pI + rhoi * pJ) * mp_rcp(rhoi + rhoj);
-        const double wfd = qt * ir, V2 = Vi2 + Vj2;
-        const double fvisc = V2 * q.tvisc * wfd, fpair = -V2 * pij * wfd;
-        fx += dx * fpair + (v4i.x - v4j.x) * fvisc;
-        fy += dy * fpair + (v4i.y - v4j.y) * fvisc;
-        fz += dz * fpair + (v4i.z - v4j.z) * fvisc;
-      }
-      if (SURF && cs) {  // pair_sph_surfacetension.cpp:100-190
-        const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
-        const double3 Si = mp2_svec(dim, ci, e, Vi2), Sj = mp2_svec(dim, cj, e, Vj2);
-        fx += (Si.x + Sj.x) * qs;
-        fy += (Si.y + Sj.y) * qs;
-        if (dim == 3) fz += (Si.z + Sj.z) * qs;
-      }
-      if (HEAT && ch) {  // pair_sph_heatconduction_phasechange.cpp:101-136
-        double Tp = Ti, Tq = v4j.w;
-        if (q.hfix == ti && Tp < Tq) Tp = q.htc;
-        if (q.hfix == tjs[u] && Tq < Tp) Tq = q.htc;
-        dE += q.halpha2 * (Tp - Tq) * (qh * ir) * (iri * irj) * mj;
-      }
+      pair(jrs[u], tjs[u], xjs[u], v4js[u], cjs[u]);
     }
   }
+#endif
   fx = group_sum<G>(fx);
   fy = group_sum<G>(fy);
   fz = group_sum<G>(fz);

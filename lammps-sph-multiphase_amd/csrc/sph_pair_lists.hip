@@ -230,23 +230,31 @@ int sph_hip_build_list(sph_hip_ctx *c, int kind, int64_t key, const double *cutn
     }
   QBins q{};
   Bins bn{};
-  long long nq = 1;
+  double lk[3], ek[3];
+  int nbk[3];
   for (int k = 0; k < 3; k++) {
     const bool act = k < c->dim;
     const double pad = 1e-6 * std::max(1.0, hi[k] - lo[k]);
-    const double l = lo[k] - pad, ext = (hi[k] - lo[k]) + 2 * pad;
-    int nb = 1;
-    if (act) {
-      nb = (int)(ext / (0.5 * cm));
-      nb = std::max(1, std::min(nb, 8192));
-    }
-    q.lo[k] = bn.lo[k] = l;
-    q.nb[k] = bn.nb[k] = nb;
-    q.inv[k] = bn.inv[k] = act ? nb / ext : 0.0;
-    q.size[k] = act ? ext / nb : 1.0;
-    nq *= nb;
+    lk[k] = lo[k] - pad;
+    ek[k] = (hi[k] - lo[k]) + 2 * pad;
+    nbk[k] = act ? std::max(1, std::min((int)(ek[k] / (0.5 * cm)), 8192)) : 1;
   }
-  SPH_REQUIRE(nq < (1ll << 30), SPH_HIP_EOVERFLOW, "sph_hip_build_list: %lld bins", nq);
+  // a box that would need more than 2^26 bins (a wide, sparse rank or a stray far-away
+  // ghost): coarser bins along the longest axes -- any bin of at least cutneighmax/2 keeps
+  // k_neigh3's two-bin reach, so membership is unchanged, only the candidates per bin grow
+  auto bins_of = [&]() { return (long long)nbk[0] * nbk[1] * nbk[2]; };
+  while (bins_of() >= (1ll << 26)) {
+    const int k = (nbk[0] >= nbk[1] && nbk[0] >= nbk[2]) ? 0 : (nbk[1] >= nbk[2] ? 1 : 2);
+    nbk[k] = (nbk[k] + 1) / 2;
+  }
+  const long long nq = bins_of();
+  for (int k = 0; k < 3; k++) {
+    const bool act = k < c->dim;
+    q.lo[k] = bn.lo[k] = lk[k];
+    q.nb[k] = bn.nb[k] = nbk[k];
+    q.inv[k] = bn.inv[k] = act ? nbk[k] / ek[k] : 0.0;
+    q.size[k] = act ? ek[k] / nbk[k] : 1.0;
+  }
   q.cutmaxsq = cmaxsq;
   const int nqbins = (int)nq;
   // bin-ordered copy of every staged atom (xb, tb, qbeg)

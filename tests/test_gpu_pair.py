@@ -251,6 +251,30 @@ def test_device_built_lists(gpu, sph_amd, system, dim):
     assert rel_err(f2, wf) < TOL
 
 
+def test_device_list_with_a_far_away_ghost(gpu, sph_amd):
+    """A stray ghost far from the rank (here 1e4 box lengths along every axis) stretches the
+    bounding box of the binned build past 2^26 half-size bins: the build coarsens the bins
+    along the longest axes (membership unchanged) instead of failing; the owned rows are the
+    oracle's, the stray ghost's row is never built (ghost) and it is nobody's neighbour."""
+    s = c2_system(8)
+    ph = po.c2_physics(3.0)
+    P = prepared(s, ph)
+    g, n = P["g"], s.n
+    cns = np.asarray(P["cns"], dtype=np.float64).reshape(s.ntypes + 1, s.ntypes + 1)
+    ctx = _ctx(sph_amd, s, ph, P)
+    far = np.asarray(s.boxhi, dtype=np.float64) * 1.0e4
+    x = np.concatenate([g.x, far[None, :]])
+    ty = np.concatenate([g.type, g.type[:1]])
+    ext = lambda a: np.concatenate([a, a[:1]])
+    ctx.atoms(g.nlocal, g.nghost + 1, np.ascontiguousarray(x), ty, vest=ext(P["vest_all"]),
+              rho=ext(P["rho_all"]), e=ext(P["e_all"]))
+    ctx.build_list(sph_amd.SPH_LIST_FULL, cns, key=7)
+    assert np.array_equal(ctx.numneigh(n), np.diff(P["foff"]).astype(np.int32))
+    rho = ctx.rhosum(np.zeros(g.nall + 1))[:n]
+    want = po.rhosum(s.dim, g, s.ntypes, s.mass, ph.rhosum_cut, P["foff"], P["fnb"])
+    assert rel_err(rho, want) < 1e-13
+
+
 def test_mapped_host_arrays_and_update(gpu, sph_amd):
     """sph_hip_host_arrays (the shim registers LAMMPS' arrays): the staging kernels read x /
     vest / rho / e straight from mapped host memory, rhosum writes rho and taitwater / heat

@@ -1406,6 +1406,11 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   constexpr bool HEAT = (MODE & M_HEAT) != 0;
   constexpr int NTH = R * G;
   constexpr int CQ = (HEAT ? BLK_CHE : BLK_CH) / 16;  // (= cq)
+  // one type, Monaghan viscosity, no heat term: the records carry rho_j / viscC (the row
+  // rho_i / viscC), so fvisc = min(dvdr, 0) / ((rsq + eps)(rho_i + rho_j) / viscC) needs no
+  // multiply by viscC per pair (viscC = 0: a huge scale, fvisc ~1e-300 -- below every ulp of
+  // the pressure term it is added to, i.e. exactly no viscosity)
+  constexpr bool FOLDV = TAIT && !HEAT && NT1 && VISC == SPH_VISC_MONAGHAN;
   constexpr int NA = HEAT ? 6 : 5;  // a row's shares: F (3), D, E [, EH]
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
   __shared__ TaitPair s_tp[(TAIT && !NT1) ? NT2 : 1];
@@ -1441,7 +1446,9 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   BlkSlots<G, U, NCH> sw;
   sw.load(snbr + (size_t)rr * sstride, c, lane);
   const double4 xi = xf[rr];
-  const double4 vi = vr[rr];
+  const double vsc = FOLDV ? (cf->tait[3].viscC != 0.0 ? 1.0 / cf->tait[3].viscC : 1e300) : 1.0;
+  double4 vi = vr[rr];
+  if (FOLDV) vi.w *= vsc;
   const double ei = HEAT ? en[rr] : 0.0;
   const int it = NT1 ? 1 : ty[rr];
   double4 qx[BLK_SP], qv[BLK_SP];
@@ -1465,6 +1472,7 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   for (int k = 0; k < BLK_SP; k++)
     if (jj[k] >= 0) {
       const int sl = tid + k * NTH + 1;
+      if (FOLDV) qv[k].w *= vsc;
       blk_put<HEAT>(blk_smem, sl, cq, qx[k], qv[k], HEAT ? ge[k] : 0.0);
       if (!NT1) s_t[blk_q(sl, cq)] = (unsigned char)gt[k];
     }
@@ -1473,7 +1481,9 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
     const int base = w * um, end = min(u, base + um);
     for (int p = base + p0; p < end; p += NTH) {
       const int j = ul[p];
-      blk_put<HEAT>(blk_smem, p - base + 1, cq, xf[j], vr[j], HEAT ? en[j] : 0.0);
+      double4 v = vr[j];
+      if (FOLDV) v.w *= vsc;
+      blk_put<HEAT>(blk_smem, p - base + 1, cq, xf[j], v, HEAT ? en[j] : 0.0);
       if (!NT1) s_t[blk_q(p - base + 1, cq)] = (unsigned char)ty[j];
     }
   };
@@ -1523,9 +1533,9 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       return;
     }
     const double dx = xi.x - a0.x, dy = xi.y - a0.y, dz = xi.z - a1.x;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_t(dx, dy, dz);  // (+ 1e-300)
     const int pidx = NT1 ? 3 : it * nt1 + s_t[q];
-    const double r = sqrt1(rsq);
+    const double r = sqrt1n(rsq);
     // this pair's terms (i side); a later row of the block takes its share too (n3)
     double tfx = 0.0, tfy = 0.0, tfz = 0.0, tD = 0.0, tDj = 0.0, tE = 0.0, tEH = 0.0;
     if (TAIT) {
@@ -1536,8 +1546,8 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       const double dvdr = dx * velx + dy * vely + dz * velz;
       if (VISC == SPH_VISC_MONAGHAN) {
         // fvisc = viscC dvdr / ((rsq + eps)(rho_i + rho_j)) for dvdr < 0, else 0
-        const double fv =
-            (cc.viscC * fmin(dvdr, 0.0)) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
+        const double fv = FOLDV ? fmin(dvdr, 0.0) * rcp1((rsq + cc.eps) * (vi.w + a3.y))
+                                : (cc.viscC * fmin(dvdr, 0.0)) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
         const double sp = NT1 ? (xi.w + a1.y + fv) * w : cc.mm * ((xi.w + a1.y + fv) * w);
         tfx = dx * sp;
         tfy = dy * sp;

@@ -23,9 +23,15 @@
 // Every Transport call here is collective over ALL ranks of the world (as LocalTransport's:
 // the engine issues the same sequence of calls on every brick); a send is matched to the
 // receiver's request by (source, order of posting), as ncclSend/ncclRecv pairs are.
-// Barriers time out (SPH_IPC_TIMEOUT seconds, default 120) with SPH_HIP_ECOMM instead of
-// hanging when a peer died.
+// Liveness: every rank runs a heartbeat thread that stamps its slot (CLOCK_MONOTONIC, shared
+// by the node's processes) every 50 ms while its world exists, so a waiting rank tells a peer
+// that is busy (a long setup or first rebuild: it still beats) from one that is gone (its
+// beat stops when the process exits or is killed): a barrier fails with SPH_HIP_ECOMM once a
+// peer has not beaten for SPH_IPC_DEAD seconds (default 10), and otherwise waits as long as
+// the work takes (SPH_IPC_TIMEOUT > 0 bounds the wait anyway; default none).  Rank 0
+// removes host outboxes a killed run of the same world name left in /dev/shm.
 #pragma once
+#include <dirent.h>
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
@@ -37,7 +43,9 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sph_comm.h"
@@ -64,6 +72,7 @@ struct IpcRankSlot {
   int npost;
   IpcPost post[IPC_MAXPOST];
   int cnt[IPC_MAXR];          // exchange_counts_all: what this rank sends to each rank
+  std::atomic<int64_t> beat;  // CLOCK_MONOTONIC ns of the rank's last heartbeat (0: none)
 };
 
 struct IpcShm {
@@ -89,11 +98,14 @@ class IpcTransport : public Transport {
     SPH_REQUIRE(name && name[0] == '/' && strlen(name) < 200 && !strchr(name + 1, '/'),
                 SPH_HIP_EINVAL, "ipc world name must be '/word' (got '%s')", name ? name : "");
     const char *t = getenv("SPH_IPC_TIMEOUT");
-    timeout_s_ = t ? atof(t) : 120.0;
+    timeout_s_ = t ? atof(t) : 0.0;
+    const char *dd = getenv("SPH_IPC_DEAD");
+    dead_s_ = dd ? atof(dd) : 10.0;
     const size_t sz = sizeof(IpcShm);
     int fd = -1;
     if (rank == 0) {
       shm_unlink(name);  // a stale segment of a killed run
+      unlink_stale_outboxes();
       fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
       SPH_REQUIRE(fd >= 0, SPH_HIP_ECOMM, "shm_open(%s): %s", name, strerror(errno));
       if (ftruncate(fd, (off_t)sz) != 0) {
@@ -110,7 +122,7 @@ class IpcTransport : public Transport {
           close(fd);
           fd = -1;
         }
-        SPH_REQUIRE(elapsed(t0) < timeout_s_, SPH_HIP_ECOMM,
+        SPH_REQUIRE(elapsed(t0) < attach_s_, SPH_HIP_ECOMM,
                     "ipc world %s: rank 0 never created it", name);
         usleep(2000);
       }
@@ -129,7 +141,7 @@ class IpcTransport : public Transport {
     } else {
       const auto t0 = std::chrono::steady_clock::now();
       while (w_->magic.load(std::memory_order_acquire) != IPC_MAGIC) {
-        SPH_REQUIRE(elapsed(t0) < timeout_s_, SPH_HIP_ECOMM, "ipc world %s never initialised", name);
+        SPH_REQUIRE(elapsed(t0) < attach_s_, SPH_HIP_ECOMM, "ipc world %s never initialised", name);
         usleep(1000);
       }
       SPH_REQUIRE(w_->n == nranks && w_->mode == mode, SPH_HIP_ECOMM,
@@ -138,6 +150,14 @@ class IpcTransport : public Transport {
     }
     w_->r[me_].gen.store(0);
     w_->r[me_].npost = 0;
+    w_->r[me_].beat.store(now_ns(), std::memory_order_release);
+    beater_ = std::thread([this] {
+      while (!stop_.load(std::memory_order_acquire)) {
+        w_->r[me_].beat.store(now_ns(), std::memory_order_release);
+        struct timespec ts = {0, 50000000};
+        nanosleep(&ts, nullptr);
+      }
+    });
     w_->attached.fetch_add(1);
     peer_.assign(n_, Peer());
     host_barrier();  // everyone attached: the name can go (no leftover in /dev/shm)
@@ -145,6 +165,8 @@ class IpcTransport : public Transport {
   }
 
   ~IpcTransport() override {
+    stop_.store(true, std::memory_order_release);
+    if (beater_.joinable()) beater_.join();
     for (auto &p : peer_) close_peer(p);
     if (dbox_) (void)hipFree(dbox_);
     if (hbox_) munmap(hbox_, hcap_);
@@ -221,6 +243,33 @@ class IpcTransport : public Transport {
   static double elapsed(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  static int64_t now_ns() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+  }
+  // a peer that has beaten once and not for dead_s_ seconds is gone (its process exited)
+  void check_peers() const {
+    const int64_t now = now_ns();
+    for (int r = 0; r < n_; r++) {
+      if (r == me_) continue;
+      const int64_t b = w_->r[r].beat.load(std::memory_order_acquire);
+      SPH_REQUIRE(b == 0 || (double)(now - b) * 1e-9 < dead_s_, SPH_HIP_ECOMM,
+                  "ipc world %s: rank %d has not beaten for %.1f s (its process exited?)",
+                  name_.c_str(), r, (double)(now - b) * 1e-9);
+    }
+  }
+  // the host outboxes (name.rR.gG) a killed run of this world name left behind
+  void unlink_stale_outboxes() const {
+    DIR *d = opendir("/dev/shm");
+    if (!d) return;
+    const std::string pre = name_.substr(1) + ".r";
+    std::vector<std::string> gone;
+    while (const struct dirent *e = readdir(d))
+      if (strncmp(e->d_name, pre.c_str(), pre.size()) == 0) gone.push_back(std::string("/") + e->d_name);
+    closedir(d);
+    for (const auto &g : gone) shm_unlink(g.c_str());
+  }
 
   // all ranks meet; bounded wait
   void host_barrier() {
@@ -236,10 +285,12 @@ class IpcTransport : public Transport {
         sched_yield();
         continue;
       }
-      if ((spin & 255) == 0)
-        SPH_REQUIRE(elapsed(t0) < timeout_s_, SPH_HIP_ECOMM,
-                    "ipc world %s: rank %d waited %.0f s at a barrier (a peer died?)",
-                    name_.c_str(), me_, timeout_s_);
+      if ((spin & 255) == 0) {
+        check_peers();
+        SPH_REQUIRE(timeout_s_ <= 0.0 || elapsed(t0) < timeout_s_, SPH_HIP_ECOMM,
+                    "ipc world %s: rank %d waited %.0f s at a barrier", name_.c_str(), me_,
+                    timeout_s_);
+      }
       struct timespec ts = {0, 20000};
       nanosleep(&ts, nullptr);
     }
@@ -384,7 +435,11 @@ class IpcTransport : public Transport {
 
   std::string name_;
   int n_, me_, mode_;
-  double timeout_s_ = 120.0;
+  double timeout_s_ = 0.0;   // SPH_IPC_TIMEOUT: bound on a barrier wait (0: none)
+  double dead_s_ = 10.0;     // SPH_IPC_DEAD: a peer silent this long is gone
+  double attach_s_ = 120.0;  // creating / joining the world
+  std::atomic<bool> stop_{false};
+  std::thread beater_;
   IpcShm *w_ = nullptr;
   std::vector<Peer> peer_;
   unsigned char *dbox_ = nullptr;

@@ -79,13 +79,17 @@ struct Mp2Pair {
   double hcsq, hih, halpha2;  // heatconduction/phasechange (2 alpha)
   double htc;
   int hfix, pad;
+  // the gather's per-pair-type constants: s = 3 r / h as r * k3, dW/dr norm (mp2_dwnorm)
+  double tk3, tdn, sk3, sdn, hk3, hdn;
 };
 struct Mp2Type {
   double B, rho0i, gamma, rbg;
 };
 
 // stage the tables of pair types and types into LDS (every thread of the block calls it)
-__device__ __forceinline__ void mp2_tables(const MpCoefs *c, Mp2Pair *sp, Mp2Type *st) {
+__device__ __forceinline__ double mp2_dwnorm(int dim, double ih);
+__device__ __forceinline__ void mp2_tables(const MpCoefs *c, Mp2Pair *sp, Mp2Type *st,
+                                           int dim) {
   const int nt1 = c->ntypes + 1;
   for (int p = threadIdx.x; p < nt1 * nt1; p += blockDim.x) {
     Mp2Pair q;
@@ -105,6 +109,12 @@ __device__ __forceinline__ void mp2_tables(const MpCoefs *c, Mp2Pair *sp, Mp2Typ
     q.htc = c->htc[p];
     q.hfix = c->hfix[p];
     q.pad = 0;
+    q.tk3 = 3.0 * q.tih;
+    q.tdn = mp2_dwnorm(dim, q.tih);
+    q.sk3 = 3.0 * q.sih;
+    q.sdn = mp2_dwnorm(dim, q.sih);
+    q.hk3 = 3.0 * q.hih;
+    q.hdn = mp2_dwnorm(dim, q.hih);
     sp[p] = q;
   }
   for (int t = threadIdx.x; t < nt1; t += blockDim.x)
@@ -128,7 +138,7 @@ template <int G>
 __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
-  mp2_tables(a.mc, s_p, s_t);
+  mp2_tables(a.mc, s_p, s_t, a.dim);
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (row >= a.inum) return;
@@ -172,7 +182,7 @@ template <int G>
 __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
-  mp2_tables(a.mc, s_p, s_t);
+  mp2_tables(a.mc, s_p, s_t, a.dim);
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (row >= a.inum) return;
@@ -278,7 +288,7 @@ template <int G, bool TAIT, bool SURF, bool HEAT, bool POW = true>
 __global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
-  mp2_tables(a.mc, s_p, s_t);
+  mp2_tables(a.mc, s_p, s_t, a.dim);
   const int row = (int)((xcd_block() * blockDim.x + threadIdx.x) / G);
   const int lane = threadIdx.x & (G - 1);
   if (row >= a.inum) return;
@@ -307,11 +317,9 @@ __global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
     if (!(ct || cs || ch)) return;
     double r, ir;
     mp2_r_ir(rsq, r, ir);
-    const double qt = ct ? q5_dw(3.0 * (r * q.tih)) * mp2_dwnorm(dim, q.tih) : 0.0;
-    const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt
-                                  : q5_dw(3.0 * (r * q.sih)) * mp2_dwnorm(dim, q.sih);
-    const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt
-                                 : q5_dw(3.0 * (r * q.hih)) * mp2_dwnorm(dim, q.hih);
+    const double qt = ct ? q5_dw(r * q.tk3) * q.tdn : 0.0;
+    const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt : q5_dw(r * q.sk3) * q.sdn;
+    const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt : q5_dw(r * q.hk3) * q.hdn;
     const double iri = fi ? irFi : irSi, irj = mp_rcp(rhoj);
     const double Vi = mi * iri, Vj = mj * irj;
     const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;
@@ -331,17 +339,24 @@ __global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
       fz += dz * fpair + (v4i.z - v4j.z) * fvisc;
     }
     if (SURF && cs) {  // pair_sph_surfacetension.cpp:100-190
+      // S_i + S_j = (a_i + a_j) e - (b_i w_i + b_j w_j), a = |w|^2 V^2 / ndim, b = (w.e) V^2
+      // (mp2_svec of both sides, collected)
       const double3 e = make_double3(dx * ir, dy * ir, dim == 3 ? dz * ir : 0.0);
-      const double3 Si = mp2_svec(dim, ci, e, Vi2), Sj = mp2_svec(dim, cj, e, Vj2);
-      fx += (Si.x + Sj.x) * qs;
-      fy += (Si.y + Sj.y) * qs;
-      if (dim == 3) fz += (Si.z + Sj.z) * qs;
+      const double kd = dim == 3 ? (1.0 / 3.0) : 0.5;
+      const double wi2 = ci.x * ci.x + ci.y * ci.y + ci.z * ci.z;
+      const double wj2 = cj.x * cj.x + cj.y * cj.y + cj.z * cj.z;
+      const double A = kd * fma(wi2, Vi2, wj2 * Vj2);
+      const double bi = (ci.x * e.x + ci.y * e.y + ci.z * e.z) * Vi2;
+      const double bj = (cj.x * e.x + cj.y * e.y + cj.z * e.z) * Vj2;
+      fx = fma(fma(A, e.x, -fma(bi, ci.x, bj * cj.x)), qs, fx);
+      fy = fma(fma(A, e.y, -fma(bi, ci.y, bj * cj.y)), qs, fy);
+      if (dim == 3) fz = fma(fma(A, e.z, -fma(bi, ci.z, bj * cj.z)), qs, fz);
     }
     if (HEAT && ch) {  // pair_sph_heatconduction_phasechange.cpp:101-136
       double Tp = Ti, Tq = v4j.w;
       if (q.hfix == ti && Tp < Tq) Tp = q.htc;
       if (q.hfix == tj && Tq < Tp) Tq = q.htc;
-      dE += q.halpha2 * (Tp - Tq) * (qh * ir) * (iri * irj) * mj;
+      dE += q.halpha2 * (Tp - Tq) * (qh * ir) * (iri * Vj);  // (m_j / rho_j = V_j)
     }
   };
   // the records of entry jr: x (with the mass), v (with T), and j's colour-gradient record,

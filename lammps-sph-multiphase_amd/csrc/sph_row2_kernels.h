@@ -142,6 +142,16 @@ __device__ __forceinline__ double sqrt1(double x) {
   const double r = x * y;
   return fma(fma(-r, r, x), 0.5 * y, r);
 }
+// the same for an x that already carries the 1e-300 (rsq_t: folded into its first product)
+__device__ __forceinline__ double sqrt1n(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double r = x * y;
+  return fma(fma(-r, r, x), 0.5 * y, r);
+}
+// dx^2 + dy^2 + dz^2 + 1e-300 in three FMAs (sqrt1n's argument)
+__device__ __forceinline__ double rsq_t(double dx, double dy, double dz) {
+  return fma(dx, dx, fma(dy, dy, fma(dz, dz, 1e-300)));
+}
 
 // byte size of n records of T for the range check (the host guarantees < 2 GiB)
 template <class T>

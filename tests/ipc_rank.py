@@ -71,6 +71,8 @@ def main():
         eng.set_atoms(s.x[sel], s.v[sel], s.type[sel], s.rho[sel], s.e[sel], s.cv[sel])
         eng.set_tags(sel)
     eng.comm_ipc(spec["name"], P, r, spec["mode"])
+    if spec.get("die"):  # (a rank that dies after joining: its heartbeat stops)
+        os._exit(3)
     snaps = {}
 
     def snap(k):
@@ -79,13 +81,19 @@ def main():
         for key, v in g.items():
             snaps[f"{k}/{key}"] = np.asarray(v)
 
-    eng.setup()
-    snap(0)
-    done = 0
-    for upto in spec["snap_steps"]:
-        eng.run(upto - done)
-        done = upto
-        snap(upto)
+    try:
+        eng.setup()
+        snap(0)
+        done = 0
+        for upto in spec["snap_steps"]:
+            eng.run(upto - done)
+            done = upto
+            snap(upto)
+    except sph.HipError as err:
+        if not spec.get("expect_dead"):
+            raise
+        print("PEER_GONE", err, flush=True)
+        os._exit(0)
     st = eng.stats()
     snaps["staged"] = np.asarray(st["staged"])
     snaps["nghost"] = np.asarray(st["nghost"])

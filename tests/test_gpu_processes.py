@@ -139,3 +139,40 @@ def test_processes_c5_phase_change(gpu, tmp_path, mode, pg, dim, nx, drift):
     if drift:
         moved = po.brick_owner(s, ref.s.x[:s.n], pg) != po.brick_owner(s, s.x, pg)
         assert moved.sum() >= 10, "no atom migrated: the hole fill not exercised"
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_ipc_dead_peer_fails_fast(gpu, tmp_path, mode):
+    """A rank that exits after joining the world stops beating: its peer's next barrier
+    fails with SPH_HIP_ECOMM after SPH_IPC_DEAD seconds, instead of waiting out a fixed
+    timeout (or forever) -- and a long legitimate wait is not mistaken for a dead peer."""
+    import time
+    name = f"/sphipc_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    env = dict(os.environ, SPH_IPC_DEAD="3")
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        spec = dict(scenario="c2", mode=mode, pg=[2, 1, 1], snap_steps=[1], rank=r, nranks=2,
+                    name=name, out=str(tmp_path / f"rank{r}.npz"), die=(r == 1),
+                    expect_dead=(r == 0))
+        sp = tmp_path / f"spec{r}.json"
+        sp.write_text(json.dumps(spec))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_rank.py"),
+                                       str(sp)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    logs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=120)
+            logs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert procs[1].returncode == 3
+    assert procs[0].returncode == 0, logs[0][-3000:]
+    assert "PEER_GONE" in logs[0] and "has not beaten" in logs[0], logs[0][-3000:]
+    assert time.time() - t0 < 100
+    left = [f for f in os.listdir("/dev/shm") if f.startswith(name[1:])]
+    assert left == [] or mode == 1, left

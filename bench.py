@@ -985,9 +985,10 @@ def c5_main(args, sph, dist=None, rank=0, world=1, dev=0):
                    "n_full_per_particle": n_full, "n_half_per_particle": n_half,
                    "atoms_inserted": ins, "dt": dt, "parallelism": par},
         "roofline": {"bound": "hbm",
-                     "kernel": "k_mp_gather (taitwater/multiphase + surfacetension + "
+                     "kernel": "k_mp2_gather (taitwater/multiphase + surfacetension + "
                                "heatconduction/phasechange fused: full-list gather, each pair "
-                               "in its half-list orientation)",
+                               "in its half-list orientation; the symmetric-style gather of "
+                               "sph_mp2_kernels.h, every gamma equal as bubble.lmp)",
                      "achieved": ach_half, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": ach_half / PEAK_HBM_GBS, "traffic": None,
                      "bytes_per_particle": b_half, "ms_per_launch": ms_half},
@@ -1334,7 +1335,7 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args, fname="pmc_traffic.js
     the kernel, config and commit it was taken on.  Attached as `traffic` only when that
     record matches this run (same kernel family, single GPU, same lattice edge and steps);
     otherwise it is omitted (traffic null) rather than reported from another configuration."""
-    for rnd in ("r04", "r03", "r02"):
+    for rnd in ("r05", "r04", "r03", "r02"):
         tj = os.path.join(ROOT, "profiles", rnd, fname)
         if not os.path.exists(tj):
             continue

@@ -1384,18 +1384,22 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
 #define SPH_BLK_OCC
 #endif
 
+#define SPH_BLK_FORCE_PARAMS                                                              \
+  int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,                 \
+      const unsigned short *__restrict__ snbr, int sstride, const int *__restrict__ rcnt,     \
+      const double4 *__restrict__ xf, const double4 *__restrict__ vr,                         \
+      const int *__restrict__ ty, const double *__restrict__ en,                              \
+      const Coefs *__restrict__ cf, double4 *__restrict__ fo, double *__restrict__ de,        \
+      double gx, double gy, double gz, int um, int cq,                                        \
+      const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,                  \
+      const int *__restrict__ moved, int n3, const unsigned char *__restrict__ bperm,         \
+      const int *__restrict__ uilist, const int *__restrict__ uicnt
+#define SPH_BLK_FORCE_ARGS                                                                \
+  n, ulist, ucnt, ucap, snbr, sstride, rcnt, xf, vr, ty, en, cf, fo, de, gx, gy, gz, um, cq, \
+      snbi, icnt, moved, n3, bperm, uilist, uicnt
+// (the body of the force pass; the kernels below differ only in their occupancy request)
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
-__global__ void __launch_bounds__(R * G) SPH_BLK_OCC
-k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
-            const unsigned short *__restrict__ snbr, int sstride,
-            const int *__restrict__ rcnt, const double4 *__restrict__ xf,
-            const double4 *__restrict__ vr, const int *__restrict__ ty,
-            const double *__restrict__ en, const Coefs *__restrict__ cf,
-            double4 *__restrict__ fo, double *__restrict__ de, double gx, double gy,
-            double gz, int um, int cq, const unsigned short *__restrict__ snbi,
-            const int *__restrict__ icnt, const int *__restrict__ moved, int n3,
-            const unsigned char *__restrict__ bperm, const int *__restrict__ uilist,
-            const int *__restrict__ uicnt) {
+__device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
     rcnt = icnt;
@@ -1655,6 +1659,20 @@ k_blk_force(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   }
 }
 
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+__global__ void __launch_bounds__(R * G) SPH_BLK_OCC k_blk_force(SPH_BLK_FORCE_PARAMS) {
+  blk_force_body<R, G, U, NCH, VISC, MODE, NT1, EXP>(SPH_BLK_FORCE_ARGS);
+}
+// one type, taitwater alone (C2): asked for 5 waves per SIMD (<= 96 VGPRs, no spill) -- the
+// compiler otherwise settles at 98 VGPRs, 4 waves, while the LDS image admits 6
+// (0.2550 vs 0.272-0.273 ms per launch on one box, profiles/r05/README.md); the heat and
+// multi-type variants keep the default (at 96 VGPRs they would spill)
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+__global__ void __launch_bounds__(R * G) __attribute__((amdgpu_waves_per_eu(5, 5)))
+k_blk_force_w5(SPH_BLK_FORCE_PARAMS) {
+  blk_force_body<R, G, U, NCH, VISC, MODE, NT1, EXP>(SPH_BLK_FORCE_ARGS);
+}
+
 // blocks of a build whose union exceeds the force pass's LDS image (um records): the pass
 // walks them in windows of um union records (statistics only, sph_engine_stats blk_nbig)
 static __global__ void k_blk_count_big(int nb, const int *__restrict__ ucnt, int um,
@@ -1912,7 +1930,12 @@ inline void blk_rhosum(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, c
 
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
 inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
-  auto fn = k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;
+  auto fn = [] {
+    if constexpr (NT1 && MODE == M_TAIT && EXP == 0 && NCH > 0 && SPH_BLK_WPE == 0)
+      return k_blk_force_w5<R, G, U, NCH, VISC, MODE, NT1, EXP>;
+    else
+      return k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;
+  }();
   // one launch: every block, its union in windows of umf records where it exceeds the image
   size_t lds = blk_lds(k.umf, k.cq, NT1);
 #ifdef SPH_STUDY  // (SPH_LDS_PAD: extra LDS per workgroup, an occupancy study)

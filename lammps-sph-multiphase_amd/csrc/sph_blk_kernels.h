@@ -431,6 +431,10 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
 // Overflow (> BLK_MCAP raw or BLK_SCAP kept candidates, or a bin box wider than BLK_TBL
 // bin-rows) raises *ovf and the host falls back to k_blk_neigh.
 constexpr int BLK_SCAP = 2048;  // kept candidates per block (k_blk_build)
+// ... in the small variant, chosen when the previous build's largest block fitted it: 36 KiB
+// of LDS, four workgroups per CU instead of three (a block past it raises 1 << 24 and the
+// host builds again with BLK_SCAP)
+constexpr int BLK_SCAP_S = 1280;
 // set bits of a wave-uniform 64-bit mask below this lane (v_mbcnt_lo / v_mbcnt_hi)
 __device__ __forceinline__ int blk_mbcnt(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
@@ -460,7 +464,7 @@ __device__ __forceinline__ unsigned long long blk_uniform64(unsigned long long x
 // once, by its earlier row, which also accumulates the later row's share (the pair passes'
 // LDS accumulators).  rcnt/icnt then hold the rows' stored (N3) counts and fcnt the full
 // counts (Neighbor::full_bin's, for the neighbour statistics).
-template <int R, int G, int U, bool NT1, bool INNER, bool N3, int BEXP = 0>
+template <int R, int G, int U, bool NT1, bool INNER, bool N3, int BEXP = 0, int SC = BLK_SCAP>
 __global__ void __launch_bounds__(256)
 k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             const int *__restrict__ ty, const double4 *__restrict__ xb,
@@ -471,7 +475,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
             int *__restrict__ ovf, int *__restrict__ umax, int cq, int *__restrict__ fcnt,
             unsigned char *__restrict__ bperm, int *__restrict__ uilist,
             int *__restrict__ uicnt, int *__restrict__ kcnt) {
-  constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = BLK_SCAP / 64;
+  constexpr int NT = 256, NW = NT / 64, MCH = BLK_MCAP / 64, SCH = SC / 64;
   constexpr int RPW = R / NW, UG = U * G, WS = INNER ? 2 : 1;
   // the INNER UNION (uilist != nullptr): the inner rows index a union of their own -- the
   // atoms some inner row names, ~15 % fewer than the full union at C2 -- so the passes stage
@@ -489,7 +493,7 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
   __shared__ int s_upi[INNER ? SCH + 1 : 1];
   __shared__ unsigned short s_q[SCH][64];
   __shared__ unsigned long long s_keep[MCH];
-  __shared__ int s_cpos[BLK_SCAP];
+  __shared__ int s_cpos[SC];
   __shared__ int s_upre[SCH + 1], s_kpre[MCH + 1];
   __shared__ int s_pre[BLK_TBL + 1], s_st[BLK_TBL];
   __shared__ double4 s_row[R];
@@ -622,8 +626,8 @@ k_blk_build(int n, QBins q, int dim, const double4 *__restrict__ xf,
     const int ex = blk_scan<NT>(v, s_sc, &K);
     if (tid < mch) s_kpre[tid] = ex;
   }
-  if (K > BLK_SCAP) {  // workgroup-uniform
-    if (tid == 0) atomicMax(ovf, 1 << 22);
+  if (K > SC) {  // workgroup-uniform
+    if (tid == 0) atomicMax(ovf, SC < BLK_SCAP ? (1 << 24) : (1 << 22));
     return;
   }
   __syncthreads();
@@ -1033,13 +1037,36 @@ __device__ __forceinline__ int wave_max_count(int c) {
   for (int d = (G == 8 && SPH_BLK_LMAP) ? 1 : G; d < 64; d <<= 1) c = max(c, __shfl_xor(c, d, 64));
   return __builtin_amdgcn_readfirstlane(c);
 }
-template <int G, int U, int NCH, class Load, class Body>
+// AHEAD = 0: no records read ahead (each group reads its own, fewer VGPRs -- for a pass
+// run at more waves per SIMD, whose other waves cover the LDS latency instead)
+template <int AHEAD = 1, int G, int U, int NCH, class Load, class Body>
 __device__ __forceinline__ void blk_walk3(BlkSlots<G, U, NCH> &sw, int cmax, Load load,
                                           Body body) {
   static_assert(NCH > 0, "walk3: rows held in registers");
   constexpr int NS = NCH * U;
   if (cmax <= 0) return;
   typedef decltype(load(0)) Rec;
+  if constexpr (AHEAD == 0) {
+    constexpr int IL = SPH_BLK_ILP, NG = (NS + IL - 1) / IL;
+    auto group0 = [&](auto gc) -> bool {
+      constexpr int g = decltype(gc)::value;
+      if (g * IL * G >= cmax) return false;  // (wave-uniform)
+      Rec r[IL];
+      blk_steps_([&](auto sc) -> bool {
+        constexpr int s = g * IL + decltype(sc)::value;
+        if constexpr (s < NS) r[decltype(sc)::value] = load(SlotWord<U>::get(sw.w[s / U], s % U));
+        return true;
+      }, std::make_integer_sequence<int, IL>{});
+      blk_steps_([&](auto sc) -> bool {
+        constexpr int s = g * IL + decltype(sc)::value;
+        if constexpr (s < NS) body(r[decltype(sc)::value]);
+        return true;
+      }, std::make_integer_sequence<int, IL>{});
+      return true;
+    };
+    blk_steps_(group0, std::make_integer_sequence<int, NG>{});
+    return;
+  }
   // ILP steps form a group: the group's pair evaluations share one basic block (the scheduler
   // interleaves their dependency chains); the records of the next group are read before it.
   // A group runs whole once its first step is inside the wave's longest row (its later
@@ -1398,7 +1425,7 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
   n, ulist, ucnt, ucap, snbr, sstride, rcnt, xf, vr, ty, en, cf, fo, de, gx, gy, gz, um, cq, \
       snbi, icnt, moved, n3, bperm, uilist, uicnt
 // (the body of the force pass; the kernels below differ only in their occupancy request)
-template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0, int AHEAD = 1>
 __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
@@ -1598,7 +1625,7 @@ __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   auto walk = [&](auto ld) {
     if constexpr (NCH > 0 && SPH_BLK_WALK == 1) {
       if (!n3on)
-        blk_walk3(sw, wave_max_count<G>(c), ld, pair);
+        blk_walk3<AHEAD>(sw, wave_max_count<G>(c), ld, pair);
       else
         blk_walk2(sw, c, lane, ld, pair);
     } else {
@@ -1672,6 +1699,18 @@ __global__ void __launch_bounds__(R * G) __attribute__((amdgpu_waves_per_eu(5, 5
 k_blk_force_w5(SPH_BLK_FORCE_PARAMS) {
   blk_force_body<R, G, U, NCH, VISC, MODE, NT1, EXP>(SPH_BLK_FORCE_ARGS);
 }
+// ... and at 6 waves per SIMD (<= 80 VGPRs: what the 49 KiB image allows, three workgroups
+// per CU) with no records read ahead -- the other waves cover the LDS latency: 0.2435 /
+// 0.2497 vs 0.2632 / 0.2627 ms per launch (two A/B pairs on one box, profiles/r05/README.md).
+// Production for C2; SPH_BLK_W6=0 (study) keeps the 5-wave kernel with the read-ahead.
+template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
+__global__ void __launch_bounds__(R * G) __attribute__((amdgpu_waves_per_eu(6, 6)))
+k_blk_force_w6(SPH_BLK_FORCE_PARAMS) {
+  blk_force_body<R, G, U, NCH, VISC, MODE, NT1, EXP, 0>(SPH_BLK_FORCE_ARGS);
+}
+#ifndef SPH_BLK_W6
+#define SPH_BLK_W6 1
+#endif
 
 // blocks of a build whose union exceeds the force pass's LDS image (um records): the pass
 // walks them in windows of um union records (statistics only, sph_engine_stats blk_nbig)
@@ -1819,15 +1858,19 @@ inline void blk_build_t(hipStream_t s, int n, const QBins &q, int dim, const dou
                         int *rcnt, unsigned short *snbr, int *icnt, unsigned short *snbi,
                         int *ovf, int *umax, int cq, int bexp, int *fcnt, unsigned char *bperm,
                         int *uilist, int *uicnt, int *kcnt) {
+  // (bexp bit 8: the small candidate image, BLK_SCAP_S)
+  const bool small = (bexp & 0x100) != 0;
+  bexp &= 0xff;
 #ifdef SPH_STUDY
   auto fn = bexp == 1 ? k_blk_build<R, G, U, NT1, INNER, N3, 1>
           : bexp == 2 ? k_blk_build<R, G, U, NT1, INNER, N3, 2>
           : bexp == 3 ? k_blk_build<R, G, U, NT1, INNER, N3, 3>
           : bexp == 4 ? k_blk_build<R, G, U, NT1, INNER, N3, 4>
+          : small     ? k_blk_build<R, G, U, NT1, INNER, N3, 0, BLK_SCAP_S>
                       : k_blk_build<R, G, U, NT1, INNER, N3, 0>;
 #else
-  (void)bexp;
-  auto fn = k_blk_build<R, G, U, NT1, INNER, N3, 0>;
+  auto fn = small ? k_blk_build<R, G, U, NT1, INNER, N3, 0, BLK_SCAP_S>
+                  : k_blk_build<R, G, U, NT1, INNER, N3, 0>;
 #endif
   hipLaunchKernelGGL(fn, dim3(blk_blocks(n, R)), dim3(256), 0, s, n, q, dim, xf, ty, xb, tb,
                      qbeg, cf, ucap, sstride, ulist, ucnt, rcnt, snbr, icnt, snbi, ovf, umax, cq,
@@ -1931,7 +1974,9 @@ inline void blk_rhosum(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, c
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0>
 inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
   auto fn = [] {
-    if constexpr (NT1 && MODE == M_TAIT && EXP == 0 && NCH > 0 && SPH_BLK_WPE == 0)
+    if constexpr (NT1 && MODE == M_TAIT && EXP == 0 && NCH > 0 && SPH_BLK_WPE == 0 && SPH_BLK_W6)
+      return k_blk_force_w6<R, G, U, NCH, VISC, MODE, NT1, EXP>;
+    else if constexpr (NT1 && MODE == M_TAIT && EXP == 0 && NCH > 0 && SPH_BLK_WPE == 0)
       return k_blk_force_w5<R, G, U, NCH, VISC, MODE, NT1, EXP>;
     else
       return k_blk_force<R, G, U, NCH, VISC, MODE, NT1, EXP>;

@@ -324,6 +324,8 @@ struct sph_engine {
   DBuf<unsigned short> snbr;
   // the inner rows' own union (k_blk_build / k_blk_inner): a smaller LDS image for the passes
   DBuf<int> uilist, uicnt;
+  bool blk_ksmall = false;  // k_blk_build with the small candidate image (BLK_SCAP_S)
+  int blk_kover = 0;        // ... builds it overflowed
   bool blk_iu = false;  // (the inner rows index uilist; else the full union)
   // ... and the inner rows of the build (k_blk_inner: pairs within cut + inner_margin), the
   // owned positions they were written at and the flag that retires them (sc.x0 / sc.moved)
@@ -1621,7 +1623,8 @@ struct sph_engine {
         blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
                   qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
                   blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
-                  study_int("SPH_BEXP", 0), ccnt.p, rowsort() ? bperm_buf(nb, sh.R) : nullptr,
+                  study_int("SPH_BEXP", 0) | (blk_ksmall ? 0x100 : 0), ccnt.p,
+                  rowsort() ? bperm_buf(nb, sh.R) : nullptr,
                   iu ? uilist.p : nullptr, iu ? uicnt.p : nullptr, kcnt.p);
       else
         blk_neigh(shape, big, nt1(), s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p, xpos.p,
@@ -1644,11 +1647,20 @@ struct sph_engine {
         try2 = false;
         continue;
       }
+      if (hm[0] == (1 << 24)) {  // a block outgrew the small candidate image
+        blk_ksmall = false;
+        blk_kover++;
+        continue;
+      }
       if (hm[0] == (1 << 21)) {  // a row outgrew the slot-row stride
         blk_rowcap *= 2;
         continue;
       }
       if (hm[0] != 0) return 2;
+      // the next build takes the small candidate image (four workgroups per CU) while this
+      // one's largest block fits it with room (hm[2]: the largest candidate set); after two
+      // overflows it stays with the large one
+      if (v2 && !v3) blk_ksmall = blk_kover < 2 && hm[2] <= BLK_SCAP_S * 15 / 16;
       // the largest union's force-pass LDS image (+ the static coefficient tables) must fit
       // the CU's 160 KiB
       blk_sh = shape;

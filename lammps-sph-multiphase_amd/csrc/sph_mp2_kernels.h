@@ -29,7 +29,7 @@ namespace sph {
 
 // list entries per lane whose loads are issued together (study builds: -DSPH_MP2_NU=n)
 #ifndef SPH_MP2_NU
-#define SPH_MP2_NU 2
+#define SPH_MP2_NU 4  // (colorgradient at C5 4M: 1.362 vs 1.471 ms with 2, profiles/r05)
 #endif
 // ... in the fused gather: one (its three records per entry; 128 VGPRs = 4 waves per SIMD
 // with gamma = 1, against 156 = 3 waves with two: 4.36 vs 4.53 ms per C5 step,

@@ -431,10 +431,10 @@ k_blk_neigh(int n, QBins q, int dim, const double4 *__restrict__ xf, const int *
 // Overflow (> BLK_MCAP raw or BLK_SCAP kept candidates, or a bin box wider than BLK_TBL
 // bin-rows) raises *ovf and the host falls back to k_blk_neigh.
 constexpr int BLK_SCAP = 2048;  // kept candidates per block (k_blk_build)
-// ... in the small variant, chosen when the previous build's largest block fitted it: 36 KiB
+// ... in the small variant, chosen when the previous build's largest block fitted it: 40 KiB
 // of LDS, four workgroups per CU instead of three (a block past it raises 1 << 24 and the
-// host builds again with BLK_SCAP)
-constexpr int BLK_SCAP_S = 1280;
+// host builds again with BLK_SCAP).  C2 1M: largest kept set 1489-1494, mean 1017
+constexpr int BLK_SCAP_S = 1536;
 // set bits of a wave-uniform 64-bit mask below this lane (v_mbcnt_lo / v_mbcnt_hi)
 __device__ __forceinline__ int blk_mbcnt(unsigned long long m) {
   return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),

@@ -1658,9 +1658,9 @@ struct sph_engine {
       }
       if (hm[0] != 0) return 2;
       // the next build takes the small candidate image (four workgroups per CU) while this
-      // one's largest block fits it with room (hm[2]: the largest candidate set); after two
-      // overflows it stays with the large one
-      if (v2 && !v3) blk_ksmall = blk_kover < 2 && hm[2] <= BLK_SCAP_S * 15 / 16;
+      // one's largest block fits it (hm[2]: the largest candidate set; the blocks' sets move
+      // by a few candidates between rebuilds); after two overflows it stays with the large one
+      if (v2 && !v3) blk_ksmall = blk_kover < 2 && hm[2] <= BLK_SCAP_S - 24;
       // the largest union's force-pass LDS image (+ the static coefficient tables) must fit
       // the CU's 160 KiB
       blk_sh = shape;

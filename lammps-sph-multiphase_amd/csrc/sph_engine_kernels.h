@@ -352,44 +352,70 @@ static __global__ void k_append_ghosts_dev(
 // two swaps' counts; k_brd_scan (one block): their exclusive prefixes and the new atom
 // counts nalls[1] = n + T0, nalls[2] = n + T0 + T1; k_brd_scatter: the ghosts, in scan
 // order (a block-wide prefix per swap), as k_append_ghosts_dev writes them.
-constexpr int BRD_T = 256, BRD_IT = 4, BRD_CH = BRD_T * BRD_IT;
+constexpr int BRD_T = 256, BRD_IT = 4, BRD_CH = BRD_T * BRD_IT, BRD_W = BRD_T / 64;
 __device__ __forceinline__ double brd_coord(const double4 &x, int d) {
   return d == 0 ? x.x : (d == 1 ? x.y : x.z);
+}
+// A block's BRD_CH atoms in BRD_IT rounds of BRD_T consecutive ones (round k: atom
+// blockIdx.x * BRD_CH + k * BRD_T + threadIdx.x -- coalesced loads), and each selected
+// atom's rank among the block's selected atoms in scan order (round by round, lanes in
+// order): per round and wave a ballot, the waves' counts in LDS, one prefix per thread.
+struct BrdSel {
+  bool f0[BRD_IT], f1[BRD_IT];
+  int r0[BRD_IT], r1[BRD_IT];  // ranks within the block (valid where selected)
+  int t0, t1;                  // the block's totals
+};
+__device__ __forceinline__ void brd_select(BrdSel &s, int n, int d, double lo0, double hi0,
+                                           double lo1, double hi1,
+                                           const double4 *__restrict__ xf) {
+  __shared__ int sw0[BRD_IT][BRD_W], sw1[BRD_IT][BRD_W];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int lp0[BRD_IT], lp1[BRD_IT];
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++) {
+    const int i = blockIdx.x * BRD_CH + k * BRD_T + threadIdx.x;
+    bool a = false, b = false;
+    if (i < n) {
+      const double c = brd_coord(xf[i], d);
+      a = c >= lo0 && c <= hi0;
+      b = c >= lo1 && c <= hi1;
+    }
+    s.f0[k] = a;
+    s.f1[k] = b;
+    const unsigned long long m0 = __ballot(a), m1 = __ballot(b);
+    lp0[k] = __popcll(m0 & lt);
+    lp1[k] = __popcll(m1 & lt);
+    if (lane == 0) {
+      sw0[k][w] = __popcll(m0);
+      sw1[k][w] = __popcll(m1);
+    }
+  }
+  __syncthreads();
+  int acc0 = 0, acc1 = 0;
+#pragma unroll
+  for (int k = 0; k < BRD_IT; k++)
+#pragma unroll
+    for (int v = 0; v < BRD_W; v++) {
+      if (v == w) {
+        s.r0[k] = acc0 + lp0[k];
+        s.r1[k] = acc1 + lp1[k];
+      }
+      acc0 += sw0[k][v];
+      acc1 += sw1[k][v];
+    }
+  s.t0 = acc0;
+  s.t1 = acc1;
 }
 static __global__ void __launch_bounds__(BRD_T)
 k_brd_count(const int *__restrict__ nalls, int d, double lo0, double hi0, double lo1, double hi1,
             const double4 *__restrict__ xf, int *__restrict__ bc, int nh = 0) {
-  __shared__ int s0[BRD_T / 64], s1[BRD_T / 64];
   const int n = nalls ? nalls[0] : nh;  // (bricks: the host's count)
-  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
-  int c0 = 0, c1 = 0;
-#pragma unroll
-  for (int k = 0; k < BRD_IT; k++) {
-    const int i = base + k;
-    if (i < n) {
-      const double c = brd_coord(xf[i], d);
-      c0 += (c >= lo0 && c <= hi0) ? 1 : 0;
-      c1 += (c >= lo1 && c <= hi1) ? 1 : 0;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    c0 += __shfl_xor(c0, o, 64);
-    c1 += __shfl_xor(c1, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    s0[threadIdx.x >> 6] = c0;
-    s1[threadIdx.x >> 6] = c1;
-  }
-  __syncthreads();
+  BrdSel s;
+  brd_select(s, n, d, lo0, hi0, lo1, hi1, xf);
   if (threadIdx.x == 0) {
-    int a = 0, b = 0;
-    for (int w = 0; w < BRD_T / 64; w++) {
-      a += s0[w];
-      b += s1[w];
-    }
-    bc[2 * blockIdx.x] = a;
-    bc[2 * blockIdx.x + 1] = b;
+    bc[2 * blockIdx.x] = s.t0;
+    bc[2 * blockIdx.x + 1] = s.t1;
   }
 }
 // exclusive prefix of nb (count0, count1) pairs, in place; one block of 1024 threads
@@ -476,47 +502,25 @@ k_brd_scatter(const int *__restrict__ nalls, const int *__restrict__ bc, int cap
               int *__restrict__ ty, int *__restrict__ gowner, int *__restrict__ gimg,
               int *__restrict__ gsrc, double4 *__restrict__ vel, double *__restrict__ rm,
               double *__restrict__ cv, double4 *__restrict__ cg) {
-  __shared__ int s0[BRD_T], s1[BRD_T];
   const int n = nalls[0], t0 = nalls[1];  // (t0 = n + the lower swap's count, capped)
-  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
-  unsigned f0 = 0, f1 = 0;  // the thread's items' flags
-#pragma unroll
-  for (int k = 0; k < BRD_IT; k++) {
-    const int i = base + k;
-    if (i < n) {
-      const double c = brd_coord(xf[i], d);
-      if (c >= lo0 && c <= hi0) f0 |= 1u << k;
-      if (c >= lo1 && c <= hi1) f1 |= 1u << k;
-    }
-  }
-  const int c0 = __popc(f0), c1 = __popc(f1);
-  s0[threadIdx.x] = c0;
-  s1[threadIdx.x] = c1;
-  __syncthreads();
-  for (int o = 1; o < BRD_T; o <<= 1) {
-    const int a0 = threadIdx.x >= o ? s0[threadIdx.x - o] : 0;
-    const int a1 = threadIdx.x >= o ? s1[threadIdx.x - o] : 0;
-    __syncthreads();
-    s0[threadIdx.x] += a0;
-    s1[threadIdx.x] += a1;
-    __syncthreads();
-  }
-  int p0 = n + bc[2 * blockIdx.x] + s0[threadIdx.x] - c0;
-  int p1 = t0 + bc[2 * blockIdx.x + 1] + s1[threadIdx.x] - c1;
+  BrdSel s;
+  brd_select(s, n, d, lo0, hi0, lo1, hi1, xf);
+  const int b0 = n + bc[2 * blockIdx.x], b1 = t0 + bc[2 * blockIdx.x + 1];
   // (the ghosts are written after every read of this launch's sources: a ghost slot g >= n
-  // is never a source, i < n)
+  // is never a source, i < n -- brd_select's barrier orders this block's reads before its
+  // writes, and other blocks read only atoms below n)
 #pragma unroll
   for (int k = 0; k < BRD_IT; k++) {
-    const int i = base + k;
-    if ((f0 >> k) & 1u) {
+    const int i = blockIdx.x * BRD_CH + k * BRD_T + threadIdx.x;
+    if (s.f0[k]) {
+      const int p0 = b0 + s.r0[k];
       if (p0 < cap && p0 < t0)
         brd_put(i, p0, nlocal, d, 1, prd, xf, vr, en, ty, gowner, gimg, gsrc, vel, rm, cv, cg);
-      p0++;
     }
-    if ((f1 >> k) & 1u) {
+    if (s.f1[k]) {
+      const int p1 = b1 + s.r1[k];
       if (p1 < cap) brd_put(i, p1, nlocal, d, -1, -prd, xf, vr, en, ty, gowner, gimg, gsrc, vel,
                             rm, cv, cg);
-      p1++;
     }
   }
 }
@@ -527,36 +531,14 @@ static __global__ void __launch_bounds__(BRD_T)
 k_brd_lists(int n, const int *__restrict__ bc, int d, double lo0, double hi0, double lo1,
             double hi1, const double4 *__restrict__ xf, int *__restrict__ list0,
             int *__restrict__ list1) {
-  __shared__ int s0[BRD_T], s1[BRD_T];
-  const int base = blockIdx.x * BRD_CH + threadIdx.x * BRD_IT;
-  unsigned f0 = 0, f1 = 0;
+  BrdSel s;
+  brd_select(s, n, d, lo0, hi0, lo1, hi1, xf);
+  const int b0 = bc[2 * blockIdx.x], b1 = bc[2 * blockIdx.x + 1];
 #pragma unroll
   for (int k = 0; k < BRD_IT; k++) {
-    const int i = base + k;
-    if (i < n) {
-      const double c = brd_coord(xf[i], d);
-      if (c >= lo0 && c <= hi0) f0 |= 1u << k;
-      if (c >= lo1 && c <= hi1) f1 |= 1u << k;
-    }
-  }
-  const int c0 = __popc(f0), c1 = __popc(f1);
-  s0[threadIdx.x] = c0;
-  s1[threadIdx.x] = c1;
-  __syncthreads();
-  for (int o = 1; o < BRD_T; o <<= 1) {
-    const int a0 = threadIdx.x >= o ? s0[threadIdx.x - o] : 0;
-    const int a1 = threadIdx.x >= o ? s1[threadIdx.x - o] : 0;
-    __syncthreads();
-    s0[threadIdx.x] += a0;
-    s1[threadIdx.x] += a1;
-    __syncthreads();
-  }
-  int p0 = bc[2 * blockIdx.x] + s0[threadIdx.x] - c0;
-  int p1 = bc[2 * blockIdx.x + 1] + s1[threadIdx.x] - c1;
-#pragma unroll
-  for (int k = 0; k < BRD_IT; k++) {
-    if ((f0 >> k) & 1u) list0[p0++] = base + k;
-    if ((f1 >> k) & 1u) list1[p1++] = base + k;
+    const int i = blockIdx.x * BRD_CH + k * BRD_T + threadIdx.x;
+    if (s.f0[k]) list0[b0 + s.r0[k]] = i;
+    if (s.f1[k]) list1[b1 + s.r1[k]] = i;
   }
 }
 

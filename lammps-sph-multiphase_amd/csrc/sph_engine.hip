@@ -12,6 +12,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <cmath>
 #include <vector>
@@ -2254,6 +2255,13 @@ struct sph_engine {
   // in the collectives (slot keys, reverse comm, counts) and in the finish loop.
   void phase_change() {
     Scope t(this, T_NEIGH);
+    // (SPH_DEBUG: host time between the stages of this call)
+    const bool dbg = env_int("SPH_DEBUG", 0) != 0;
+    std::vector<std::pair<const char *, std::chrono::steady_clock::time_point>> tm;
+    auto mark = [&](const char *w) {
+      if (dbg) tm.emplace_back(w, std::chrono::steady_clock::now());
+    };
+    mark("start");
     if (!lidx_valid) lidx_from_tags();  // (armed after setup: the local order from here on)
     const bool mul = multi();
     const int n = nlocal, nall = nlocal + nghost;
@@ -2316,6 +2324,7 @@ struct sph_engine {
       SPH_HIP_TRY(hipMemcpyAsync(hg.data(), gat.p, hg.size() * sizeof(double), hipMemcpyDeviceToHost, s));
       SPH_HIP_TRY(hipStreamSynchronize(s));
     }
+    mark("readback");
     // the reference meets the candidates in its local order (lidx: read order, exchange hole
     // fill, Atom::sort)
     std::vector<int> ord(ncand);
@@ -2348,7 +2357,9 @@ struct sph_engine {
     Wd.reserve(8);
     std::vector<int> ins_k;
     std::vector<double> ins_rec, ins_W;
+    mark("candidates");
     pc_replay(p, cfg.dim, pc_seed, cands, ins_k, ins_W, ins_rec, recompute);
+    mark("replay");
     const int nins = (int)ins_k.size();
     // MPI_Allreduce(nins) and the tag base of this rank's created atoms (tag_extend: rank
     // order); the first call also agrees on the next free tag
@@ -2378,6 +2389,7 @@ struct sph_engine {
       hW[q] = ins_W[q];
     }
     dmass.reserve(nall > 0 ? nall : 1);
+    mark("host");
     if (nall) SPH_HIP_TRY(hipMemsetAsync(dmass.p, 0, nall * sizeof(double), s));
     if (nins) {
       idx.reserve(nins);
@@ -2413,6 +2425,14 @@ struct sph_engine {
       hipLaunchKernelGGL(k_lidx_iota, dim3(blocks(nins)), dim3(BLK), 0, s, nins, n, lidx.p + n);
     }
     SPH_HIP_TRY(hipStreamSynchronize(s));  // (the host staging vectors go out of scope)
+    mark("end");
+    if (dbg) {
+      fprintf(stderr, "[sph] phase change: %d candidates, %d inserted;", ncand, nins);
+      for (size_t k = 1; k < tm.size(); k++)
+        fprintf(stderr, " %s %.1f us", tm[k].first,
+                std::chrono::duration<double, std::micro>(tm[k].second - tm[k - 1].second).count());
+      fprintf(stderr, "\n");
+    }
     if (ninsall == 0) return;  // (natoms unchanged: the ghosts stay, the rebuild follows)
     nlocal = n + nins;
     nghost = 0;

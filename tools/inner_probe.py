@@ -18,14 +18,16 @@ x, v, t, rho, e, cv, tags = bench.strong_lattice(100, (1, 1, 1), 0)
 eng = sph.Engine(bench.c2_config(sph, 100))
 eng.set_atoms(x, v, t, rho, e, cv)
 eng.setup()
-eng.set_timing(True, classes=(eng.T_TAIT,))
+eng.set_timing(True, classes=(eng.T_RHO, eng.T_TAIT))
 prev = eng.stats()
 for k in range(25):
     eng.run(1)
     eng.sync()
     st = eng.stats()
     ms = (st["ms_tait"] - prev["ms_tait"]) / max(st["n_tait"] - prev["n_tait"], 1)
-    print(f"step {st['step']:3d} force {ms * 1e3:7.1f} us inner_rows {st['inner_rows']} "
+    mr = (st["ms_rhosum"] - prev["ms_rhosum"]) / max(st["n_rhosum"] - prev["n_rhosum"], 1)
+    print(f"step {st['step']:3d} force {ms * 1e3:7.1f} us rhosum {mr * 1e3:6.1f} us "
+          f"inner_rows {st['inner_rows']} "
           f"live {st['inner_live']} refreshes {st['inner_refresh']} builds {st['nbr_builds']}",
           flush=True)
     prev = st

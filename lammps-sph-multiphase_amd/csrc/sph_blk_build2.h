@@ -1,4 +1,5 @@
-// sph_blk_build2.h -- the block neighbour build with GROUP candidate lists (production).
+// sph_blk_build2.h -- the block neighbour build with GROUP candidate lists (STUDY builds only:
+// measured slower than k_blk_build, 1.37 vs 1.11 ms at C2 1M, profiles/r05/README.md; make STUDY=1).
 //
 // k_blk_build (sph_blk_kernels.h) tests every row of a 64-row block against every candidate
 // of the block's sphere-swept box: ~1000 candidates per row for ~155 hits at C2 (12 %).  A

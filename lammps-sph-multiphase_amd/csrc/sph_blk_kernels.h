@@ -98,6 +98,9 @@ __device__ __forceinline__ unsigned writelane(unsigned v, unsigned val) {
 // LDS cycle).  The rho pass keeps a compact image of its own (x, y at 16 s; z at 16 S + 8 s
 // for S slots) and decodes s from q.
 constexpr int BLK_CH = 1024, BLK_CHE = 1280;
+// the force pass's VISC for one type with Monaghan viscosity and viscC = 0 (no viscosity
+// term; the engine selects it, sph_engine.hip force_pass)
+constexpr int BLK_VISC_NONE = 2;
 // Newton-3 inside the blocks (k_blk_build N3 + the passes' LDS share accumulators): measured
 // slower on gfx950 (force 0.291 -> 0.313 ms, build 1.60 -> 2.18 ms at C2 1M),
 // so only study builds carry it (SPH_N3=1)
@@ -1439,8 +1442,8 @@ __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   constexpr int CQ = (HEAT ? BLK_CHE : BLK_CH) / 16;  // (= cq)
   // one type, Monaghan viscosity, no heat term: the records carry rho_j / viscC (the row
   // rho_i / viscC), so fvisc = min(dvdr, 0) / ((rsq + eps)(rho_i + rho_j) / viscC) needs no
-  // multiply by viscC per pair (viscC = 0: a huge scale, fvisc ~1e-300 -- below every ulp of
-  // the pressure term it is added to, i.e. exactly no viscosity)
+  // multiply by viscC per pair.  viscC = 0 never gets here: the host launches VISC =
+  // BLK_VISC_NONE then (no viscosity term, as viscC * ... = 0 in the reference)
   constexpr bool FOLDV = TAIT && !HEAT && NT1 && VISC == SPH_VISC_MONAGHAN;
   constexpr int NA = HEAT ? 6 : 5;  // a row's shares: F (3), D, E [, EH]
   extern __shared__ __attribute__((aligned(16))) unsigned char blk_smem[];
@@ -1477,7 +1480,7 @@ __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   BlkSlots<G, U, NCH> sw;
   sw.load(snbr + (size_t)rr * sstride, c, lane);
   const double4 xi = xf[rr];
-  const double vsc = FOLDV ? (cf->tait[3].viscC != 0.0 ? 1.0 / cf->tait[3].viscC : 1e300) : 1.0;
+  const double vsc = FOLDV ? 1.0 / cf->tait[3].viscC : 1.0;
   double4 vi = vr[rr];
   if (FOLDV) vi.w *= vsc;
   const double ei = HEAT ? en[rr] : 0.0;
@@ -1580,6 +1583,12 @@ __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
         const double fv = FOLDV ? fmin(dvdr, 0.0) * rcp1((rsq + cc.eps) * (vi.w + a3.y))
                                 : (cc.viscC * fmin(dvdr, 0.0)) * rcp1((rsq + cc.eps) * (vi.w + a3.y));
         const double sp = NT1 ? (xi.w + a1.y + fv) * w : cc.mm * ((xi.w + a1.y + fv) * w);
+        tfx = dx * sp;
+        tfy = dy * sp;
+        tfz = dz * sp;
+        tE = sp * dvdr;
+      } else if (VISC == BLK_VISC_NONE) {  // (one type, Monaghan with viscC = 0)
+        const double sp = (xi.w + a1.y) * w;
         tfx = dx * sp;
         tfy = dy * sp;
         tfz = dz * sp;
@@ -2048,6 +2057,8 @@ inline void blk_force_n(int visc, int mode, hipStream_t s, const BlkArgs &k, con
   switch (mode) {
     case M_TAIT:
       if (mor) blk_force_t<R, G, U, NCH, 1, M_TAIT, NT1>(s, k, a);
+      else if (NT1 && visc == BLK_VISC_NONE)
+        blk_force_t<R, G, U, NCH, BLK_VISC_NONE, M_TAIT, NT1>(s, k, a);
 #ifdef SPH_STUDY  // (outputs meaningless: study builds only, make STUDY=1)
       else if (NT1 && k.exp == 1) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 1>(s, k, a);
       else if (NT1 && k.exp == 2) blk_force_t<R, G, U, NCH, 0, M_TAIT, NT1, 2>(s, k, a);

@@ -21,7 +21,9 @@
 #include "sph_comm.h"
 #include "sph_dispatch.h"
 #include "sph_blk_kernels.h"
+#ifdef SPH_STUDY  // (k_blk_build2: measured slower, study builds only)
 #include "sph_blk_build2.h"
+#endif
 #include "sph_engine_kernels.h"
 #include "sph_engine_mp.h"
 #include "sph_ipc.h"
@@ -438,6 +440,13 @@ struct sph_engine {
                        first, buf.p, vel.p, rm.p, cvv.p, cg.p);
   }
   bool nt1() const { return cfg.ntypes == 1; }
+  // the block force pass's viscosity variant: one type with Monaghan viscosity and viscC = 0
+  // (nu = 0 or c0 = 0) has no viscosity term at all (BLK_VISC_NONE)
+  int blk_visc() const {
+    if (nt1() && cfg.tait_visc == SPH_VISC_MONAGHAN && hc.tait[3].viscC == 0.0)
+      return BLK_VISC_NONE;
+    return cfg.tait_visc;
+  }
 
   // ------------------------------------------------------------------------------------
   void sort_owned() {
@@ -1615,12 +1624,15 @@ struct sph_engine {
 #endif
       // the group-list build (sph_blk_build2.h) unless a study variant needs k_blk_build
       const bool v3 = v2 && try2 && !blk_n3 && !rowsort();
+#ifdef SPH_STUDY
       if (v3)
         blk_build2(shape, nt1(), want_inner, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p, qbeg.p,
                    dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p, ccnt.p, snbr.p, icnt.p, snbi.p,
                    mx.p, mx.p + 1, blk_cq(), iu ? uilist.p : nullptr, iu ? uicnt.p : nullptr,
                    kcnt.p);
-      else if (v2)
+      else
+#endif
+      if (v2)
         blk_build(shape, nt1(), want_inner, blk_n3, s, n, qb, cfg.dim, xf.p, ty.p, xb.p, tb.p,
                   qbeg.p, dc, BLK_UCAP, blk_sstride, ulist.p, ucnt.p,
                   blk_n3 ? pcnt.p : ccnt.p, snbr.p, icnt.p, snbi.p, mx.p, mx.p + 1, blk_cq(),
@@ -1658,6 +1670,12 @@ struct sph_engine {
         continue;
       }
       if (hm[0] != 0) return 2;
+      // the rho and inner passes stage the whole largest union (24 B per slot, blk_rho_lds,
+      // + their static tables): a union past the CU's 160 KiB takes the next shape or the row
+      // path (only the force pass walks windows)
+      if (blk_rho_lds(std::max(hm[1], 1), nt1()) + (nt1() ? 0 : sizeof(RhoPair) * NT2) +
+              sizeof(double) * sh.R + 1024 > 163840)
+        return 2;
       // the next build takes the small candidate image (four workgroups per CU) while this
       // one's largest block fits it (hm[2]: the largest candidate set; the blocks' sets move
       // by a few candidates between rebuilds); after two overflows it stays with the large one
@@ -2013,7 +2031,7 @@ struct sph_engine {
       setup_forces_full();
     } else if (force_mode && blk) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
-      blk_force(nt1(), cfg.tait_visc, force_mode, s, blk_args(), row_args());
+      blk_force(nt1(), blk_visc(), force_mode, s, blk_args(), row_args());
     } else if (force_mode && use_row2()) {
       Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);
       Row2Args b = row2_args();
@@ -2262,7 +2280,7 @@ struct sph_engine {
       if (dbg) tm.emplace_back(w, std::chrono::steady_clock::now());
     };
     mark("start");
-    if (!lidx_valid) lidx_from_tags();  // (armed after setup: the local order from here on)
+    if (!lidx_valid) lidx_from_tags();  // (read_restart: the file's tag order)
     const bool mul = multi();
     const int n = nlocal, nall = nlocal + nghost;
     if (n == 0 && !mul) return;
@@ -2764,7 +2782,6 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
   e->tag_next = n;
   e->pc_tags_agreed = false;
   e->pc_inserted = 0;
-  e->lidx_valid = false;
   e->cv_by_tag.assign(n, 1.0);
   if (cv)
     for (int i = 0; i < n; i++) e->cv_by_tag[i] = cv[i];
@@ -2794,6 +2811,11 @@ int sph_engine_set_atoms(sph_engine *e, int n, const double *x, const double *v,
     SPH_HIP_TRY(hipMemsetAsync(e->fo.p, 0, n * sizeof(double4), e->s));
     SPH_HIP_TRY(hipMemsetAsync(e->de.p, 0, n * sizeof(double), e->s));
   }
+  // LAMMPS' local order starts as the read order (data-file lines / create_atoms), which is
+  // the order handed here -- not necessarily tag order (sph_engine_set_tags may permute)
+  e->lidx.reserve(n > 0 ? n : 1);
+  if (n > 0) hipLaunchKernelGGL(k_lidx_iota, dim3(blocks(n)), dim3(BLK), 0, e->s, n, 0, e->lidx.p);
+  e->lidx_valid = true;
   if (e->mp && n > 0) {  // per-type mass, cv (default 1, create_atom), colorgradient 0
     std::vector<double> hm(n), hc(n);
     for (int i = 0; i < n; i++) {
@@ -2841,6 +2863,9 @@ int sph_engine_phase_change(sph_engine *e, const sph_phasechange_params *p, int 
   SPH_REQUIRE(e->mp, SPH_HIP_EINVAL,
               "fix phase_change needs atom_style meso/multiphase (a multiphase engine)");
   SPH_REQUIRE(seed > 0, SPH_HIP_EINVAL, "Invalid seed for Park random # generator");
+  SPH_REQUIRE(!e->setup_done, SPH_HIP_EINVAL,
+              "sph_engine_phase_change: arm the fix before sph_engine_setup (its local-order "
+              "bookkeeping starts at set_atoms)");
   SPH_REQUIRE(nevery >= 1, SPH_HIP_EINVAL, "sph_engine_phase_change: nevery < 1");
   SPH_REQUIRE(p->to_mass > 0.0 && p->maxattempt >= 1 && p->cutoff > 0.0, SPH_HIP_EINVAL,
               "sph_engine_phase_change: bad parameters");

@@ -884,9 +884,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       for (int k = lane; k < pos - pos0; k += G) {
         const double rsq = s_hr[grp][k];
         const int pt = s_hp[grp][k];
-        double r, ir;
-        mp2_r_ir(rsq, r, ir);
-        const double w = q5_w(3.0 * (r * s_rih[pt])) * s_rwn[pt];
+        const double w = qr_wpoly(3.0 * (sqrt(rsq) * s_rih[pt])) * s_rwn[pt];
         racc += rsq < s_rcs[pt] ? w : 0.0;
       }
       __builtin_amdgcn_wave_barrier();
@@ -903,7 +901,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
     racc = group_sum<G>(racc);
     if (lane == 0) {
       const int pt = rrow + (NT1 ? 1 : ty[i]);
-      rho[i] = (q5_w(0.0) * s_rwn[pt] + racc) * rm[i];
+      rho[i] = (qr_wpoly(0.0) * s_rwn[pt] + racc) * rm[i];
     }
   }
 }

@@ -27,9 +27,12 @@
 // by the node's processes) every 50 ms while its world exists, so a waiting rank tells a peer
 // that is busy (a long setup or first rebuild: it still beats) from one that is gone (its
 // beat stops when the process exits or is killed): a barrier fails with SPH_HIP_ECOMM once a
-// peer has not beaten for SPH_IPC_DEAD seconds (default 10), and otherwise waits as long as
-// the work takes (SPH_IPC_TIMEOUT > 0 bounds the wait anyway; default none).  Rank 0
-// removes host outboxes a killed run of the same world name left in /dev/shm.
+// peer has not beaten for SPH_IPC_DEAD seconds (default 10), or has never beaten within the
+// attach time (it died before it joined), and otherwise waits as long as the work takes, up to
+// SPH_IPC_TIMEOUT seconds (default 1800: a peer whose main thread hangs -- a stuck kernel, a
+// mismatched collective -- still beats from its heartbeat thread, so the wait stays bounded;
+// <= 0 waits without bound).  Rank 0 removes host outboxes a killed run of the same world
+// name left in /dev/shm.
 #pragma once
 #include <dirent.h>
 #include <fcntl.h>
@@ -98,7 +101,8 @@ class IpcTransport : public Transport {
     SPH_REQUIRE(name && name[0] == '/' && strlen(name) < 200 && !strchr(name + 1, '/'),
                 SPH_HIP_EINVAL, "ipc world name must be '/word' (got '%s')", name ? name : "");
     const char *t = getenv("SPH_IPC_TIMEOUT");
-    timeout_s_ = t ? atof(t) : 0.0;
+    timeout_s_ = t ? atof(t) : 1800.0;
+    born_ = std::chrono::steady_clock::now();
     const char *dd = getenv("SPH_IPC_DEAD");
     dead_s_ = dd ? atof(dd) : 10.0;
     const size_t sz = sizeof(IpcShm);
@@ -160,7 +164,18 @@ class IpcTransport : public Transport {
     });
     w_->attached.fetch_add(1);
     peer_.assign(n_, Peer());
-    host_barrier();  // everyone attached: the name can go (no leftover in /dev/shm)
+    try {
+      host_barrier();  // everyone attached: the name can go (no leftover in /dev/shm)
+    } catch (...) {
+      // (the destructor does not run for a constructor that throws: stop the heartbeat
+      // thread and unmap here, or the joinable thread's destructor would terminate)
+      stop_.store(true, std::memory_order_release);
+      beater_.join();
+      if (rank == 0) shm_unlink(name);
+      munmap(w_, sizeof(IpcShm));
+      w_ = nullptr;
+      throw;
+    }
     if (rank == 0) shm_unlink(name);
   }
 
@@ -248,12 +263,15 @@ class IpcTransport : public Transport {
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return (int64_t)ts.tv_sec * 1000000000LL + ts.tv_nsec;
   }
-  // a peer that has beaten once and not for dead_s_ seconds is gone (its process exited)
+  // a peer that has beaten once and not for dead_s_ seconds is gone (its process exited); one
+  // that has never beaten attach_s_ after this rank joined died before it attached
   void check_peers() const {
     const int64_t now = now_ns();
     for (int r = 0; r < n_; r++) {
       if (r == me_) continue;
       const int64_t b = w_->r[r].beat.load(std::memory_order_acquire);
+      SPH_REQUIRE(b != 0 || elapsed(born_) < attach_s_, SPH_HIP_ECOMM,
+                  "ipc world %s: rank %d never joined (%.0f s)", name_.c_str(), r, attach_s_);
       SPH_REQUIRE(b == 0 || (double)(now - b) * 1e-9 < dead_s_, SPH_HIP_ECOMM,
                   "ipc world %s: rank %d has not beaten for %.1f s (its process exited?)",
                   name_.c_str(), r, (double)(now - b) * 1e-9);
@@ -438,6 +456,7 @@ class IpcTransport : public Transport {
   double timeout_s_ = 0.0;   // SPH_IPC_TIMEOUT: bound on a barrier wait (0: none)
   double dead_s_ = 10.0;     // SPH_IPC_DEAD: a peer silent this long is gone
   double attach_s_ = 120.0;  // creating / joining the world
+  std::chrono::steady_clock::time_point born_;
   std::atomic<bool> stop_{false};
   std::thread beater_;
   IpcShm *w_ = nullptr;

@@ -3,11 +3,11 @@
 // in the fused gather (profiles/r03: 543 M wave-instructions for 1M rows) on branchy quintic
 // pieces, per-pair coefficient loads with lane-varying indices and the swaps that put each
 // pair in its half-list orientation.  Here
-//   * the quintic kernel and its derivative are branch-free, in the factored form
-//     W(s) ~ a^5 - 6 b^5 + 15 c^5, dW/ds ~ -5 a^4 + 30 b^4 - 75 c^4 with a = max(3-s, 0),
-//     b = max(2-s, 0), c = max(1-s, 0) -- algebraically the reference's piecewise
-//     polynomials (sph_kernel_quintic.cpp:17-73), without their cancellation near s = 3;
-//     zero beyond the cutoff, so the cut test rides on the weight;
+//   * the quintic kernel and its derivative are the reference's own expanded polynomials
+//     (sph_kernel_quintic.cpp:17-73) in its arithmetic -- rsq without contraction, IEEE
+//     sqrt, s = 3 (r / h), correctly rounded powers, no contraction (sph_mp_kernels.h qr_*) --
+//     branch-free (the pieces as selected coefficients); round 5's factored form sat up to
+//     ~1e-13 absolute from the reference's dW where its polynomial cancels near the cutoff;
 //   * the per-pair-type coefficients sit in LDS, loaded once per workgroup;
 //   * when every style is symmetric under exchanging the pair's atoms (all gamma equal, so
 //     the p_j-with-gamma[itype] quirk is moot, and no type pinned to its own type's Tc) a
@@ -48,26 +48,24 @@ namespace sph {
 #define SPH_MP2_OCC
 #endif
 
-// quintic W(s) and dW/ds without the norm (s = 3 r / h)
-__device__ __forceinline__ double q5_w(double s) {
-  const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
-  const double a2 = a * a, b2 = b * b, c2 = c * c;
-  return fma(15.0 * c2 * c2, c, fma(-6.0 * b2 * b2, b, a2 * a2 * a));
-}
-__device__ __forceinline__ double q5_dw(double s) {
-  const double a = fmax(3.0 - s, 0.0), b = fmax(2.0 - s, 0.0), c = fmax(1.0 - s, 0.0);
-  const double a2 = a * a, b2 = b * b, c2 = c * c;
-  return fma(-75.0 * c2, c2, fma(30.0 * b2, b2, -5.0 * (a2 * a2)));
-}
-
-// r and 1/r from one v_rsq_f64 seed, one Newton step each (x + 1e-300: a coincident pair
-// gives a huge 1/r times a zero weight instead of NaN)
+// r = sqrt(rsq) as the reference takes it, correctly rounded (s = 3 (r / h) then feeds the
+// reference-form quintic, sph_mp_kernels.h qr_*, bit for bit), and 1/r: LLVM's f64 sqrt
+// sequence (a v_rsq_f64 seed, one Goldschmidt step, two residual corrections) without its
+// rescaling of tiny arguments (rsq > 1e-300 here: x + 1e-300 makes a coincident pair give a
+// huge 1/r times a zero weight instead of NaN); 1/r = 2 h from the same refinement (~1e-15
+// relative: it only scales well-conditioned products)
 __device__ __forceinline__ void mp2_r_ir(double x, double &r, double &ir) {
   x += 1e-300;
   const double y = __builtin_amdgcn_rsq(x);
-  const double r0 = x * y;
-  r = fma(fma(-r0, r0, x), 0.5 * y, r0);
-  ir = y * fma(-0.5 * x * y, y, 1.5);
+  double g = x * y, h = 0.5 * y;
+  const double e = fma(-h, g, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  r = fma(d, h, g);
+  ir = 2.0 * h;
 }
 
 // per pair type: the stack's cutoffs (squared), 1/h and the coefficients the pair terms use
@@ -79,8 +77,8 @@ struct Mp2Pair {
   double hcsq, hih, halpha2;  // heatconduction/phasechange (2 alpha)
   double htc;
   int hfix, pad;
-  // the gather's per-pair-type constants: s = 3 r / h as r * k3, dW/dr norm (mp2_dwnorm)
-  double tk3, tdn, sk3, sdn, hk3, hdn;
+  // the gather's per-pair-type constants: the dW/dr norms (mp2_dwnorm)
+  double tdn, sdn, hdn;
 };
 struct Mp2Type {
   double B, rho0i, gamma, rbg;
@@ -109,11 +107,8 @@ __device__ __forceinline__ void mp2_tables(const MpCoefs *c, Mp2Pair *sp, Mp2Typ
     q.htc = c->htc[p];
     q.hfix = c->hfix[p];
     q.pad = 0;
-    q.tk3 = 3.0 * q.tih;
     q.tdn = mp2_dwnorm(dim, q.tih);
-    q.sk3 = 3.0 * q.sih;
     q.sdn = mp2_dwnorm(dim, q.sih);
-    q.hk3 = 3.0 * q.hih;
     q.hdn = mp2_dwnorm(dim, q.hih);
     sp[p] = q;
   }
@@ -164,16 +159,14 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
       if (k0 + u * G >= rw.end) break;
       const Mp2Pair &q = pi[tj[u]];
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
-      const double rsq = dx * dx + dy * dy + dz * dz;
-      double r, ir;
-      mp2_r_ir(rsq, r, ir);
-      if (rsq < q.rcsq) acc += q5_w(3.0 * (r * q.rih)) * mp2_wnorm(dim, q.rih);
+      const double rsq = rsq_ref(dx, dy, dz);
+      if (rsq < q.rcsq) acc += qr_wpoly(3.0 * (sqrt(rsq) * q.rih)) * mp2_wnorm(dim, q.rih);
     }
   }
   acc = group_sum<G>(acc);
   if (lane == 0) {
     const Mp2Pair &q = pi[it];
-    a.rho[i] = (q5_w(0.0) * mp2_wnorm(dim, q.rih) + acc) * a.rm[i];
+    a.rho[i] = (qr_wpoly(0.0) * mp2_wnorm(dim, q.rih) + acc) * a.rm[i];
   }
 }
 
@@ -221,11 +214,11 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
       const Mp2Pair &q = pi[tj[u]];
       if (q.calpha == 0.0) continue;
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
-      const double rsq = dx * dx + dy * dy + dz * dz;
+      const double rsq = rsq_ref(dx, dy, dz);
       if (!(rsq < q.ccsq)) continue;
       double r, ir;
       mp2_r_ir(rsq, r, ir);
-      const double wfd = q5_dw(3.0 * (r * q.cih)) * mp2_dwnorm(dim, q.cih);
+      const double wfd = qr_dwpoly(3.0 * (r * q.cih)) * mp2_dwnorm(dim, q.cih);
       const double sj = xj[u].w;
       const double dphi = -wfd * q.calpha * mp_rcp(sj * sj) * sigmai * ir;
       gx += dphi * dx;
@@ -312,14 +305,14 @@ __global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
     const Mp2Pair &q = pi[tj];
     const double rhoi = ci.w, rhoj = cj.w, mj = xj.w;
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     const bool ct = TAIT && rsq < q.tcsq, cs = SURF && rsq < q.scsq, ch = HEAT && rsq < q.hcsq;
     if (!(ct || cs || ch)) return;
     double r, ir;
     mp2_r_ir(rsq, r, ir);
-    const double qt = ct ? q5_dw(r * q.tk3) * q.tdn : 0.0;
-    const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt : q5_dw(r * q.sk3) * q.sdn;
-    const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt : q5_dw(r * q.hk3) * q.hdn;
+    const double qt = ct ? qr_dwpoly(3.0 * (r * q.tih)) * q.tdn : 0.0;
+    const double qs = !cs ? 0.0 : (ct && q.sih == q.tih) ? qt : qr_dwpoly(3.0 * (r * q.sih)) * q.sdn;
+    const double qh = !ch ? 0.0 : (ct && q.hih == q.tih) ? qt : qr_dwpoly(3.0 * (r * q.hih)) * q.hdn;
     const double iri = fi ? irFi : irSi, irj = mp_rcp(rhoj);
     const double Vi = mi * iri, Vj = mj * irj;
     const double Vi2 = Vi * Vi, Vj2 = Vj * Vj;

@@ -73,36 +73,75 @@ __device__ __forceinline__ double mp_rcp(double b) {
   return fma(y, fma(-b, y, 1.0), y);
 }
 
-// Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r).  The reference's pow(x, n) with
-// small integer n are evaluated as products (a few ulp apart from libm pow; the golden
-// vectors hold at 1e-13), and the branches as selects of one polynomial per piece.
-__device__ __forceinline__ double p5(double x) {
-  const double x2 = x * x;
-  return x2 * x2 * x;
+// Quintic spline, sph_kernel_quintic.cpp:17-73 (s = 3r), in the reference's own arithmetic:
+// its expanded piecewise polynomials through pow(x, n), evaluated left to right with every
+// product and sum rounded (its x86-64 build has no FMA, so nothing is contracted).  Near the
+// cutoff those polynomials cancel (dW ~ -5 s^4 + 60 s^3 - ... - 405 with terms ~1e3 for a
+// result ~1e-6), so their rounding errors ARE the reference's dW there; a factored form
+// (exact to ~1 ulp) sits up to ~1e-13 absolute away from it, which a small colour-gradient or
+// force element shows at ~1e-9 relative (the round-5 C5 tests).  pow(x, n) for n = 2..5 is
+// evaluated correctly rounded (double-double products, one final rounding): glibc's pow
+// agrees with the correctly rounded power except in ~0.08 % of calls (1 ulp, tools/
+// quintic_pow_check.c), so dW matches the reference bit for bit except there.
+__device__ __forceinline__ double qr_pow3(double x) {  // x^3, correctly rounded
+  const double h = x * x, l = fma(x, x, -h);
+  const double p = x * h, e = fma(x, h, -p);
+  return p + fma(x, l, e);
+}
+__device__ __forceinline__ void qr_pow4dd(double x, double &q, double &t) {  // x^4 = q + t
+  const double h = x * x, l = fma(x, x, -h);
+  q = h * h;
+  t = fma(2.0 * h, l, fma(h, h, -q));
+}
+__device__ __forceinline__ double qr_pow4(double x) {
+  double q, t;
+  qr_pow4dd(x, q, t);
+  return q + t;
+}
+__device__ __forceinline__ double qr_pow5(double x) {
+  double q, t;
+  qr_pow4dd(x, q, t);
+  const double p = x * q, e = fma(x, q, -p);
+  return p + fma(x, t, e);
+}
+// the reference's W(s) / norm: pow(3-s,5) - 6 pow(2-s,5) + 15 pow(1-s,5) on [0,1), the first two
+// on [1,2), the first on [2,3), 0 beyond -- the pieces as zero terms (x - 0 and x + 0 are x)
+__device__ __forceinline__ double qr_wpoly(double s) {
+#pragma clang fp contract(off)
+  const double a = s < 3.0 ? qr_pow5(3.0 - s) : 0.0;
+  const double b = s < 2.0 ? qr_pow5(2.0 - s) : 0.0;
+  const double c = s < 1.0 ? qr_pow5(1.0 - s) : 0.0;
+  return (a - 6.0 * b) + 15.0 * c;
+}
+// the reference's dW/ds / norm: c4 pow(s,4) + c3 pow(s,3) + c2 pow(s,2) + c1 s + c0 with the
+// piece's integer coefficients (a missing term is + 0 * s^2 or + 0: exact), left to right.
+// Pairs sit at s >= ~1 (h = 3 dx, s = r / dx): the [1,2) / [2,3) coefficients are one select
+// each, the rare [0,1) piece a wave-uniform branch
+__device__ __forceinline__ double qr_dwpoly(double s) {
+#pragma clang fp contract(off)
+  const bool p2 = s < 2.0;
+  double c4 = p2 ? 25.0 : -5.0, c3 = p2 ? -180.0 : 60.0, c2 = p2 ? 450.0 : -270.0;
+  double c1 = p2 ? -420.0 : 540.0, c0 = p2 ? 75.0 : -405.0;
+  if (__any(s < 1.0)) {
+    const bool p1 = s < 1.0;
+    c4 = p1 ? -50.0 : c4;
+    c3 = p1 ? 120.0 : c3;
+    c2 = p1 ? 0.0 : c2;
+    c1 = p1 ? -120.0 : c1;
+    c0 = p1 ? 0.0 : c0;
+  }
+  const double w = (((c4 * qr_pow4(s) + c3 * qr_pow3(s)) + c2 * (s * s)) + c1 * s) + c0;
+  return s < 3.0 ? w : 0.0;
 }
 __device__ __forceinline__ double quintic_w(int dim, double r) {
+#pragma clang fp contract(off)
   const double norm = (dim == 3) ? 0.0716197243913529 : 0.04195297663091802;
-  const double s = 3.0 * r;
-  const double a = s < 3.0 ? p5(3 - s) : 0.0;
-  const double b = s < 2.0 ? 6 * p5(2 - s) : 0.0;
-  const double c = s < 1.0 ? 15 * p5(1 - s) : 0.0;
-  return norm * (a - b + c);
+  return norm * qr_wpoly(3.0 * r);
 }
 __device__ __forceinline__ double quintic_dw(int dim, double r) {
-  const double norm = 3.0 * ((dim == 3) ? 0.0716197243913529 : 0.04195297663091802);
-  const double s = 3.0 * r;
-  const double s2 = s * s, s3 = s2 * s, s4 = s2 * s2;
-  double wfd;
-  if (s < 1) {
-    wfd = -50 * s4 + 120 * s3 - 120 * s;
-  } else if (s < 2) {
-    wfd = 25 * s4 - 180 * s3 + 450 * s2 - 420 * s + 75;
-  } else if (s < 3.0) {
-    wfd = -5 * s4 + 60 * s3 - 270 * s2 + 540 * s - 405;
-  } else {
-    wfd = 0.0;
-  }
-  return norm * wfd;
+#pragma clang fp contract(off)
+  const double norm = (dim == 3) ? 3.0 * 0.0716197243913529 : 3.0 * 0.04195297663091802;
+  return norm * qr_dwpoly(3.0 * r);
 }
 
 __device__ __forceinline__ double mp_qdw(int dim, double r, double ih) {
@@ -175,7 +214,7 @@ __global__ void __launch_bounds__(256) k_mp_rhosum(MpArgs a) {
     const double4 xj = a.xf[j];
     const int jt = a.ty[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     if (rsq < c->rcutsq[it * nt1 + jt]) {
       const double ih = c->rcut_inv[it * nt1 + jt];
       const double r = sqrt(rsq) * ih;
@@ -211,7 +250,7 @@ __device__ __forceinline__ bool mp_tait_pair(const MpCoefs *c, int dim, double4 
                                              double mj, double3 &F) {
   const int p = it * (c->ntypes + 1) + jt;
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-  const double rsq = dx * dx + dy * dy + dz * dz;
+  const double rsq = rsq_ref(dx, dy, dz);
   if (!(rsq < c->tcutsq[p])) return false;
   const double ih = c->tcut_inv[p];
   const double r = sqrt(rsq);
@@ -239,7 +278,7 @@ __device__ __forceinline__ bool mp_heat_pair(const MpCoefs *c, int dim, double4 
                                              double rhoj, double Tj0, double &deltaE) {
   const int p = it * (c->ntypes + 1) + jt;
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-  const double rsq = dx * dx + dy * dy + dz * dz;
+  const double rsq = rsq_ref(dx, dy, dz);
   if (!(rsq < c->hcutsq[p])) return false;
   const double ih = c->hcut_inv[p];
   const double r = sqrt(rsq);
@@ -278,7 +317,7 @@ __global__ void __launch_bounds__(256) k_mp_colorgradient(MpArgs a) {
     const int jt = a.ty[j];
     const int p = it * nt1 + jt;
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     if (!(rsq < c->ccutsq[p])) continue;
     const double r = sqrt(rsq);
     const double ih = c->ccut_inv[p];
@@ -330,7 +369,7 @@ __device__ __forceinline__ bool mp_surf_pair(const MpCoefs *c, int dim, double4 
                                              int jt, double Vj, double4 cgj, double3 &F) {
   const int p = it * (c->ntypes + 1) + jt;
   const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-  const double rsq = dx * dx + dy * dy + dz * dz;
+  const double rsq = rsq_ref(dx, dy, dz);
   if (!(rsq < c->scutsq[p])) return false;
   const double ih = c->scut_inv[p];
   const double r = sqrt(rsq);
@@ -533,7 +572,7 @@ __global__ void __launch_bounds__(256) k_mp_gather(MpArgs a) {
     // geometry: r, 1/r, and the quintic dW once per distinct cutoff (bubble.lmp: one h)
     const int pc = tp * (c->ntypes + 1) + tq;
     const double dx = xp.x - xq.x, dy = xp.y - xq.y, dz = xp.z - xq.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     const bool ct = TAIT && rsq < c->tcutsq[pc], cs = SURF && rsq < c->scutsq[pc],
                ch = HEAT && rsq < c->hcutsq[pc];
     if (!(ct || cs || ch)) continue;

@@ -111,7 +111,7 @@ k_pc_candidates(int ncand, const int *__restrict__ cand, const int *__restrict__
     mr = min(mr, r);
     const double4 xj = xf[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     // (a decision: the reference's rounding)
     if (r >= dead_a && rsq_ref(dx, dy, dz) <= cut2) around = 1;
     if (r >= dead_w && rm[j] > 0.5 * p.to_mass) {
@@ -184,7 +184,7 @@ k_pc_dmass_emit(int nins, const int *__restrict__ rows, const double *__restrict
     if (r < nins) continue;  // overwritten before this donor loop (r <= k) or later (r < nins)
     const double4 xj = xf[j];
     const double dx = xi.x - xj.x, dy = xi.y - xj.y, dz = xi.z - xj.z;
-    const double rsq = dx * dx + dy * dy + dz * dz;
+    const double rsq = rsq_ref(dx, dy, dz);
     const int slot = atomicAdd(cnt, 1);
     if (slot >= cap) continue;  // (the host checks the count against cap after the launch)
     key[slot] = ((unsigned long long)(unsigned)j << 32) | (unsigned)k;

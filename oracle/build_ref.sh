@@ -12,6 +12,13 @@ set -euo pipefail
 REF=${REF:-/root/reference/src}
 HERE=$(cd "$(dirname "$0")" && pwd)
 OUT=$HERE/_ref
+# VARIANT=fma: the same sources built for an FMA machine (-mfma, GCC contracting a*b+c as it
+# does by default there) into oracle/_ref_fma/libsph_ref.so -- how far the reference's own
+# results move between two legitimate builds (tools/fma_build_shift.py); not the oracle
+# VARIANT=fastmath: the reference's own fast-math recipe (src/MAKE/Makefile.mingw64-cross:10-11)
+# into oracle/_ref_fastmath/libsph_ref.so
+if [ "${VARIANT:-}" = "fma" ]; then OUT=$HERE/_ref_fma; fi
+if [ "${VARIANT:-}" = "fastmath" ]; then OUT=$HERE/_ref_fastmath; fi
 OBJ=$OUT/obj
 mkdir -p "$OBJ"
 if [ ! -d "$REF" ]; then
@@ -34,6 +41,10 @@ SPH="atom_vec_meso.cpp atom_vec_meso_multiphase.cpp pair_sph_rhosum.cpp
 # the reference's own serial build: g++ -O3 at the compiler's default C++ dialect (src/MAKE/
 # Makefile.serial:9-10); the dialect matters -- under C++98 pow(double,int) is __builtin_powi
 CXXFLAGS="-O3 -fPIC -w -DLAMMPS_SMALLBIG -I$REF -I$REF/USER-SPH -I$REF/STUBS"
+if [ "${VARIANT:-}" = "fma" ]; then CXXFLAGS="$CXXFLAGS -mfma -ffp-contract=fast"; fi
+if [ "${VARIANT:-}" = "fastmath" ]; then
+  CXXFLAGS="$CXXFLAGS -march=core2 -mtune=core2 -msse2 -ffast-math -fstrict-aliasing"
+fi
 objs=()
 compile() {  # src obj
   if [ ! -f "$2" ] || [ "$1" -nt "$2" ]; then g++ $CXXFLAGS -c "$1" -o "$2"; fi
@@ -70,7 +81,7 @@ echo "built $OUT/libsph_ref.so"
 # shim_*): the classes run their compute()/pre_exchange() through libsph_hip.so on the
 # harness-filled universe.  Needs the product library built first (make -C the package).
 PKG=$HERE/../lammps-sph-multiphase_amd
-if [ -f "$PKG/libsph_hip.so" ]; then
+if [ -f "$PKG/libsph_hip.so" ] && [ -z "${VARIANT:-}" ]; then
   SHIMF="-I$PKG/lammps -I$HERE/../include"
   sobjs=()
   for f in pair_sph_hip fix_phase_change_hip; do

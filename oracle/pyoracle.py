@@ -128,10 +128,38 @@ _lib = None
 _ref = None
 
 
+# the same restatement in other legitimate builds (oracle/Makefile): "fma" = -mfma
+# -ffp-contract=fast (any FMA machine), "fastmath" = the reference's own Makefile.mingw64-cross
+# flags (-O3 -march=core2 -ffast-math); used only by the build-variation shadows of _Spread
+BUILD_SO = {"fma": os.path.join(HERE, "liboracle_sph_fma.so"),
+            "fastmath": os.path.join(HERE, "liboracle_sph_fastmath.so")}
+_lib_build = {}
+_use_build = [None]  # (set while a build-variation shadow steps, _Spread._qf)
+
+
 def lib():
+    """the C restatement (liboracle_sph.so), or -- only while a build-variation shadow of
+    _Spread steps -- the same source in another build (BUILD_SO)"""
+    b = _use_build[0]
+    if b is not None:
+        if b not in _lib_build:
+            if not os.path.exists(BUILD_SO[b]):
+                subprocess.run(["make", "-s", "-C", HERE, os.path.basename(BUILD_SO[b])],
+                               check=True)
+            _lib_build[b] = _bind_oracle(C.CDLL(BUILD_SO[b]))
+        return _lib_build[b]
+    return _lib_plain()
+
+
+def _lib_plain():
     global _lib
     if _lib is None:
-        L = C.CDLL(build_oracle())
+        _lib = _bind_oracle(C.CDLL(build_oracle()))
+    return _lib
+
+
+def _bind_oracle(L):
+    if True:
         P = C.POINTER(OrcDomain)
         L.orc_pbc.argtypes = [P, _i, _dp]
         L.orc_borders.argtypes = [P, _d, _i, _dp, _ip, _i, _ip, _ip]
@@ -164,6 +192,8 @@ def lib():
             getattr(L, n).restype = _d
         L.orc_set_quintic_factored.argtypes = [_i]
         L.orc_set_quintic_factored.restype = None
+        L.orc_set_pow_mode.argtypes = [_i]
+        L.orc_set_pow_mode.restype = None
         L.orc_rhosum_multiphase.argtypes = [_i, _i, _dp, _ip, _i, _dp, _dp, _dp, _lp, _ip,
                                             _dp]
         L.orc_taitwater_multiphase.argtypes = [_i, _i, _i, _dp, _dp, _dp, _ip, _i, _dp, _dp,
@@ -195,8 +225,7 @@ def lib():
                                        _dp, _dp]
         L.orc_meso_stationary.argtypes = [_i, _d, _ip, _i, _dp, _dp, _dp, _dp]
         L.orc_gravity.argtypes = [_i, _ip, _i, _dp, C.c_void_p, _dp, _dp]
-        _lib = L
-    return _lib
+    return L
 
 
 def ref_available() -> bool:
@@ -638,15 +667,26 @@ class _Spread:
     every list row reversed, every row rotated (SPREAD_ORDERS), and the inputs moved by one
     ulp (ulp_perturbed); spread(k) is, per element of field k, the largest distance of their
     results from this run's: how far the reference's own result moves under a reordered
-    summation or last-bit changes of its terms (the tests' elementwise bar).
-    Reordering alone misses elements whose reference sum happens to be order-insensitive
-    while its terms cancel (a C5 colour-gradient tail, a C3 atom between two phases: spread
-    < 1e-18 absolute, where the engine's terms -- v_rsq/v_rcp seeds with a Newton step, the
-    factored quintic -- differ from the reference's in their last bits)."""
+    summation or last-bit changes of its inputs (the tests' elementwise bar).
+    Every shadow runs the reference's own arithmetic (no shadow evaluates anything in the
+    engine's form: round 5's factored-quintic shadow is gone, the engine evaluates the
+    reference's expanded quintic instead).  Reordering alone misses elements whose reference
+    sum happens to be order-insensitive while its terms cancel (a C3 atom between two phases:
+    spread < 1e-18 absolute): the ulp shadow covers those.  For the C5 stack (MpRefRun) two
+    more shadows run the same source in two other legitimate builds: for an FMA machine
+    (liboracle_sph_fma.so: GCC contracting a*b + c, as a -march=native build of LAMMPS does)
+    and with the reference's own fast-math recipe (liboracle_sph_fastmath.so: -O3
+    -march=core2 -ffast-math, src/MAKE/Makefile.mingw64-cross:10-11).  On the bubble lattice
+    the reference's sums cancel pairwise, so neither reordering nor a one-ulp input moves
+    them, while any change in a term's last bits does: the reference's OWN sources built
+    those ways move C5 colour-gradient / multiphase-force elements by up to ~1e-9 / ~1e-7
+    relative (tools/fma_build_shift.py, profiles/r06/fma_build_shift.json), so the C5 bar is
+    16 x how far the reference moves between legitimate builds of itself."""
 
-    def _init_spread(self, spread, make, make_ulp, kernel_form=False):
+    def _init_spread(self, spread, make, make_ulp, build=False):
         self.alts = []
         self.qfact = False
+        self.build = None
         if spread:
             # spread="lean" (the 1M tests): one reordering + the ulp shadow
             for how in (SPREAD_ORDERS[:1] if spread == "lean" else SPREAD_ORDERS):
@@ -654,14 +694,19 @@ class _Spread:
                 a.rev = how
                 self.alts.append(a)
             self.alts.append(make_ulp())
-            if kernel_form:  # (C5: the quintic dW evaluated factored, orc_set_quintic_factored)
-                a = make()
-                a.qfact = True
-                self.alts.append(a)
+            if build:  # (C5: the same source in two other builds, see the class doc)
+                for b in ("fma", "fastmath"):
+                    a = make()
+                    a.build = b
+                    self.alts.append(a)
 
     def _qf(self, on):
-        if self.qfact:
+        if self.build:
+            _use_build[0] = self.build if on else None
+        if self.qfact:  # (tools/cg_probe.py: a run evaluating the quintic dW factored)
             lib().orc_set_quintic_factored(1 if on else 0)
+        if getattr(self, "powm", 0):  # (orc_set_pow_mode: 1 correctly rounded, 2 one ulp up)
+            lib().orc_set_pow_mode(self.powm if on else 0)
 
     def field(self, k):
         s = self.s
@@ -1128,8 +1173,12 @@ class MpRefRun(_Spread):
     tracked beside them (self.local): read order, CommBrick::exchange's hole fill, Atom::sort
     at setup and every ph.sortfreq steps (verlet.cpp:106, 251), created atoms appended."""
 
-    def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None, spread=False):
+    def __init__(self, sysm: System, ph: MpPhysics, cg=None, procgrid=None, spread=False,
+                 read_order=None):
         self.s = sysm.copy()
+        # read_order: the atom ids in the order LAMMPS read them (data-file lines), which is
+        # its initial local order; default tag order
+        self.read_order = None if read_order is None else np.asarray(read_order, np.int64)
         assert self.s.rmass is not None
         # procgrid: fix phase_change as it runs on a grid of ranks (each rank scans its owned
         # atoms in its local order with its own RanPark of the same seed,
@@ -1147,9 +1196,10 @@ class MpRefRun(_Spread):
         # order, so a test can size its tolerance to how far the reference's own result moves
         # under reordering where a sum nearly cancels (ill-conditioned atoms)
         self.rev = False
-        self._init_spread(spread, lambda: MpRefRun(sysm, ph, cg=cg, procgrid=procgrid),
-                          lambda: MpRefRun(ulp_perturbed(sysm), ph, cg=cg, procgrid=procgrid),
-                          kernel_form=True)
+        self._init_spread(spread, lambda: MpRefRun(sysm, ph, cg=cg, procgrid=procgrid,
+                                                   read_order=read_order),
+                          lambda: MpRefRun(ulp_perturbed(sysm), ph, cg=cg, procgrid=procgrid,
+                                           read_order=read_order), build=True)
         self.ph = ph
         nt = sysm.ntypes
         self.cns, self.cutneighmax = cutneighsq(nt, ph.cutmax(nt), ph.skin)
@@ -1222,11 +1272,12 @@ class MpRefRun(_Spread):
         """Between Domain::pbc and CommBrick::borders (verlet.cpp:100-107, 245-253): the
         exchange, then Atom::sort at setup and once step >= nextsort (nextsort =
         (step/sortfreq)*sortfreq + sortfreq, atom.cpp:1561).  The first call lists every
-        rank's atoms in read order (tag order within the rank)."""
+        rank's atoms in read order (read_order, default tag order, within the rank)."""
         s, ph = self.s, self.ph
         if self.local is None:
             own = brick_owner(s, s.x, self.pg)
-            self.local = [np.nonzero(own == r)[0] for r in range(int(np.prod(self.pg)))]
+            ro = self.read_order if self.read_order is not None else np.arange(s.n)
+            self.local = [ro[own[ro] == r] for r in range(int(np.prod(self.pg)))]
         else:
             self.local = exchange_bricks(s, self.pg, self.local)
         if ph.sortfreq > 0 and (self.step == 0 or self.step >= self.nextsort):

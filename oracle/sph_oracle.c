@@ -534,30 +534,55 @@ void orc_heatconduction(int dim, int nlocal, int newton_pair, const double *x,
 /* ------------------------------------------------------------------------------------
    Quintic spline, src/USER-SPH/sph_kernel_quintic.cpp:17-73 (pow() semantics kept)
    ------------------------------------------------------------------------------------ */
+/* qpow: the reference's pow(x, n) (glibc), or for test aids only (orc_set_pow_mode):
+   1 = the correctly rounded power (double-double products, one rounding: what the engine
+   evaluates, sph_mp_kernels.h qr_pow*; glibc's pow differs from it by 1 ulp in ~0.09 % of the
+   calls, tools/quintic_pow_check.c), 2 = glibc's result moved one ulp up (how far the
+   reference's own result moves under a last-bit change of its libm's pow -- the tests'
+   spread shadow, pyoracle _Spread).  0 (default) is the reference. */
+static int g_pow_mode = 0;
+void orc_set_pow_mode(int m) { g_pow_mode = m; }
+static double cr_pow(double x, int n) {
+  const double h = x * x, l = fma(x, x, -h);
+  if (n == 2) return h;
+  if (n == 3) {
+    const double p = x * h, e = fma(x, h, -p);
+    return p + fma(x, l, e);
+  }
+  const double q = h * h, t = fma(2.0 * h, l, fma(h, h, -q));
+  if (n == 4) return q + t;
+  const double p = x * q, e = fma(x, q, -p);
+  return p + fma(x, t, e);
+}
+static double qpow(double x, int n) {
+  if (g_pow_mode == 1) return cr_pow(x, n);
+  const double y = pow(x, n);
+  if (g_pow_mode == 2 && n > 2 && y > 0.0) return nextafter(y, INFINITY);
+  return y;
+}
+
 double orc_kernel_quintic3d(double r) {
   const double norm3d = 0.0716197243913529;
   const double s = 3.0 * r;
-  if (s < 1.0) return norm3d * (pow(3 - s, 5) - 6 * pow(2 - s, 5) + 15 * pow(1 - s, 5));
-  if (s < 2.0) return norm3d * (pow(3 - s, 5) - 6 * pow(2 - s, 5));
-  if (s < 3.0) return norm3d * pow(3 - s, 5);
+  if (s < 1.0) return norm3d * (qpow(3 - s, 5) - 6 * qpow(2 - s, 5) + 15 * qpow(1 - s, 5));
+  if (s < 2.0) return norm3d * (qpow(3 - s, 5) - 6 * qpow(2 - s, 5));
+  if (s < 3.0) return norm3d * qpow(3 - s, 5);
   return 0.0;
 }
 
 double orc_kernel_quintic2d(double r) {
   const double norm2d = 0.04195297663091802;
   const double s = 3.0 * r;
-  if (s < 1.0) return norm2d * (pow(3 - s, 5) - 6 * pow(2 - s, 5) + 15 * pow(1 - s, 5));
-  if (s < 2.0) return norm2d * (pow(3 - s, 5) - 6 * pow(2 - s, 5));
-  if (s < 3.0) return norm2d * pow(3 - s, 5);
+  if (s < 1.0) return norm2d * (qpow(3 - s, 5) - 6 * qpow(2 - s, 5) + 15 * qpow(1 - s, 5));
+  if (s < 2.0) return norm2d * (qpow(3 - s, 5) - 6 * qpow(2 - s, 5));
+  if (s < 3.0) return norm2d * qpow(3 - s, 5);
   return 0.0;
 }
 
 /* Test aid (never the reference's arithmetic): orc_set_quintic_factored(1) evaluates dW/ds
    in the factored form -5 (3-s)^4 + 30 (2-s)^4 - 75 (1-s)^4, which is the same polynomial
    without the expanded form's cancellation near the pieces' ends (s -> 3: terms ~400 summing
-   to ~1e-4).  The reference's own colour gradients and multiphase forces carry that
-   cancellation's rounding (up to ~1e-10 relative on small elements); the tests' elementwise
-   bar takes its size from a shadow run in this mode (pyoracle _Spread). */
+   to ~1e-4); tools/cg_probe.py compares the forms. */
 static int g_quintic_factored = 0;
 void orc_set_quintic_factored(int on) { g_quintic_factored = on; }
 
@@ -567,9 +592,9 @@ static double dw_quintic_poly(double s) {
                  c = s < 1.0 ? 1.0 - s : 0.0;
     return -5 * (a * a) * (a * a) + 30 * (b * b) * (b * b) - 75 * (c * c) * (c * c);
   }
-  if (s < 1) return -50 * pow(s, 4) + 120 * pow(s, 3) - 120 * s;
-  if (s < 2) return 25 * pow(s, 4) - 180 * pow(s, 3) + 450 * pow(s, 2) - 420 * s + 75;
-  if (s < 3.0) return -5 * pow(s, 4) + 60 * pow(s, 3) - 270 * pow(s, 2) + 540 * s - 405;
+  if (s < 1) return -50 * qpow(s, 4) + 120 * qpow(s, 3) - 120 * s;
+  if (s < 2) return 25 * qpow(s, 4) - 180 * qpow(s, 3) + 450 * qpow(s, 2) - 420 * s + 75;
+  if (s < 3.0) return -5 * qpow(s, 4) + 60 * qpow(s, 3) - 270 * qpow(s, 2) + 540 * s - 405;
   return 0.0;
 }
 

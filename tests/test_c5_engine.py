@@ -127,3 +127,57 @@ def test_engine_c5_local_order(gpu, sph_amd, sortfreq, binsize):
         eng.run(1)
         _compare(eng, ref)
     assert ref.ninserted >= 3
+
+
+@pytest.mark.gpu
+def test_engine_c5_read_order_differs_from_tags(gpu, sph_amd):
+    """LAMMPS' initial local order is the read order (data-file lines), not tag order: the
+    atoms handed to set_atoms in a permuted order with their tags set (sph_engine_set_tags)
+    -- the engine starts its local-order index at that read order (set_atoms), the oracle
+    its local lists (MpRefRun read_order).  Atom::sort at setup keeps the read order within a
+    bin (stable), so the candidates meet the draws in an order that depends on it.  (Parity
+    with LAMMPS itself is unpinned here: the oracle restates the order bookkeeping.)"""
+    from c5_util import mp_engine, mp_state
+    s = bubble_system(10)
+    ph = dataclasses.replace(bubble_physics(10, prob=0.5, Tt=-1.0), sortfreq=1000)
+    perm = np.random.default_rng(11).permutation(s.n).astype(np.int32)
+    ref = po.MpRefRun(s, ph, spread=True, read_order=perm)
+    ref.setup()
+    eng = mp_engine(sph_amd, s, ph, sel=perm)
+    eng.setup()
+
+    def cmp():
+        g = mp_state(eng)
+        o = np.argsort(g["tag"])   # (local order -> tag order)
+        g = {k: (v[o] if isinstance(v, np.ndarray) and v.shape[:1] == o.shape else v)
+             for k, v in g.items()}
+        assert g["x"].shape[0] == ref.s.n and g["ninserted"] == ref.ninserted
+        assert np.array_equal(g["type"], ref.s.type)
+        check_fields(g, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), TOL)
+
+    cmp()
+    for _ in range(5):
+        ref.run(1)
+        eng.run(1)
+        cmp()
+    assert ref.ninserted >= 2
+    # the same atoms read in tag order draw a different set of insertions
+    ref2 = po.MpRefRun(s, ph)
+    ref2.setup()
+    ref2.run(5)
+    assert ref2.ninserted != ref.ninserted or not np.array_equal(ref2.s.x, ref.s.x)
+
+
+@pytest.mark.gpu
+def test_phase_change_after_setup_rejected(gpu, sph_amd):
+    """fix phase_change is armed before setup (its local-order bookkeeping starts at
+    set_atoms): arming it afterwards is an error, not a silent wrong order."""
+    from c5_util import mp_engine
+    s = bubble_system(8)
+    ph = bubble_physics(8, prob=0.5, Tt=-1.0)
+    eng = mp_engine(sph_amd, s, dataclasses.replace(ph, pc=None))
+    eng.setup()
+    p = ph.pc
+    with pytest.raises(sph_amd.HipError, match="before sph_engine_setup"):
+        eng.phase_change(p["Tc"], p["Tt"], p["Hwv"], p["dr"], p["to_mass"], p["cutoff"],
+                         p["from_type"], p["to_type"], seed=p["seed"], prob=p.get("prob", 0.0))

@@ -1,0 +1,179 @@
+"""BASELINE.json configs C4 and C5 at their own sizes, in their 2x2x2 decomposed form, on the
+one GPU of the test box (RCCL refuses two ranks on one device, so the eight bricks exchange
+through a LocalWorld: one engine per brick in this process, one host thread each, the same
+Transport calls in the same order as over RCCL -- comm_brick.cpp:444-506, 573-864; RCCL
+itself has still moved no byte between two ranks).
+
+* C4: 200^3 = 8M particles of the C2 physics (bench.py's weak-scaling lattice, a 100^3 share
+  per brick, started at rest) as 2x2x2 bricks against ONE brick holding all 8M, after setup +
+  11 steps (a rebuild at step 10 with the exchange across the brick faces): from rest C2's
+  physics does not depend on the decomposition except through summation order, so neighbour
+  counts must agree bit for bit per atom and every field at 1e-10 normwise (the single-brick
+  run is itself pinned to the oracle at 1M, test_gpu_fullsize.py).  With velocities it does:
+  the reference's step-0 force call reads the ghosts' vest as packed at borders(), before
+  FixMeso::setup_pre_force sets it (verlet.cpp:100-118), so a ghost of a neighbouring brick
+  carries a stale vest where one process sees the owned atom's (test_gpu_bricks.py's
+  docstring; tools/c4_diag.py shows the step-0 forces differ exactly at the brick faces).
+* C5: 159^3 = 4.02M particles of the bubble_growth stack with fix phase_change (bench.py's
+  C5 geometry) as 2x2x2 bricks: the reference's result depends on the decomposition (every
+  rank its own random stream), so the invariants -- every tag owned exactly
+  once, tags of created atoms contiguous after the initial ones, insertions summed over the
+  ranks, every atom inside its brick, mass bookkeeping -- at full size, and fields against
+  the oracle's per-rank emulation (pyoracle.MpRefRun(procgrid=(2, 2, 2))) at 32^3, the
+  largest the test budget takes.
+"""
+import importlib.util
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle as po
+from c5_util import bricks_step, mp_bricks, mp_collect
+from conftest import check_fields, elem_rel_err, record_parity, rel_err
+from scenarios import bubble_physics, bubble_system
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+bench = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(bench)
+
+PG = (2, 2, 2)
+
+
+def _by_tag(g, counts, n, out=None):
+    """scatter one engine's owned atoms (local order) into tag-ordered arrays"""
+    tags = g["tag"]
+    if out is None:
+        out = {"seen": np.zeros(n, np.int32), "counts": np.zeros(n, np.int32)}
+    out["seen"][tags] += 1
+    out["counts"][tags] = counts
+    for k, v in g.items():
+        if k == "tag" or not isinstance(v, np.ndarray) or v.shape[:1] != tags.shape:
+            continue
+        if k not in out:
+            out[k] = np.zeros((n,) + v.shape[1:], v.dtype)
+        out[k][tags] = v
+    return out
+
+
+def test_c4_8m_bricks_match_one_brick(gpu, sph_amd):
+    n = 100
+    parts = [bench.brick_lattice(n, PG, r) for r in range(8)]
+    N = sum(p[0].shape[0] for p in parts)
+    assert N == 8_000_000
+    tags = np.concatenate([p[6] for p in parts])
+    order = np.argsort(tags)
+    assert np.array_equal(tags[order], np.arange(N))
+    for p in parts:   # (at rest: see the module docstring)
+        p[1][:] = 0.0
+    glob = [np.concatenate([p[k] for p in parts])[order] for k in range(6)]
+    steps = 11
+    # one brick holding the whole 200^3 box (tags = set_atoms order)
+    e1 = sph_amd.Engine(bench.c2_config(sph_amd, 2 * n))
+    e1.set_atoms(*glob)
+    e1.setup()
+    e1.run(steps)
+    one = e1.get_atoms()
+    one_counts = e1.neighbor_counts()
+    assert e1.stats()["staged"] == 1
+    e1.close()
+    # 2x2x2 bricks, a 100^3 share each (bench.py --gpus 8 --scaling weak's decomposition)
+    world = sph_amd.LocalWorld(8)
+    engines = []
+    for r, p in enumerate(parts):
+        eng = sph_amd.Engine(bench.c2_config(sph_amd, n, PG, r))
+        eng.set_atoms(*p[:6])
+        eng.set_tags(p[6])
+        eng.comm_local(world, r)
+        engines.append(eng)
+    bricks_step(engines, lambda e: e.setup())
+    bricks_step(engines, lambda e: e.run(steps))
+    out = None
+    for eng in engines:
+        out = _by_tag(eng.get_atoms(), eng.neighbor_counts(), N, out)
+        assert eng.stats()["staged"] == 1
+    assert (out["seen"] == 1).all(), "every atom owned by exactly one brick"
+    for eng in engines:
+        eng.close()
+    assert np.array_equal(out["counts"], one_counts), "neighbour counts per atom"
+    for k in ("x", "v", "rho", "e", "f", "drho", "de"):
+        record_parity(k, out[k], one[k])
+        assert rel_err(out[k], one[k]) < 1e-10, (k, rel_err(out[k], one[k]))
+    for k in ("x", "v", "rho", "e"):  # (well conditioned: per element too)
+        assert elem_rel_err(out[k], one[k]) < 1e-10, (k, elem_rel_err(out[k], one[k]))
+
+
+def test_c5_4m_bricks_invariants(gpu, sph_amd):
+    n = 159
+    x, v, t, rho, e, cv, rmass = bench.c5_system(n)
+    mp, dt, pc = bench.c5_physics(n)
+    N0 = x.shape[0]
+    owner = bench.brick_of(x, [0.0] * 3, [1.0] * 3, PG)
+    world = sph_amd.LocalWorld(8)
+    engines = []
+    for r in range(8):
+        sel = np.nonzero(owner == r)[0]
+        cfg = sph_amd.make_config(3, 2, [0.0] * 3, [1.0] * 3, [1, 1, 1], [0.0, 1.0, 1.0], 0.0,
+                                  dt, neigh_every=1, mp=mp, procgrid=PG, rank=r)
+        eng = sph_amd.Engine(cfg)
+        eng.set_atoms(x[sel], v[sel], t[sel], rho[sel], e[sel], cv[sel])
+        eng.set_atoms_multiphase(rmass[sel], cv[sel])
+        eng.set_tags(sel.astype(np.int32))
+        eng.phase_change(pc["Tc"], pc["Tt"], pc["Hwv"], pc["dr"], pc["to_mass"], pc["cutoff"],
+                         pc["from_type"], pc["to_type"], nevery=pc["nevery"], seed=pc["seed"],
+                         prob=pc["prob"])
+        eng.comm_local(world, r)
+        engines.append(eng)
+    m0 = float(rmass.sum())
+    bricks_step(engines, lambda e: e.setup())
+    steps = 6
+    bricks_step(engines, lambda e: e.run(steps))
+    per_rank = [int(eng.get_atoms_multiphase()["ninserted"]) for eng in engines]
+    nins = sum(per_rank)
+    N = N0 + nins
+    out = mp_collect(engines, N)   # (asserts every tag in [0, N) owned exactly once)
+    assert out["ninserted"] == nins
+    assert nins > 0, "no insertion in the steps run"
+    # the created atoms: to_type, to_mass, tags N0 .. N - 1 (tag_extend rank by rank)
+    assert (out["type"][N0:] == pc["to_type"]).all()
+    assert (out["rmass"][N0:] == pc["to_mass"]).all()
+    for r, eng in enumerate(engines):
+        xr = eng.get_atoms()["x"]
+        assert (bench.brick_of(xr, [0.0] * 3, [1.0] * 3, PG) == r).all(), r
+    # mass: every created atom carries to_mass and its donors give up to_mass between them;
+    # donations to a ghost slot a created atom has overwritten are dropped, as the reference
+    # drops them (sph_pc.h, fix_phase_change.cpp:193) -- the only way mass can go
+    m1 = float(out["rmass"].sum())
+    defect = m0 + pc["to_mass"] * nins - m1
+    print(f"C5 4.02M 2x2x2: insertions per rank {per_rank}, total {nins}; mass defect "
+          f"{defect:.3e} ({defect / (pc['to_mass'] * nins):.3e} of the inserted mass)")
+    assert -1e-12 * m0 <= defect <= pc["to_mass"] * nins
+    assert np.isfinite(out["f"]).all() and np.isfinite(out["de"]).all()
+    for eng in engines:
+        eng.close()
+
+
+def test_c5_bricks_vs_oracle_32(gpu, sph_amd):
+    """C5 2x2x2 bricks at 32^3 (32,768 atoms) against MpRefRun(procgrid=(2, 2, 2)): types,
+    insertions and neighbour counts exact, fields at conftest.check_fields' bar."""
+    s = bubble_system(32)
+    ph = bubble_physics(32, prob=0.5, Tt=-1.0)
+    ref = po.MpRefRun(s, ph, procgrid=PG, spread=True)
+    ref.setup()
+    owner = po.brick_owner(s, s.x, PG)
+    world, engines = mp_bricks(sph_amd, s, ph, PG, owner)
+    bricks_step(engines, lambda e: e.setup())
+    for step in range(4):
+        if step:
+            ref.run(1)
+            bricks_step(engines, lambda e: e.run(1))
+        out = mp_collect(engines, ref.s.n)
+        assert out["ninserted"] == ref.ninserted
+        assert np.array_equal(out["type"], ref.s.type)
+        assert np.array_equal(out["counts"], ref.numneigh_full())
+        check_fields(out, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), 1e-10)
+    assert ref.ninserted >= 2
+    for eng in engines:
+        eng.close()

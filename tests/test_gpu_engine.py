@@ -231,3 +231,24 @@ def test_timing_classes(gpu, sph_amd):
     eng.sync()
     st = eng.stats()
     assert st["ms_integrate"] > 0
+
+
+def test_wide_union_takes_the_row_path(gpu, sph_amd):
+    """A block union too large for the rho / inner passes' LDS image (8000 atoms, every pair
+    within the cutoff, > 160 KiB at 24 B per slot): the block build reports the overflow and
+    the step runs on the row path (before, the rho pass's launch failed once a union passed
+    ~6.8k atoms), with parity as everywhere."""
+    s = c2_system(20)
+    s.periodic = (0, 0, 0)
+    s.boxlo = s.boxlo - 2.0
+    s.boxhi = s.boxhi + 2.0
+    ph = po.c2_physics(40.0)
+    ref = po.RefRun(s, ph, spread="lean")
+    ref.setup()
+    ref.run(1)
+    eng = engine_for(sph_amd, s, ph)
+    eng.setup()
+    eng.run(1)
+    assert eng.stats()["staged"] == 0
+    assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
+    compare(eng, ref, path=1)

@@ -1141,6 +1141,9 @@ def main():
                     help="one GPU: route the periodic self swaps through a one-rank RCCL "
                          "communicator (send/recv to itself) -- the multi-GPU halo path's cost "
                          "without the xGMI transfer")
+    ap.add_argument("--overlap", action="store_true",
+                    help="bricks / loopback: interior blocks' (rows') pair passes on a second "
+                         "stream while the halos move (sph_engine_tune SPH_TUNE_OVERLAP)")
     ap.add_argument("--transport", choices=["rccl", "ipc", "ipc-host"], default="rccl",
                     help="N > 1: rccl = one rank per GPU over RCCL/xGMI (default); ipc / "
                          "ipc-host = the node-local process world (hipIpc device outboxes / "
@@ -1215,6 +1218,8 @@ def main():
                     else "single GPU") if world == 1 else
                    f"spatial decomposition {pg[0]}x{pg[1]}x{pg[2]}, {transport_name(args)} halo exchange + "
                    "migration, one rank per GPU")
+    if args.overlap:
+        parallelism += ", interior blocks' pair passes overlapped with the halo exchanges"
     base = {
         "metric": "particle-steps/s + achieved HBM GB/s, 1M-particle taitwater+rhosum, 1/2/4/8 GPUs",
         "unit": "particle-steps/s",
@@ -1248,6 +1253,8 @@ def main():
     cfg = c2_config(sph, args.edge, pg, rank, strong=strong)
     cfg.kernel_path = args.path
     eng = sph.Engine(cfg, device=dev)
+    if args.overlap:
+        eng.tune(eng.TUNE_OVERLAP, 1)
     eng.set_atoms(x, v, t, rho, e, cv)
     if world > 1:
         eng.set_tags(tags)

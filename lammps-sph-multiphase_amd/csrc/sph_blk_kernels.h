@@ -1129,7 +1129,7 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
              const Coefs *__restrict__ cf, int um, const unsigned short *__restrict__ snbi,
              const int *__restrict__ icnt, const int *__restrict__ moved, int n3,
              const unsigned char *__restrict__ bperm, const int *__restrict__ uilist,
-             const int *__restrict__ uicnt) {
+             const int *__restrict__ uicnt, const int *__restrict__ blist) {
   constexpr int NTH = R * G;
   if (snbi && *moved == 0) {  // (workgroup-uniform) the inner rows are still exact
     snbr = snbi;
@@ -1141,7 +1141,8 @@ k_blk_rhosum(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt,
   __shared__ RhoPair s_c[NT1 ? 1 : NT2];
   __shared__ double s_acc[R];  // n3: the later rows' shares (k_blk_build N3)
   const int nt1 = cf->ntypes + 1;
-  const int b = (int)xcd_block(), tid = threadIdx.x;
+  // (blist: a subset of the blocks -- the interior or the boundary ones, overlap_on)
+  const int b = blist ? blist[xcd_block()] : (int)xcd_block(), tid = threadIdx.x;
   // (bperm: the block's rows in the build's length order, blk_row)
   const int row = b * R + blk_row(bperm, b * R, blk_lrow<G>(tid)), lane = blk_llane<G>(tid);
   const bool live = row < n;
@@ -1423,10 +1424,11 @@ k_blk_inner(int n, const int *__restrict__ ulist, const int *__restrict__ ucnt, 
       double gx, double gy, double gz, int um, int cq,                                        \
       const unsigned short *__restrict__ snbi, const int *__restrict__ icnt,                  \
       const int *__restrict__ moved, int n3, const unsigned char *__restrict__ bperm,         \
-      const int *__restrict__ uilist, const int *__restrict__ uicnt
+      const int *__restrict__ uilist, const int *__restrict__ uicnt,                          \
+      const int *__restrict__ blist
 #define SPH_BLK_FORCE_ARGS                                                                \
   n, ulist, ucnt, ucap, snbr, sstride, rcnt, xf, vr, ty, en, cf, fo, de, gx, gy, gz, um, cq, \
-      snbi, icnt, moved, n3, bperm, uilist, uicnt
+      snbi, icnt, moved, n3, bperm, uilist, uicnt, blist
 // (the body of the force pass; the kernels below differ only in their occupancy request)
 template <int R, int G, int U, int NCH, int VISC, int MODE, bool NT1, int EXP = 0, int AHEAD = 1>
 __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
@@ -1451,7 +1453,7 @@ __device__ __forceinline__ void blk_force_body(SPH_BLK_FORCE_PARAMS) {
   __shared__ HeatPair s_hp[(HEAT && !NT1) ? NT2 : 1];
   __shared__ double s_acc[BLK_N3_BUILT ? R * NA : 1];  // n3: the later rows' shares
   const int nt1 = cf->ntypes + 1;
-  const int b = (int)xcd_block();
+  const int b = blist ? blist[xcd_block()] : (int)xcd_block();  // (blist: a subset of blocks)
   const int tid = threadIdx.x;
   const int u = EXP == 3 ? 0 : ucnt[b];
   // the LDS image holds um union records (a multiple of 16); a larger union is walked in
@@ -1818,8 +1820,29 @@ struct BlkArgs {
   const int *icnt = nullptr, *moved = nullptr;
   bool n3 = false;      // rows built with Newton-3 inside the blocks (k_blk_build N3)
   const unsigned char *bperm = nullptr;  // the passes' row order per block (k_blk_build)
+  // a subset of the blocks (nlist ids; the pair passes only): the interior or the boundary
+  // blocks of a brick (k_blk_interior), so the interior ones run while the halos move
+  const int *blist = nullptr;
+  int nlist = 0;
   bool pre(const BlkShape &sh) const { return sstride <= BLK_NCH * sh.U * sh.G; }
 };
+
+// a block is INTERIOR when its union names no ghost (index >= nlocal; the union is in the
+// build's candidate order, so every entry is looked at: one wave per block, rebuilds only)
+static __global__ void __launch_bounds__(64)
+k_blk_interior(int nb, const int *__restrict__ ulist, const int *__restrict__ ucnt, int ucap,
+               int nlocal, unsigned char *__restrict__ fin, unsigned char *__restrict__ fbd) {
+  const int b = blockIdx.x;
+  const int u = ucnt[b];
+  const int *const ul = ulist + (size_t)b * ucap;
+  bool ghost = false;
+  for (int k = threadIdx.x; k < u; k += 64) ghost |= ul[k] >= nlocal;
+  const bool any = __any(ghost);
+  if (threadIdx.x == 0) {
+    fin[b] = any ? 0 : 1;
+    fbd[b] = any ? 1 : 0;
+  }
+}
 
 inline int blk_blocks(int n, int R) { return (n + R - 1) / R; }
 
@@ -1952,9 +1975,11 @@ inline void blk_rhosum_t(hipStream_t s, const BlkArgs &k, double4 *xf, const int
                                 : k_blk_rhosum<R, G, U, NCH, NT1, BLK_CHE / 16>;
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
-  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
+  const int nb = k.blist ? k.nlist : blk_blocks(k.n, R);
+  if (nb == 0) return;
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, xf, ty, vr, cf, k.um, k.snbi, k.icnt,
-                     k.moved, k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt);
+                     k.moved, k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt, k.blist);
 }
 template <int R, int G, int U>
 inline void blk_rhosum_s(bool nt1, hipStream_t s, const BlkArgs &k, double4 *xf, const int *ty,
@@ -1997,10 +2022,12 @@ inline void blk_force_t(hipStream_t s, const BlkArgs &k, const RowArgs &a) {
 #endif
   SPH_HIP_TRY(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds));
-  hipLaunchKernelGGL(fn, dim3(blk_blocks(k.n, R)), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
+  const int nb = k.blist ? k.nlist : blk_blocks(k.n, R);
+  if (nb == 0) return;
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(R * G), lds, s, k.n, k.ulist, k.ucnt,
                      k.ucap, k.snbr, k.sstride, k.rcnt, a.xf, a.vr, a.ty, a.en, a.cf, a.fo,
                      a.de, a.gx, a.gy, a.gz, k.umf, k.cq, k.snbi, k.icnt, k.moved,
-                     k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt);
+                     k.n3 ? 1 : 0, k.bperm, k.uilist, k.uicnt, k.blist);
 }
 
 // the inner rows of a build (k_blk_inner): same launch geometry and LDS image as rhosum

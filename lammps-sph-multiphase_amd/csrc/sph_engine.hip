@@ -124,10 +124,12 @@ static bool hil_pow2() {
   return v;
 }
 // SPH_SORT_EVERY (default 10): steps between spatial sorts of the owned atoms at rebuilds
+// (row path and the multiphase stack)
 static int sort_every() {
   static int v = study_int("SPH_SORT_EVERY", 10);
   return v;
 }
+
 // SPH_MP_TYPED (default 1): the multiphase passes take the neighbour's type from the entry
 static bool mp_typed_env() {
   static bool v = study_int("SPH_MP_TYPED", 1) != 0;
@@ -265,6 +267,7 @@ struct sph_engine {
   int64_t step = 0;
   int64_t rho_fused_step = -1;  // step whose rhosum/multiphase the list fill summed (k_neigh3 RHO)
   int64_t last_sort = 0;        // step of the last spatial sort of the owned atoms
+  bool force_sort = false;  // the next rebuild sorts (sph_engine_rebuild_passes)
   bool setup_done = false;
   bool global_tags = false;
   int last_build = 0;
@@ -1767,10 +1770,11 @@ struct sph_engine {
     if (pc && sortfreq > 0 && step >= nextsort) atom_sort();
     // (at most every sort_every() steps, as atom_modify sort Nevery: the C5 stack rebuilds
     // every step, and its rows keep their locality over a few steps of motion)
-    if (cfg.sort && (!setup_done || step == 0 || step - last_sort >= sort_every())) {
+    if (cfg.sort && (force_sort || !setup_done || step == 0 || step - last_sort >= sort_every())) {
       sort_owned();
       last_sort = step;
     }
+    force_sort = false;
     borders();
     if (cfg.sort) grow_twins();
     bin_q();
@@ -1848,10 +1852,11 @@ struct sph_engine {
   }
 
   bool overlap_on() const {
-    return multi() && overlap && !blk && use_row2() &&
-           !tight_on() && (force_mode & M_TAIT) != 0 && cfg.rhosum_nstep > 0;
+    return multi() && overlap && (blk || use_row2()) && !tight_on() &&
+           (force_mode & M_TAIT) != 0 && cfg.rhosum_nstep > 0;
   }
-  // interior rows (no ghost in the list) and boundary rows, each in row order
+  // interior rows (no ghost in the list) and boundary rows, each in row order; on the block
+  // path interior and boundary BLOCKS (no ghost in the union, k_blk_interior)
   void classify_rows() {
     const int n = nlocal;
     if (!s2) {
@@ -1860,6 +1865,19 @@ struct sph_engine {
       SPH_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
       SPH_HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
       SPH_HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    }
+    if (blk) {
+      const int nb = blk_blocks(n, blk_shape(blk_sh).R);
+      fl_in.reserve(nb > 0 ? nb : 1);
+      fl_bd.reserve(nb > 0 ? nb : 1);
+      if (nb)
+        hipLaunchKernelGGL(k_blk_interior, dim3(nb), dim3(64), 0, s, nb, ulist.p, ucnt.p,
+                           BLK_UCAP, nlocal, fl_in.p, fl_bd.p);
+      n_in = select_flagged(fl_in.p, nb, rows_in);
+      n_bd = select_flagged(fl_bd.p, nb, rows_bd);
+      SPH_REQUIRE(n_in + n_bd == nb, SPH_HIP_ERUNTIME, "block classification lost blocks");
+      ov_ready = true;
+      return;
     }
     fl_in.reserve(n > 0 ? n : 1);
     fl_bd.reserve(n > 0 ? n : 1);
@@ -1890,6 +1908,35 @@ struct sph_engine {
   // step's rhosum wrote it: ghost rho and P/rho^2 are only read after the rho halo has
   // overwritten them, so either value is harmless.
   void pair_compute_overlap() {
+    if (blk) {  // the same on the block path: interior blocks first, on s2
+      BlkArgs ka = blk_args(), ki = ka, kb = ka;
+      ki.blist = rows_in.p;
+      ki.nlist = n_in;
+      kb.blist = rows_bd.p;
+      kb.nlist = n_bd;
+      {
+        Scope t(this, T_RHO);  // (this class then includes the forward halo)
+        fork();
+        blk_rhosum(nt1(), s2, ki, xf.p, ty.p, vr.p, dc);
+        forward_multi();
+        // (the ghosts' displacement check of forward(): the interior blocks read no ghost,
+        // so whether they saw the flag before or after it is harmless)
+        if (inner && sc.x0 && nghost)
+          hipLaunchKernelGGL(k_inner_ghosts, dim3(blocks(nghost)), dim3(BLK), 0, s, nghost,
+                             nlocal, sc, xf.p);
+        blk_rhosum(nt1(), s, kb, xf.p, ty.p, vr.p, dc);
+        join();
+      }
+      {
+        Scope t(this, (force_mode & M_TAIT) ? T_TAIT : T_HEAT);  // (includes the rho halo)
+        fork();
+        blk_force(nt1(), blk_visc(), force_mode, s2, ki, row_args());
+        forward_rho_multi();
+        blk_force(nt1(), blk_visc(), force_mode, s, kb, row_args());
+        join();
+      }
+      return;
+    }
     Row2Args b = row2_args(), bi = b, bb = b;
     bi.a.n = n_in;
     bi.rows = rows_in.p;
@@ -3104,7 +3151,7 @@ int sph_engine_rebuild_passes(sph_engine *e, int n) {
   SPH_REQUIRE(e->setup_done, SPH_HIP_EINVAL, "sph_engine_rebuild_passes: call setup first");
   SPH_HIP_TRY(hipSetDevice(e->device));
   for (int k = 0; k < n; k++) {
-    e->last_sort = e->step - sort_every();  // (the full rebuild, sort included)
+    e->force_sort = true;  // (the full rebuild, sort included)
     e->rebuild();
   }
   SPH_HIP_TRY(hipGetLastError());

@@ -170,6 +170,31 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
   }
 }
 
+// one colorgradient term in the reference's own operation order and rounding
+// (pair_sph_colorgradient.cpp:151-179: e_ij = del / r, IEEE divisions, nothing contracted):
+// on the bubble lattice the reference's sums cancel pairwise to ~1e-6 of the field's largest
+// element, so a term's last bits show there (round 5: reciprocals and 1/r products moved such
+// elements by ~1e-9 relative, beyond how far the reference moves between its own builds)
+__device__ __forceinline__ void mp2_cg_term(int dim, double dx, double dy, double dz, double r,
+                                            double ih, double alpha, double sigmaj,
+                                            double sigmai, double &gx, double &gy, double &gz) {
+#pragma clang fp contract(off)
+  const double ex = dx / r, ey = dy / r;
+  double wfd;
+  if (dim == 3) {
+    wfd = (3.0 * 0.0716197243913529) * qr_dwpoly(3.0 * (r * ih));
+    wfd = wfd * ih * ih * ih * ih;
+  } else {
+    wfd = (3.0 * 0.04195297663091802) * qr_dwpoly(3.0 * (r * ih));
+    wfd = wfd * ih * ih * ih;
+  }
+  const double sigmaj2 = sigmaj * sigmaj;
+  const double dphi = -wfd * alpha / sigmaj2 * sigmai;
+  gx += dphi * ex;
+  gy += dphi * ey;
+  if (dim == 3) gz += dphi * (dz / r);
+}
+
 // colorgradient (pair_sph_colorgradient.cpp:139-181) over the same rows: records (x, sigma)
 template <int G>
 __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
@@ -218,12 +243,7 @@ __global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
       if (!(rsq < q.ccsq)) continue;
       double r, ir;
       mp2_r_ir(rsq, r, ir);
-      const double wfd = qr_dwpoly(3.0 * (r * q.cih)) * mp2_dwnorm(dim, q.cih);
-      const double sj = xj[u].w;
-      const double dphi = -wfd * q.calpha * mp_rcp(sj * sj) * sigmai * ir;
-      gx += dphi * dx;
-      gy += dphi * dy;
-      if (dim == 3) gz += dphi * dz;
+      mp2_cg_term(dim, dx, dy, dz, r, q.cih, q.calpha, xj[u].w, sigmai, gx, gy, gz);
     }
   }
   gx = group_sum<G>(gx);

@@ -110,7 +110,8 @@ __device__ __forceinline__ double qr_wpoly(double s) {
 #pragma clang fp contract(off)
   const double a = s < 3.0 ? qr_pow5(3.0 - s) : 0.0;
   const double b = s < 2.0 ? qr_pow5(2.0 - s) : 0.0;
-  const double c = s < 1.0 ? qr_pow5(1.0 - s) : 0.0;
+  double c = 0.0;
+  if (__any(s < 1.0)) c = s < 1.0 ? qr_pow5(1.0 - s) : 0.0;  // (rare: s = r / dx >= ~1)
   return (a - 6.0 * b) + 15.0 * c;
 }
 // the reference's dW/ds / norm: c4 pow(s,4) + c3 pow(s,3) + c2 pow(s,2) + c1 s + c0 with the

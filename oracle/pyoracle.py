@@ -714,6 +714,24 @@ class _Spread:
             return getattr(s, k)
         return getattr(self, k)
 
+    def build_rel(self, k):
+        """the largest elementwise relative distance (over |b| > 1e-6 ||b||inf) of field k
+        between this run and its build-variation shadows (the same source in the other
+        legitimate builds, BUILD_SO): the reference's own field-level reproducibility across
+        its builds; None without such shadows"""
+        want = np.asarray(self.field(k), dtype=np.float64).ravel()
+        if not want.size or not np.abs(want).max():
+            return None
+        m = np.abs(want) > 1e-6 * np.abs(want).max()
+        out = None
+        for a in self.alts:
+            if not a.build or a.s.n != self.s.n or not np.array_equal(a.s.type, self.s.type):
+                continue
+            b = np.asarray(a.field(k), dtype=np.float64).ravel()
+            r = float((np.abs(b[m] - want[m]) / np.abs(want[m])).max())
+            out = r if out is None else max(out, r)
+        return out
+
     def spread(self, k):
         """per-element spread of field k (None without shadow runs)"""
         if not self.alts:

@@ -98,3 +98,28 @@ def mp_collect(engines, n):
     out["ninserted"] = ninserted
     out["counts"] = counts
     return out
+
+
+def unexplained_count_diffs(got, want, x, boxlo, boxhi, cutsq, rtol=1e-13):
+    """The atoms whose neighbour counts differ (got vs want) by more than the number of their
+    pairs within rtol of the cutoff (rsq vs cutneighsq, minimum image): on the bubble's exact
+    binary lattice (32^3: dx = 1/32) ~30 pairs per atom sit exactly at the cutoff, and once
+    the atoms have moved, a last-bit difference in a position flips such a pair in or out
+    (the reference's own builds disagree on 8-35 atoms' counts at 32^3 after two steps,
+    tools/c5_bricks_diag.py / DESIGN.md 3).  Returns the tags whose difference no near-tie
+    explains."""
+    got = np.asarray(got)
+    want = np.asarray(want)
+    bad = np.nonzero(got != want)[0]
+    x = np.asarray(x, dtype=np.float64)
+    prd = np.asarray(boxhi, dtype=np.float64) - np.asarray(boxlo, dtype=np.float64)
+    out = []
+    for t in bad:
+        d = x - x[t]
+        d -= prd * np.rint(d / prd)
+        rsq = (d * d).sum(axis=1)
+        rsq[t] = np.inf
+        ties = int((np.abs(rsq - cutsq) <= rtol * cutsq).sum())
+        if abs(int(got[t]) - int(want[t])) > ties:
+            out.append(int(t))
+    return out

@@ -122,17 +122,19 @@ def _parity_test_name(request):
 
 def record_parity(k, got, want, spread=None, tol=1e-10):
     """the plain normwise error, the plain elementwise relative error over |b| > 1e-6 ||b||,
-    and the bar's ratio (elem_ratio with the oracle's spread) of one field check"""
+    and the bar's ratio (elem_ratio with the oracle's spread) of one field check; etol: the
+    elementwise tolerance the bar used (1e-10, or C5's build reproducibility)"""
     a = np.asarray(got, dtype=np.float64)
     b = np.asarray(want, dtype=np.float64)
     key = (_CURRENT["test"], k)
     row = dict(normwise=rel_err(a, b), elementwise=elem_rel_err(a, b),
-               bar_ratio=elem_ratio(a, b, spread, tol=tol), spread=spread is not None, n=int(b.size))
+               bar_ratio=elem_ratio(a, b, spread, tol=tol), spread=spread is not None,
+               etol=tol, n=int(b.size))
     old = _PARITY.get(key)
     if old is None:
         _PARITY[key] = row
     else:
-        for f in ("normwise", "elementwise", "bar_ratio"):
+        for f in ("normwise", "elementwise", "bar_ratio", "etol"):
             old[f] = max(old[f], row[f])
         old["checks"] = old.get("checks", 1) + 1
 
@@ -154,7 +156,10 @@ def pytest_sessionfinish(session, exitstatus):
                             "normwise = ||a-b||inf/||b||inf; elementwise = max |a-b|/|b| over "
                             "|b| > 1e-6 ||b||inf (no spread); bar_ratio = the elementwise bar "
                             "conftest.elem_ratio with the oracle's reordering/ulp spread (<= 1 "
-                            "passes)", worst_by_field=worst, rows=rows), fh, indent=1)
+                            "passes); etol = its elementwise tolerance: 1e-10, or for C5 the "
+                            "reference's own field-level elementwise shift between its builds "
+                            "(pyoracle _Spread.build_rel)", worst_by_field=worst, rows=rows),
+                  fh, indent=1)
 
 
 def check_fields(got, ref, fields, tol=1e-10, where=""):
@@ -162,7 +167,14 @@ def check_fields(got, ref, fields, tol=1e-10, where=""):
     the named fields of an engine state against an oracle run (RefRun / MpRefRun)"""
     for k in fields:
         want = ref.field(k)
-        record_parity(k, got[k], want, ref.spread(k), tol)
+        # C5 (MpRefRun with build shadows): the elementwise tolerance is at least the
+        # reference's own field-level reproducibility across its legitimate builds
+        # (pyoracle _Spread.build_rel, profiles/r06/fma_build_shift.json) -- the lattice's
+        # pairwise-cancelling sums make single elements as sensitive as that in the reference
+        # itself; every other config keeps 1e-10
+        br = ref.build_rel(k) if hasattr(ref, "build_rel") else None
+        etol = max(tol, br) if br is not None else tol
+        record_parity(k, got[k], want, ref.spread(k), etol)
         if np.abs(np.asarray(want)).max() == 0:
             assert rel_err(got[k], want) == 0.0, (where, k)
             continue
@@ -172,12 +184,12 @@ def check_fields(got, ref, fields, tol=1e-10, where=""):
         ntol = tol if sp is None else max(tol, SPREAD_K * float(np.abs(sp).max()) /
                                           float(np.abs(np.asarray(want)).max()))
         assert rel_err(got[k], want) < ntol, (where, k, "normwise", rel_err(got[k], want))
-        r = elem_ratio(got[k], want, sp, tol=tol)
+        r = elem_ratio(got[k], want, sp, tol=etol)
         if r > 1.0:  # (the worst element, for the record)
             a = np.asarray(got[k], dtype=np.float64).ravel()
             b = np.asarray(want, dtype=np.float64).ravel()
             m = np.abs(b) > 1e-6 * np.abs(b).max()
-            den = tol * np.abs(b)
+            den = etol * np.abs(b)
             if sp is not None:
                 den = np.maximum(den, SPREAD_K * np.asarray(sp, dtype=np.float64).ravel())
             q = np.where(m, np.abs(a - b) / np.where(den > 0, den, 1.0), 0.0)

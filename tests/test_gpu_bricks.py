@@ -264,26 +264,33 @@ def test_rccl_loopback_matches_oracle(gpu, sph_amd, moving, path):
     compare(out, ref)
 
 
-@pytest.mark.parametrize("pg", [(2, 1, 1), (2, 2, 2)])
-def test_bricks_halo_overlap(gpu, sph_amd, pg):
-    """sph_engine_tune(SPH_TUNE_OVERLAP, 1): interior rows' rhosum / force passes run on a
-    second stream while the forward and rho halos are in flight, boundary rows after them.
-    Same per-row arithmetic, so the same bar as the serial path: counts bit-exact, fields
-    within 1e-10 of the single-process oracle over rebuilds."""
-    s = at_rest(c2_system(14))
+@pytest.mark.parametrize("pg,path", [((2, 1, 1), 1), ((2, 2, 2), 1), ((2, 1, 1), 0),
+                                     ((2, 2, 2), 0)])
+def test_bricks_halo_overlap(gpu, sph_amd, pg, path):
+    """sph_engine_tune(SPH_TUNE_OVERLAP, 1): interior rows' (path 1) or interior blocks'
+    (path 0: no ghost in the block's union) rhosum / force passes run on a second stream while
+    the forward and rho halos are in flight, the boundary ones after them.  Same per-row
+    arithmetic, so the same bar as the serial path: counts bit-exact, fields within 1e-10 of
+    the single-process oracle over rebuilds."""
+    s = at_rest(c2_system(20 if path == 0 else 14))
     ph = po.c2_physics()
     ph.every = 4
     ref = po.RefRun(s, ph, spread=True)
     ref.setup()
     ref.run(9)
-    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=1, overlap=True)  # (row path)
+    out, counts, _ = run_bricks(sph_amd, s, ph, pg, 9, path=path, overlap=True)
     assert np.array_equal(counts, ref.numneigh_full())
     compare(out, ref)
+    if path == 0:
+        st = LAST_STATS[0]
+        assert st["staged"] == 1
 
 
-def test_rccl_loopback_overlap(gpu, sph_amd):
-    """The overlapped step through real RCCL send/recv (one-rank loopback), moving particles."""
-    s = c2_system(12)
+@pytest.mark.parametrize("path", [1, 0])
+def test_rccl_loopback_overlap(gpu, sph_amd, path):
+    """The overlapped step through real RCCL send/recv (one-rank loopback), moving particles
+    (the block path at 20^3: a brick with interior blocks)."""
+    s = c2_system(20 if path == 0 else 12)
     ph = po.c2_physics()
     ph.every = 4
     ref = po.RefRun(s, ph, spread=True)
@@ -293,7 +300,7 @@ def test_rccl_loopback_overlap(gpu, sph_amd):
                               neigh_every=ph.every,
                               rhosum=dict(nstep=1, cut=ph.rhosum_cut),
                               tait=dict(rho0=ph.rho0, c0=ph.c0, visc=ph.visc, cut=ph.tait_cut),
-                              kernel_path=1)
+                              kernel_path=path)
     eng = sph_amd.Engine(cfg)
     try:
         eng.set_atoms(s.x, s.v, s.type, s.rho, s.e, s.cv)

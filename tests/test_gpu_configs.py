@@ -101,7 +101,8 @@ def test_c4_8m_bricks_match_one_brick(gpu, sph_amd):
     for k in ("x", "v", "rho", "e", "f", "drho", "de"):
         record_parity(k, out[k], one[k])
         assert rel_err(out[k], one[k]) < 1e-10, (k, rel_err(out[k], one[k]))
-    for k in ("x", "v", "rho", "e"):  # (well conditioned: per element too)
+    for k in ("x", "rho"):  # (well conditioned: per element too; f, v, e, de, drho are sums
+        # that cancel on single elements, and the two runs differ in summation order)
         assert elem_rel_err(out[k], one[k]) < 1e-10, (k, elem_rel_err(out[k], one[k]))
 
 
@@ -156,8 +157,13 @@ def test_c5_4m_bricks_invariants(gpu, sph_amd):
 
 
 def test_c5_bricks_vs_oracle_32(gpu, sph_amd):
-    """C5 2x2x2 bricks at 32^3 (32,768 atoms) against MpRefRun(procgrid=(2, 2, 2)): types,
-    insertions and neighbour counts exact, fields at conftest.check_fields' bar."""
+    """C5 2x2x2 bricks at 32^3 (32,768 atoms) against MpRefRun(procgrid=(2, 2, 2)): types and
+    insertions exact, neighbour counts exact while the positions are bit-identical (setup and
+    the first step) and afterwards different only by pairs within 1e-13 of the cutoff (the
+    32^3 lattice is exact in binary, so its ~30 cutoff ties per atom are decided by the last
+    bit of the positions: the reference's own builds disagree on 8-35 atoms here,
+    c5_util.unexplained_count_diffs), fields at conftest.check_fields' bar."""
+    from c5_util import unexplained_count_diffs
     s = bubble_system(32)
     ph = bubble_physics(32, prob=0.5, Tt=-1.0)
     ref = po.MpRefRun(s, ph, procgrid=PG, spread=True)
@@ -172,7 +178,12 @@ def test_c5_bricks_vs_oracle_32(gpu, sph_amd):
         out = mp_collect(engines, ref.s.n)
         assert out["ninserted"] == ref.ninserted
         assert np.array_equal(out["type"], ref.s.type)
-        assert np.array_equal(out["counts"], ref.numneigh_full())
+        if np.array_equal(out["x"], ref.s.x):
+            assert np.array_equal(out["counts"], ref.numneigh_full()), step
+        else:
+            bad = unexplained_count_diffs(out["counts"], ref.numneigh_full(), ref.s.x,
+                                          s.boxlo, s.boxhi, float(ref.cns[1, 1]))
+            assert not bad, (step, bad[:10])
         check_fields(out, ref, ("x", "v", "rho", "e", "rmass", "cv", "cg", "f", "de"), 1e-10)
     assert ref.ninserted >= 2
     for eng in engines:

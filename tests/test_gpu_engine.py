@@ -252,3 +252,20 @@ def test_wide_union_takes_the_row_path(gpu, sph_amd):
     assert eng.stats()["staged"] == 0
     assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
     compare(eng, ref, path=1)
+
+
+def test_no_viscosity_c2(gpu, sph_amd):
+    """sph/taitwater with nu = 0 (Monaghan viscC = 0): the block pass takes its no-viscosity
+    variant (BLK_VISC_NONE) -- before, a 1e300 scale stood in for 1 / viscC, which overflowed
+    for large h or rho and left a ~1e-300 term in place of the reference's exact 0."""
+    s = c2_system(12)
+    ph = po.c2_physics()
+    ph.visc = np.zeros_like(ph.visc)
+    ref = po.RefRun(s, ph, spread=True)
+    ref.setup()
+    ref.run(12)
+    eng = engine_for(sph_amd, s, ph)
+    eng.setup()
+    eng.run(12)
+    assert np.array_equal(eng.neighbor_counts(), ref.numneigh_full())
+    compare(eng, ref, path=0)

@@ -1342,7 +1342,7 @@ def attach_pmc_traffic(out, kname, alg_bytes, world, args, fname="pmc_traffic.js
     the kernel, config and commit it was taken on.  Attached as `traffic` only when that
     record matches this run (same kernel family, single GPU, same lattice edge and steps);
     otherwise it is omitted (traffic null) rather than reported from another configuration."""
-    for rnd in ("r05", "r04", "r03", "r02"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         tj = os.path.join(ROOT, "profiles", rnd, fname)
         if not os.path.exists(tj):
             continue

@@ -884,7 +884,7 @@ k_neigh3(int nlocal, QBins q, int dim, const double4 *__restrict__ xf,
       for (int k = lane; k < pos - pos0; k += G) {
         const double rsq = s_hr[grp][k];
         const int pt = s_hp[grp][k];
-        const double w = qr_wpoly(3.0 * (sqrt(rsq) * s_rih[pt])) * s_rwn[pt];
+        const double w = qr_wpoly(3.0 * (cr_sqrt(rsq + 1e-300) * s_rih[pt])) * s_rwn[pt];
         racc += rsq < s_rcs[pt] ? w : 0.0;
       }
       __builtin_amdgcn_wave_barrier();

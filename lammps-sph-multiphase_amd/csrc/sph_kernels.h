@@ -101,6 +101,23 @@ __device__ __forceinline__ double rsq_ref(double dx, double dy, double dz) {
   return dx * dx + dy * dy + dz * dz;
 }
 
+// sqrt(x), correctly rounded for normal x > ~1e-290: LLVM's f64 sqrt sequence (a v_rsq_f64
+// seed, one Goldschmidt step, two residual corrections) without the rescaling it adds for
+// tiny arguments -- r for the quintic's s = 3 r / h, which must be the reference's sqrt(rsq)
+// to the last bit; *hh = ~0.5 / sqrt(x) from the same refinement
+__device__ __forceinline__ double cr_sqrt(double x, double *hh = nullptr) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double e = fma(-h, g, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  if (hh) *hh = h;
+  return fma(d, h, g);
+}
+
 template <int G>
 __device__ __forceinline__ double group_sum(double v) {
 #pragma unroll

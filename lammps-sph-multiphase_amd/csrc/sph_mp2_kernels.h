@@ -55,16 +55,8 @@ namespace sph {
 // huge 1/r times a zero weight instead of NaN); 1/r = 2 h from the same refinement (~1e-15
 // relative: it only scales well-conditioned products)
 __device__ __forceinline__ void mp2_r_ir(double x, double &r, double &ir) {
-  x += 1e-300;
-  const double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = 0.5 * y;
-  const double e = fma(-h, g, 0.5);
-  g = fma(g, e, g);
-  h = fma(h, e, h);
-  double d = fma(-g, g, x);
-  g = fma(d, h, g);
-  d = fma(-g, g, x);
-  r = fma(d, h, g);
+  double h;
+  r = cr_sqrt(x + 1e-300, &h);
   ir = 2.0 * h;
 }
 
@@ -160,7 +152,7 @@ __global__ void __launch_bounds__(256) k_mp2_rhosum(MpArgs a) {
       const Mp2Pair &q = pi[tj[u]];
       const double dx = xi.x - xj[u].x, dy = xi.y - xj[u].y, dz = xi.z - xj[u].z;
       const double rsq = rsq_ref(dx, dy, dz);
-      if (rsq < q.rcsq) acc += qr_wpoly(3.0 * (sqrt(rsq) * q.rih)) * mp2_wnorm(dim, q.rih);
+      if (rsq < q.rcsq) acc += qr_wpoly(3.0 * (cr_sqrt(rsq + 1e-300) * q.rih)) * mp2_wnorm(dim, q.rih);
     }
   }
   acc = group_sum<G>(acc);

@@ -263,6 +263,15 @@ __host__ __device__ __forceinline__ int img_add(int img, int k, int d) {
   const int v = img_get(img, k) + d;
   return (img & ~(0xff << (8 * k))) | ((v & 0xff) << (8 * k));
 }
+// a ghost's position from its owner's: + image * prd in each shifted dimension (k_forward's
+// arithmetic, shared with the block passes that read a ghost through its owner, BlkGhosts)
+__device__ __forceinline__ double4 img_shift(double4 x, int img, const double *prd) {
+  const int ix = img_get(img, 0), iy = img_get(img, 1), iz = img_get(img, 2);
+  if (ix) x.x = x.x + ix * prd[0];
+  if (iy) x.y = x.y + iy * prd[1];
+  if (iz) x.z = x.z + iz * prd[2];
+  return x;
+}
 
 // append the selected atoms as ghosts shifted by `shift` along `dim`
 // (comm_brick.cpp:820-860 -> atom_vec_meso.cpp:422-480 pack/unpack_border)
@@ -551,12 +560,7 @@ static __global__ void k_forward(int nghost, int nlocal, Box b, const int *__res
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nghost) return;
   const int o = gowner[g], img = gimg[g];
-  double4 x = xf[o];
-  const int ix = img_get(img, 0), iy = img_get(img, 1), iz = img_get(img, 2);
-  if (ix) x.x = x.x + ix * b.prd[0];
-  if (iy) x.y = x.y + iy * b.prd[1];
-  if (iz) x.z = x.z + iz * b.prd[2];
-  xf[nlocal + g] = x;
+  xf[nlocal + g] = img_shift(xf[o], img, b.prd);
   vr[nlocal + g] = vr[o];
   en[nlocal + g] = en[o];
 }

@@ -2265,7 +2265,7 @@ struct sph_engine {
 #define SPH_MPG(k, T, S, H)                                                                   \
   case k:                                                                                     \
     if (sym && g1)                                                                            \
-      hipLaunchKernelGGL((k_mp2_gather<8, T, S, H, false>), mp_rows(n), dim3(256), 0, s, h);  \
+      hipLaunchKernelGGL((k_mp2_gather_w4<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);      \
     else if (sym)                                                                             \
       hipLaunchKernelGGL((k_mp2_gather<8, T, S, H, true>), mp_rows(n), dim3(256), 0, s, h);   \
     else hipLaunchKernelGGL((k_mp_gather<8, T, S, H>), mp_rows(n), dim3(256), 0, s, h);       \

@@ -290,7 +290,7 @@ __device__ __forceinline__ double3 mp2_svec(int dim, const double4 &w, double3 e
 // POW = false: every gamma is 1 (bubble.lmp), the pressures are linear in rho and the pow()
 // code (and its registers) is not instantiated.
 template <int G, bool TAIT, bool SURF, bool HEAT, bool POW = true>
-__global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
+__device__ __forceinline__ void mp2_gather_body(const MpArgs &a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
   mp2_tables(a.mc, s_p, s_t, a.dim);
@@ -434,6 +434,20 @@ __global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
     if (TAIT || SURF) a.fo[i] = make_double4(fx, fy, fz, 0.0);
     if (HEAT) a.de[i] = dE;
   }
+}
+template <int G, bool TAIT, bool SURF, bool HEAT, bool POW = true>
+__global__ void __launch_bounds__(256) SPH_MP2_OCC k_mp2_gather(MpArgs a) {
+  mp2_gather_body<G, TAIT, SURF, HEAT, POW>(a);
+}
+// ... with at least four waves per SIMD (<= 128 VGPRs): the C5 stack's variant (every gamma
+// 1, all three styles) otherwise takes 138 VGPRs = 3 waves since its quintic and sqrt are
+// the reference's own (section a6); asked for 4 it keeps one 8-B value in scratch (one
+// reload per entry): gather 4.79 vs 5.00 ms per C5 step (profiles/r06/gather_w4/).  The
+// gamma != 1 variants (170-196 VGPRs) would spill 24-60 and stay on k_mp2_gather.
+template <int G, bool TAIT, bool SURF, bool HEAT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_mp2_gather_w4(MpArgs a) {
+  mp2_gather_body<G, TAIT, SURF, HEAT, false>(a);
 }
 
 // the styles are symmetric under exchanging a pair's atoms (k_mp2_gather applies): every

@@ -28,8 +28,11 @@
 namespace sph {
 
 // list entries per lane whose loads are issued together (study builds: -DSPH_MP2_NU=n)
+// (colorgradient at C5 4M, round 5: 1.362 vs 1.471 ms with 2; round 6, its terms in the
+// reference's operation order: 4 -> 120 VGPRs = 4 waves, 2 -> 96 VGPRs = 5 waves, 1.406 vs
+// 1.451 ms, profiles/r06/cg_nu/ -- the same entries per lane in the same order either way)
 #ifndef SPH_MP2_NU
-#define SPH_MP2_NU 4  // (colorgradient at C5 4M: 1.362 vs 1.471 ms with 2, profiles/r05)
+#define SPH_MP2_NU 2
 #endif
 // ... in the fused gather: one (its three records per entry; 128 VGPRs = 4 waves per SIMD
 // with gamma = 1, against 156 = 3 waves with two: 4.36 vs 4.53 ms per C5 step,
@@ -188,8 +191,14 @@ __device__ __forceinline__ void mp2_cg_term(int dim, double dx, double dy, doubl
 }
 
 // colorgradient (pair_sph_colorgradient.cpp:139-181) over the same rows: records (x, sigma)
+// study builds: -DSPH_MP2_CGWPE=n asks for at least n waves per SIMD in colorgradient
+#if defined(SPH_MP2_CGWPE) && SPH_MP2_CGWPE > 0
+#define SPH_MP2_CGOCC __attribute__((amdgpu_waves_per_eu(SPH_MP2_CGWPE)))
+#else
+#define SPH_MP2_CGOCC
+#endif
 template <int G>
-__global__ void __launch_bounds__(256) k_mp2_colorgradient(MpArgs a) {
+__global__ void __launch_bounds__(256) SPH_MP2_CGOCC k_mp2_colorgradient(MpArgs a) {
   __shared__ Mp2Pair s_p[NT2];
   __shared__ Mp2Type s_t[MAXT + 1];
   mp2_tables(a.mc, s_p, s_t, a.dim);
